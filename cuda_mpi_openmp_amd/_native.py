@@ -1,0 +1,141 @@
+"""ctypes binding of ``libmpx.so`` — the single native library (HIP kernels for
+gfx950, OpenMP CPU references, host statistics) shared with the lab CLIs.
+
+Import order matters on ROCm: PyTorch ships its own ``libamdhip64.so.7``. Loading
+torch first makes the dynamic loader resolve libmpx's ``libamdhip64.so.7``
+dependency to torch's already-loaded runtime (same SONAME), so device pointers,
+streams and contexts are shared between torch tensors and mpx kernels.
+
+The library is built in-tree (``make lib`` or ``__graft_entry__.build()``). On a
+GPU path a missing library is an error, never a silent fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded before libmpx; see module docstring)
+
+_PKG_DIR = Path(__file__).resolve().parent
+REPO_ROOT = _PKG_DIR.parent
+LIB_PATH = _PKG_DIR / "_lib" / "libmpx.so"
+
+_lib = None
+_lock = threading.Lock()
+
+c_int, c_i64, c_size, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+_dp = ctypes.POINTER(ctypes.c_double)
+_fp = ctypes.POINTER(ctypes.c_float)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "mpx_last_error": (c_char_p, []),
+    "mpx_version": (c_char_p, []),
+    "mpx_device_count": (c_int, [_ip]),
+    "mpx_device_report": (c_int, [c_int, ctypes.c_char_p, c_size]),
+    "mpx_stream_sync": (c_int, [c_vp]),
+    "mpx_vsub_f64": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "mpx_vsub_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "mpx_roberts": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "mpx_conv": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
+    "mpx_conv_direct": (
+        c_int,
+        [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
+    ),
+    "mpx_filter_lookup": (c_int, [c_char_p, _ip, _ip, _ip, _fp, _fp]),
+    "mpx_filter_name": (c_char_p, [c_int]),
+    "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
+    "mpx_classify": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp]),
+    "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "mpx_jacobi_f32": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "mpx_cpu_threads": (c_int, []),
+    "mpx_cpu_vsub_f64": (None, [c_vp, c_vp, c_vp, c_i64]),
+    "mpx_cpu_vsub_f32": (None, [c_vp, c_vp, c_vp, c_i64]),
+    "mpx_cpu_roberts": (None, [c_vp, c_vp, c_int, c_int]),
+    "mpx_cpu_conv": (None, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp]),
+    "mpx_cpu_classify": (None, [c_vp, c_i64, c_int, _dp, _dp]),
+    "mpx_cpu_jacobi_f64": (ctypes.c_double, [c_vp, c_vp, c_int, c_int, c_int, c_int]),
+}
+
+
+class MpxError(RuntimeError):
+    """A libmpx entry point returned a non-zero status."""
+
+
+def build(quiet: bool = True) -> None:
+    """Build libmpx.so in-tree with the repository Makefile (gfx950 cross-compile)."""
+    jobs = str(min(8, os.cpu_count() or 1))
+    res = subprocess.run(
+        ["make", "-C", str(REPO_ROOT), "-j", jobs, "lib"],
+        capture_output=quiet,
+        text=True,
+    )
+    if res.returncode != 0:
+        raise MpxError(f"building libmpx failed:\n{res.stdout}\n{res.stderr}")
+
+
+def lib(auto_build: bool = True) -> ctypes.CDLL:
+    """Return the loaded library, building it first if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            if not auto_build:
+                raise MpxError(f"{LIB_PATH} not built; run `make lib`")
+            build()
+        handle = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+        return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (OSError, MpxError):
+        return False
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().mpx_last_error()
+        raise MpxError(msg.decode() if msg else f"libmpx error {rc}")
+
+
+def ptr(t: "torch.Tensor") -> int:
+    return t.data_ptr()
+
+
+def stream_of(t: "torch.Tensor") -> int:
+    """hipStream_t of the current torch stream on t's device (0 for CPU)."""
+    if t.is_cuda:
+        return torch.cuda.current_stream(t.device).cuda_stream
+    return 0
+
+
+def f32_array(values) -> ctypes.Array:
+    vals = list(values)
+    return (ctypes.c_float * max(1, len(vals)))(*vals)
+
+
+def f64_array(values) -> ctypes.Array:
+    vals = list(values)
+    return (ctypes.c_double * max(1, len(vals)))(*vals)
+
+
+def i32_array(values) -> ctypes.Array:
+    vals = list(values)
+    return (ctypes.c_int * max(1, len(vals)))(*vals)

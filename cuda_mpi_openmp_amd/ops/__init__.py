@@ -1,0 +1,21 @@
+"""Operators backed by hand-written gfx950 HIP kernels (GPU tensors) and the
+OpenMP C references (CPU tensors) of libmpx."""
+
+from .classify import class_stats, classify_
+from .edge import conv, conv_rows, roberts
+from .filters import Filter, get_filter, list_filters
+from .stencil import jacobi_sweep
+from .vector import vsub
+
+__all__ = [
+    "class_stats",
+    "classify_",
+    "conv",
+    "conv_rows",
+    "roberts",
+    "Filter",
+    "get_filter",
+    "list_filters",
+    "jacobi_sweep",
+    "vsub",
+]

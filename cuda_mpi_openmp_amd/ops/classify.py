@@ -1,0 +1,62 @@
+"""lab3 operators: class statistics (host, fp64) and per-pixel Mahalanobis
+maximum-likelihood classification (reference lab3/src/main.cu:40-155)."""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native
+from .edge import check_image
+
+PATHS = {"direct": 0, "mfma": 1, "auto": 2}
+MAX_CLASSES = 32
+
+
+def class_stats(img: torch.Tensor, classes: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-class mean (nc, 3) and inverse covariance (nc, 3, 3) from (x, y) points.
+
+    Mirrors the reference host code operation for operation (unbiased
+    covariance, cofactor determinant, adjugate inverse), so a class with a
+    single point produces the same NaN/inf statistics as the reference.
+    """
+    h, w = check_image(img)
+    nc = len(classes)
+    if not 1 <= nc <= MAX_CLASSES:
+        raise ValueError(f"need 1 <= nc <= {MAX_CLASSES}")
+    host = img.detach().to("cpu").contiguous()
+    pts = [np.asarray(c, dtype=np.int64).reshape(-1, 2) for c in classes]
+    np_arr = _native.i32_array([len(p) for p in pts])
+    coords = _native.i32_array(np.concatenate(pts).reshape(-1).tolist())
+    mu = (ctypes.c_double * (3 * nc))()
+    inv = (ctypes.c_double * (9 * nc))()
+    _native.check(_native.lib().mpx_class_stats(host.data_ptr(), w, h, nc, np_arr, coords, mu, inv))
+    return np.array(mu[:], dtype=np.float64).reshape(nc, 3), np.array(inv[:], dtype=np.float64).reshape(nc, 3, 3)
+
+
+def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "auto", grid: int = 0,
+              block: int = 0) -> torch.Tensor:
+    """In place: alpha of every pixel = argmin_c (p - mu_c)^T inv_c (p - mu_c).
+
+    ``path``: ``direct`` (reference FMA chain), ``mfma`` (fp64 MFMA quadratic-form
+    GEMM with an exact fallback for near ties) or ``auto``. Every path returns
+    the same classes; CPU tensors use the OpenMP reference.
+    """
+    h, w = check_image(img)
+    mu = np.ascontiguousarray(mu, dtype=np.float64).reshape(-1)
+    inv = np.ascontiguousarray(inv, dtype=np.float64).reshape(-1)
+    nc = mu.size // 3
+    if inv.size != 9 * nc or not 1 <= nc <= MAX_CLASSES:
+        raise ValueError("mu must be (nc, 3) and inv (nc, 3, 3) with 1 <= nc <= 32")
+    mu_c = _native.f64_array(mu.tolist())
+    inv_c = _native.f64_array(inv.tolist())
+    L = _native.lib()
+    if img.is_cuda:
+        _native.check(L.mpx_classify(img.data_ptr(), h * w, nc, mu_c, inv_c, grid, block, PATHS[path],
+                                     _native.stream_of(img)))
+    else:
+        L.mpx_cpu_classify(img.data_ptr(), h * w, nc, mu_c, inv_c)
+    return img

@@ -1,0 +1,23 @@
+"""Multi-GPU tier: one process per MI355X, torch.distributed over RCCL/xGMI."""
+
+from .collectives import all_reduce_max, all_reduce_sum, broadcast_object, gather_slabs, max_over_ranks, scatter_rows
+from .dist import DistContext, context, init, shutdown
+from .halo import HaloExchange
+from .slab import Slab, max_rows_per_gpu, min_ranks_for
+
+__all__ = [
+    "all_reduce_max",
+    "all_reduce_sum",
+    "broadcast_object",
+    "gather_slabs",
+    "max_over_ranks",
+    "scatter_rows",
+    "DistContext",
+    "context",
+    "init",
+    "shutdown",
+    "HaloExchange",
+    "Slab",
+    "max_rows_per_gpu",
+    "min_ranks_for",
+]

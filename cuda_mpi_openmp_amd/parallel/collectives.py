@@ -1,0 +1,78 @@
+"""Global reductions and slab assembly over torch.distributed (RCCL on GPU).
+
+The reference's only "global reduction" is the harness's median over runs; the
+distributed tier needs real ones: a residual max for Jacobi, a max over ranks
+for step timing, a gather of output slabs for verification, and a broadcast of
+lab3 class parameters computed on one rank.
+"""
+
+from __future__ import annotations
+
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .dist import DistContext
+from .slab import Slab
+
+
+def all_reduce_max(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    if ctx.is_distributed:
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    return x
+
+
+def all_reduce_sum(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    if ctx.is_distributed:
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x
+
+
+def max_over_ranks(value: float, ctx: DistContext) -> float:
+    """Max of a host scalar over ranks (e.g. each rank's step time)."""
+    if not ctx.is_distributed:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def broadcast_object(obj: Any, ctx: DistContext, src: int = 0) -> Any:
+    if not ctx.is_distributed:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, device=ctx.device if ctx.backend == "nccl" else None)
+    return box[0]
+
+
+def gather_slabs(own: torch.Tensor, slab: Slab, ctx: DistContext, dst: int = 0) -> Optional[torch.Tensor]:
+    """Assemble every rank's owned rows into the full array on ``dst``.
+
+    Slabs differ by at most one row, so each rank pads to the largest slab and
+    a single all_gather moves everything; ``dst`` trims and concatenates.
+    """
+    if not ctx.is_distributed:
+        return own
+    maxr = max(slab.rows_of(r) for r in range(slab.world))
+    pad = torch.zeros((maxr,) + tuple(own.shape[1:]), dtype=own.dtype, device=own.device)
+    pad[: own.shape[0]] = own
+    parts: List[torch.Tensor] = [torch.empty_like(pad) for _ in range(slab.world)]
+    dist.all_gather(parts, pad)
+    if ctx.rank != dst:
+        return None
+    return torch.cat([parts[r][: slab.rows_of(r)] for r in range(slab.world)], dim=0)
+
+
+def scatter_rows(full: Optional[torch.Tensor], slab: Slab, ctx: DistContext, like: torch.Tensor,
+                 src: int = 0) -> torch.Tensor:
+    """Inverse of gather_slabs: rank ``src`` holds the full array, every rank
+    receives its owned rows (broadcast of the whole array, then slice: fine for
+    test-sized data; production runs generate slabs in place)."""
+    if not ctx.is_distributed:
+        return full[slab.row0: slab.row0 + slab.rows].clone()
+    shape = (slab.global_rows,) + tuple(like.shape[1:])
+    buf = full.to(like.device).contiguous() if ctx.rank == src else torch.empty(shape, dtype=like.dtype,
+                                                                                  device=like.device)
+    dist.broadcast(buf, src=src)
+    return buf[slab.row0: slab.row0 + slab.rows].clone()

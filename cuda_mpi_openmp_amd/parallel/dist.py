@@ -1,0 +1,98 @@
+"""Process-group bootstrap: one process per GPU over torch.distributed.
+
+On ROCm the ``nccl`` backend IS RCCL, which moves halo rows and reductions
+over the xGMI point-to-point links between MI355X GPUs. CPU runs (tests, the
+container without a GPU) use ``gloo`` with the same code path. Rendezvous comes
+from the standard torchrun environment (RANK, WORLD_SIZE, LOCAL_RANK,
+MASTER_ADDR, MASTER_PORT); there is no MPI anywhere (the reference has none
+either — its name promises MPI, its code has none: SURVEY §0).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world > 1 and dist.is_available() and dist.is_initialized()
+
+    @property
+    def up(self) -> Optional[int]:
+        """Neighbour holding the rows above this rank's slab."""
+        return self.rank - 1 if self.rank > 0 else None
+
+    @property
+    def down(self) -> Optional[int]:
+        """Neighbour holding the rows below this rank's slab."""
+        return self.rank + 1 if self.rank + 1 < self.world else None
+
+    def barrier(self) -> None:
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+
+_CTX: Optional[DistContext] = None
+
+
+def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float = 300.0) -> DistContext:
+    """Initialise (once) from the torchrun environment.
+
+    device: "cuda", "cpu" or "auto" (cuda when available). A single process
+    without RANK/WORLD_SIZE in the environment gets a world of one and no
+    process group.
+    """
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    if use_cuda:
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise RuntimeError("device='cuda' requested but no GPU is visible")
+        torch.cuda.set_device(local_rank % ndev)
+        dev = torch.device("cuda", local_rank % ndev)
+    else:
+        dev = torch.device("cpu")
+    if backend is None:
+        backend = "nccl" if use_cuda else "gloo"
+    ctx = DistContext(rank=rank, world=world, local_rank=local_rank, device=dev, backend=backend)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_cuda:
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    _CTX = ctx
+    return ctx
+
+
+def shutdown() -> None:
+    global _CTX
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
+
+
+def context() -> DistContext:
+    return _CTX if _CTX is not None else DistContext()

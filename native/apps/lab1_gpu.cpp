@@ -1,0 +1,57 @@
+// lab1 GPU program: c = a - b over fp64 vectors, stdin/stdout contract of
+// the reference.
+//
+//   benchmark personality (default build, "to_plot_hip_exe"):
+//     stdin  "<grid>\n<block>\n<n>\n<a0 .. a(n-1)>\n<b0 .. b(n-1)>"
+//     stdout "HIP execution time: <X ms>\n" then n x "%.10e "
+//     (reference lab1/src/to_plot.cu:36-40,72,82,86-88)
+//   submission personality (-DMPX_SUBMISSION, "hip_exe"):
+//     no geometry lines, fixed launch, values only (reference lab1/src/main.cu).
+// Geometry 0 0 selects the MI355X-tuned launch.
+#include <vector>
+
+#include "mpx/host.hpp"
+
+int main() {
+    using namespace mpx::host;
+    Scanner in;
+    int grid = 512, block = 512;  // reference submission launch <<<512, 512>>>
+#ifndef MPX_SUBMISSION
+    if (!in.next_int(grid) || !in.next_int(block)) {
+        std::fprintf(stderr, "[ERROR CPU] expected launch geometry <grid> <block> on stdin\n");
+        return 1;
+    }
+#endif
+    int n = 0;
+    if (!in.next_int(n) || n < 0) {
+        std::fprintf(stderr, "[ERROR CPU] expected vector size on stdin\n");
+        return 1;
+    }
+    std::vector<double> a(n), b(n), c(n);
+    for (int i = 0; i < n; ++i)
+        if (!in.next_double(a[i])) {
+            std::fprintf(stderr, "[ERROR CPU] first vector: expected %d values, got %d\n", n, i);
+            return 1;
+        }
+    for (int i = 0; i < n; ++i)
+        if (!in.next_double(b[i])) {
+            std::fprintf(stderr, "[ERROR CPU] second vector: expected %d values, got %d\n", n, i);
+            return 1;
+        }
+
+    DeviceBuffer<double> da(n), db(n), dc(n);
+    if (n) {
+        HIP_CHECK(hipMemcpy(da.get(), a.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(db.get(), b.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    }
+    const float ms = time_kernel([&] { MPX_CHECK(mpx_vsub_f64(da.get(), db.get(), dc.get(), n, grid, block, nullptr)); });
+#ifndef MPX_SUBMISSION
+    std::printf("HIP execution time: <%f ms>\n", ms);
+#else
+    (void)ms;
+#endif
+    std::fflush(stdout);
+    if (n) HIP_CHECK(hipMemcpy(c.data(), dc.get(), sizeof(double) * n, hipMemcpyDeviceToHost));
+    print_e10(c.data(), n);
+    return 0;
+}

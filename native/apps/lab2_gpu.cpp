@@ -1,0 +1,73 @@
+// lab2 GPU program: Roberts-cross edge detection (and, with MPX_LAB2_OP, any
+// filter of the KxK generalisation), stdin/stdout contract of the reference
+// (SURVEY Appendix A.2).
+//
+//   benchmark personality ("to_plot_hip_exe"):
+//     stdin  "<block_x>\n<block_y>\n<grid_x>\n<grid_y>\n<in.data>\n<out.data>"
+//     stdout "HIP execution time: <X ms>\n" ... "FINISHED!\n"
+//     (reference lab2/src/to_plot.cu:57-68,106,122,130)
+//   submission personality (-DMPX_SUBMISSION, "hip_exe"): paths only, no output
+//     lines (reference lab2/src/main.cu).
+// Geometry 0 0 0 0 selects the tuned LDS-tiled kernel. Paths are read as
+// whole tokens (no %1024s off-by-one).
+#include <string>
+#include <vector>
+
+#include "mpx/cio.h"
+#include "mpx/filters.h"
+#include "mpx/host.hpp"
+
+int main(int argc, char **argv) {
+    using namespace mpx::host;
+    std::string op = "roberts";
+    if (const char *e = std::getenv("MPX_LAB2_OP")) op = e;
+    for (int i = 1; i + 1 < argc; ++i)
+        if (std::string(argv[i]) == "--op") op = argv[i + 1];
+    const mpx_filter *flt = mpx_find_filter(op.c_str());
+    if (!flt) {
+        std::fprintf(stderr, "[ERROR CPU] unknown filter '%s'\n", op.c_str());
+        return 1;
+    }
+
+    Scanner in;
+    int bx = 0, by = 0, gx = 0, gy = 0;
+#ifndef MPX_SUBMISSION
+    if (!in.next_int(bx) || !in.next_int(by) || !in.next_int(gx) || !in.next_int(gy)) {
+        std::fprintf(stderr, "[ERROR CPU] expected block_x block_y grid_x grid_y on stdin\n");
+        return 1;
+    }
+#endif
+    std::string in_path, out_path;
+    if (!in.next_token(in_path) || !in.next_token(out_path)) {
+        std::fprintf(stderr, "[ERROR CPU] expected input and output paths on stdin\n");
+        return 1;
+    }
+    int w = 0, h = 0;
+    uint32_t *img = mpx_read_data_image(in_path.c_str(), &w, &h);
+    if (!img) return 1;
+    const size_t npix = (size_t)w * h;
+
+    DeviceBuffer<uint32_t> din(npix), dout(npix);
+    HIP_CHECK(hipMemcpy(din.get(), img, npix * 4, hipMemcpyHostToDevice));
+    const bool roberts = (op == "roberts");
+    const float ms = time_kernel([&] {
+        if (roberts)
+            MPX_CHECK(mpx_roberts(din.get(), dout.get(), w, h, bx, by, gx, gy, nullptr));
+        else
+            MPX_CHECK(mpx_conv(din.get(), dout.get(), w, w, 0, h, 0, h - 1, flt->k, flt->anchor, flt->mode, flt->wx,
+                               flt->wy, nullptr));
+    });
+    HIP_CHECK(hipMemcpy(img, dout.get(), npix * 4, hipMemcpyDeviceToHost));
+#ifndef MPX_SUBMISSION
+    std::printf("HIP execution time: <%f ms>\n", ms);
+#else
+    (void)ms;
+#endif
+    const int rc = mpx_write_data_image(out_path.c_str(), img, w, h);
+    std::free(img);
+    if (rc) return 1;
+#ifndef MPX_SUBMISSION
+    std::printf("FINISHED!\n");
+#endif
+    return 0;
+}

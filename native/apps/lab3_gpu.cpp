@@ -1,0 +1,80 @@
+// lab3 GPU program: per-pixel Mahalanobis maximum-likelihood classification,
+// stdin/stdout contract of the reference.
+//
+//   benchmark personality ("to_plot_hip_exe"):
+//     stdin  "<blocks>\n<threads>\n<in.data>\n<out.data>\n<nc>\n<np x y x y ...>\n..."
+//     stdout "HIP execution time: <X ms>\n" (reference lab3/src/to_plot.cu:76-117,174)
+//   submission personality (-DMPX_SUBMISSION, "hip_exe"): no geometry, no output line.
+// Output: the input image with alpha = class index (255 when every distance is NaN).
+// MPX_LAB3_PATH = direct (default, geometry honoured) | mfma | auto.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mpx/cio.h"
+#include "mpx/common.h"
+#include "mpx/host.hpp"
+
+int main() {
+    using namespace mpx::host;
+    Scanner in;
+    int blocks = 256, threads = 256;  // reference submission launch (lab3/src/main.cu:32-33)
+#ifndef MPX_SUBMISSION
+    if (!in.next_int(blocks) || !in.next_int(threads)) {
+        std::fprintf(stderr, "[ERROR CPU] expected <blocks> <threads> on stdin\n");
+        return 1;
+    }
+#endif
+    int path = MPX_CLS_DIRECT;
+    if (const char *e = std::getenv("MPX_LAB3_PATH")) {
+        if (!std::strcmp(e, "mfma")) path = MPX_CLS_MFMA;
+        else if (!std::strcmp(e, "auto")) path = MPX_CLS_AUTO;
+    }
+    std::string in_path, out_path;
+    if (!in.next_token(in_path) || !in.next_token(out_path)) {
+        std::fprintf(stderr, "[ERROR CPU] expected input and output paths on stdin\n");
+        return 1;
+    }
+    int w = 0, h = 0;
+    uint32_t *img = mpx_read_data_image(in_path.c_str(), &w, &h);
+    if (!img) return 1;
+    const int64_t npix = (int64_t)w * h;
+
+    int nc = 0;
+    if (!in.next_int(nc) || nc < 1 || nc > MPX_MAX_CLASSES) {
+        std::fprintf(stderr, "[ERROR CPU] expected 1 <= nc <= %d\n", MPX_MAX_CLASSES);
+        return 1;
+    }
+    std::vector<int> np(nc), coords;
+    for (int c = 0; c < nc; ++c) {
+        if (!in.next_int(np[c]) || np[c] < 1) {
+            std::fprintf(stderr, "[ERROR CPU] class %d: expected a positive point count\n", c);
+            return 1;
+        }
+        for (int i = 0; i < 2 * np[c]; ++i) {
+            int v;
+            if (!in.next_int(v)) {
+                std::fprintf(stderr, "[ERROR CPU] class %d: truncated coordinate list\n", c);
+                return 1;
+            }
+            coords.push_back(v);
+        }
+    }
+    std::vector<double> mu(3 * nc), inv(9 * nc);
+    MPX_CHECK(mpx_class_stats(img, w, h, nc, np.data(), coords.data(), mu.data(), inv.data()));
+
+    DeviceBuffer<uint32_t> dimg(npix);
+    HIP_CHECK(hipMemcpy(dimg.get(), img, npix * 4, hipMemcpyHostToDevice));
+    const float ms = time_kernel(
+        [&] { MPX_CHECK(mpx_classify(dimg.get(), npix, nc, mu.data(), inv.data(), blocks, threads, path, nullptr)); });
+    HIP_CHECK(hipMemcpy(img, dimg.get(), npix * 4, hipMemcpyDeviceToHost));
+    const int rc = mpx_write_data_image(out_path.c_str(), img, w, h);
+    std::free(img);
+    if (rc) return 1;
+#ifndef MPX_SUBMISSION
+    std::printf("HIP execution time: <%f ms>\n", ms);
+#else
+    (void)ms;
+#endif
+    return 0;
+}

@@ -1,0 +1,123 @@
+/*
+ * C ABI of libmpx.so — the one native library behind every lab CLI, the
+ * multi-GPU tools and the Python package (loaded with ctypes).
+ *
+ * Conventions
+ *   - every function returns 0 on success, a non-zero mpx error code otherwise;
+ *     mpx_last_error() returns a thread-local human readable message;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream), so a
+ *     PyTorch caller passes torch.cuda.current_stream().cuda_stream;
+ *   - GPU entry points never allocate, free or synchronise (graph-capturable);
+ *   - grid/block arguments of 0 mean "choose for MI355X" (256 CUs, wave64).
+ *
+ * The reference has no library at all (its library.cu is an empty kernel,
+ * reference library.cu:3-4); every lab re-declared its own macros.
+ */
+#ifndef MPX_CAPI_H
+#define MPX_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mpx_status {
+    MPX_OK = 0,
+    MPX_ERR_ARG = 1,
+    MPX_ERR_HIP = 2,
+    MPX_ERR_UNSUPPORTED = 3,
+    MPX_ERR_IO = 4
+};
+
+const char *mpx_last_error(void);
+const char *mpx_version(void);
+
+/* ---------------- device queries ---------------- */
+int mpx_device_count(int *count);
+/* Writes a multi-line report like the reference gpu_info (gpu_info/src/main.cu:9-16). */
+int mpx_device_report(int device, char *buf, size_t len);
+int mpx_stream_sync(void *stream);
+
+/* ---------------- lab1: element-wise vector subtraction ---------------- */
+/* c[i] = a[i] - b[i]; reference lab1/src/main.cu:22-29 */
+int mpx_vsub_f64(const double *a, const double *b, double *c, int64_t n, int grid, int block,
+                 void *stream);
+int mpx_vsub_f32(const float *a, const float *b, float *c, int64_t n, int grid, int block,
+                 void *stream);
+
+/* ---------------- lab2: Roberts cross (launch-geometry faithful) ---------------- */
+/* block (bx,by) and grid (gx,gy) exactly as the harness passes them
+ * (reference lab2/src/to_plot.cu:57-64,106). Each thread owns 4 pixels of a row. */
+int mpx_roberts(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by, int gx, int gy,
+                void *stream);
+
+/* ---------------- lab2 generalisation: KxK convolution on luminance ---------------- */
+/*
+ * Output rows [oy0, oy1) of a (possibly slab-local) image.
+ *   in/out   point at row 0 of the local slab, `pitch` pixels per row;
+ *   y_lo/y_hi are the rows (relative to row 0, may be negative / >= rows when
+ *            halo rows are resident) that input reads are clamped into;
+ *   k, anchor  window size (2..7) and its anchor (taps at y+dy-anchor);
+ *   wx, wy   k*k row-major taps (wy ignored unless mode == MPX_CONV_MAG2).
+ * Accumulation order is fixed: dy ascending, dx ascending, one fmaf per tap.
+ */
+int mpx_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
+             int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
+             void *stream);
+
+/* Generic direct (untiled, one pixel per thread) variant of mpx_conv: any
+ * anchor, naive global loads; the baseline the tiled kernel is measured against. */
+int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
+                    int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
+                    void *stream);
+
+/* Named filter table (native/include/mpx/filters.h). Returns MPX_ERR_ARG for an
+ * unknown name; wx/wy receive k*k taps (wy zero-filled for one-filter modes).
+ * mpx_filter_name(i) enumerates the table (NULL past the end). */
+int mpx_filter_lookup(const char *name, int *k, int *anchor, int *mode, float *wx, float *wy);
+const char *mpx_filter_name(int i);
+
+/* ---------------- lab3: Mahalanobis maximum-likelihood classifier ---------------- */
+/*
+ * Per-class statistics from training points (reference lab3/src/main.cu:102-152).
+ * coords holds (x, y) pairs for every class back to back; np[c] points per class.
+ * mu: nc*3, inv: nc*9 (row-major inverse covariance), computed in fp64 on the host.
+ */
+int mpx_class_stats(const uint32_t *img, int w, int h, int nc, const int *np, const int *coords,
+                    double *mu, double *inv);
+/* img[i].a = argmin_c (p - mu_c)^T inv_c (p - mu_c), in place (alpha = 255 if all NaN). */
+int mpx_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv,
+                 int grid, int block, int path, void *stream);
+
+/* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
+/*
+ * One sweep over rows [r0, r1) of a slab stored with one halo row above and
+ * below: `u`/`un` point at the first halo row, rows 1..rows are owned, the row
+ * pitch is `pitch` elements, columns 0 and cols-1 are Dirichlet boundary.
+ *   un[i][j] = 0.25*(u[i-1][j] + u[i+1][j] + u[i][j-1] + u[i][j+1])  (j in 1..cols-2)
+ * Rows listed in [r0, r1) are 1-based owned rows. When `resid` is non-NULL the
+ * kernel folds max|un-u| over the swept points into *resid (atomic max, bit
+ * pattern of a non-negative double), so callers zero it first.
+ */
+int mpx_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1,
+                   double *resid, void *stream);
+int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r1, float *resid,
+                   void *stream);
+
+/* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */
+int mpx_cpu_threads(void);
+void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n);
+void mpx_cpu_vsub_f32(const float *a, const float *b, float *c, int64_t n);
+void mpx_cpu_roberts(const uint32_t *in, uint32_t *out, int w, int h);
+void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
+                  int y_hi, int k, int anchor, int mode, const float *wx, const float *wy);
+void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv);
+double mpx_cpu_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPX_CAPI_H */

@@ -1,0 +1,230 @@
+/*
+ * CPU reference operators (see cpu_kernels.h). OpenMP pragmas are inert in the
+ * serial -O0 build (no -fopenmp), which reproduces the reference's single-thread
+ * methodology; the library build uses -O3 -fopenmp.
+ */
+#include "cpu_kernels.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpx/common.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* On x86-64 gcc only emits a hardware FMA for fmaf() inside an "fma" target
+ * clone; the default clone calls libm's correctly rounded fmaf. Both give the
+ * same bits, the clone is just faster. */
+#if defined(__GNUC__) && !defined(__clang__) && defined(__x86_64__) && !defined(MPX_NO_CLONES)
+#define MPX_FMA_CLONES __attribute__((target_clones("fma", "default")))
+#else
+#define MPX_FMA_CLONES
+#endif
+
+int mpx_cpu_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n) {
+    int64_t i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < n; ++i) c[i] = a[i] - b[i];
+}
+
+void mpx_cpu_vsub_f32(const float *a, const float *b, float *c, int64_t n) {
+    int64_t i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < n; ++i) c[i] = a[i] - b[i];
+}
+
+/* Roberts cross exactly as the reference CPU program evaluates it, including
+ * recomputing luminance four times per pixel (reference lab2/src/main.c:23-59). */
+void mpx_cpu_roberts(const uint32_t *in, uint32_t *out, int w, int h) {
+    int y;
+#pragma omp parallel for schedule(static)
+    for (y = 0; y < h; ++y) {
+        const int y1 = y + 1 < h ? y + 1 : h - 1;
+        for (int x = 0; x < w; ++x) {
+            const int x1 = x + 1 < w ? x + 1 : w - 1;
+            const uint32_t p00 = in[(int64_t)y * w + x];
+            const float y00 = mpx_luma(p00);
+            const float y10 = mpx_luma(in[(int64_t)y * w + x1]);
+            const float y01 = mpx_luma(in[(int64_t)y1 * w + x]);
+            const float y11 = mpx_luma(in[(int64_t)y1 * w + x1]);
+            const float gx = y11 - y00;
+            const float gy = y10 - y01;
+            const float g2 = gx * gx + gy * gy;
+            const float g = sqrtf(g2);
+            out[(int64_t)y * w + x] = mpx_px_gray(mpx_sat_u8(g), mpx_px_a(p00));
+        }
+    }
+}
+
+static inline float conv_finish(int mode, float gx, float gy) {
+    if (mode == MPX_CONV_MAG2) {
+        const float a = gx * gx;
+        const float b = gy * gy;
+        return sqrtf(a + b);
+    }
+    if (mode == MPX_CONV_ABS1) return fabsf(gx);
+    return gx;
+}
+
+MPX_FMA_CLONES
+static void conv_rows(const float *lum, int lum_y0, const uint32_t *in, uint32_t *out, int w,
+                      int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor, int mode,
+                      const float *wx, const float *wy) {
+    int y;
+#pragma omp parallel for schedule(static)
+    for (y = oy0; y < oy1; ++y) {
+        for (int x = 0; x < w; ++x) {
+            float ax = 0.0f, ay = 0.0f;
+            for (int dy = 0; dy < k; ++dy) {
+                const int yy = mpx_clampi(y + dy - anchor, y_lo, y_hi);
+                const float *row = lum + (int64_t)(yy - lum_y0) * w;
+                for (int dx = 0; dx < k; ++dx) {
+                    const int xx = mpx_clampi(x + dx - anchor, 0, w - 1);
+                    ax = fmaf(wx[dy * k + dx], row[xx], ax);
+                    if (mode == MPX_CONV_MAG2) ay = fmaf(wy[dy * k + dx], row[xx], ay);
+                }
+            }
+            const float g = conv_finish(mode, ax, ay);
+            out[(int64_t)y * pitch + x] = mpx_px_gray(mpx_sat_u8(g), mpx_px_a(in[(int64_t)y * pitch + x]));
+        }
+    }
+}
+
+void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
+                  int y_hi, int k, int anchor, int mode, const float *wx, const float *wy) {
+    if (oy1 <= oy0 || w <= 0) return;
+    /* luminance plane for every input row the requested outputs touch */
+    const int r0 = mpx_clampi(oy0 - anchor, y_lo, y_hi);
+    const int r1 = mpx_clampi(oy1 - 1 + (k - 1 - anchor), y_lo, y_hi);
+    const int nrows = r1 - r0 + 1;
+    float *lum = (float *)malloc(sizeof(float) * (size_t)nrows * (size_t)w);
+    if (!lum) return;
+    int r;
+#pragma omp parallel for schedule(static)
+    for (r = 0; r < nrows; ++r) {
+        const uint32_t *src = in + (int64_t)(r0 + r) * pitch;
+        float *dst = lum + (int64_t)r * w;
+        for (int x = 0; x < w; ++x) dst[x] = mpx_luma(src[x]);
+    }
+    conv_rows(lum, r0, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy);
+    free(lum);
+}
+
+/* lab3 per-pixel quadratic form, FMA chain of the reference GPU kernel
+ * (reference lab3/src/main.cu:49-72): strict '<' keeps the lowest class on
+ * ties, an all-NaN pixel keeps class -1 which is stored as 255. */
+MPX_FMA_CLONES
+void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv) {
+    int64_t i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < npix; ++i) {
+        const uint32_t p = img[i];
+        const double pr = (double)mpx_px_r(p), pg = (double)mpx_px_g(p), pb = (double)mpx_px_b(p);
+        double best = DBL_MAX;
+        int cls = -1;
+        for (int c = 0; c < nc; ++c) {
+            const double d0 = pr - mu[3 * c + 0];
+            const double d1 = pg - mu[3 * c + 1];
+            const double d2 = pb - mu[3 * c + 2];
+            const double *A = inv + 9 * c;
+            double t0 = fma(d0, A[0], 0.0), t1 = fma(d0, A[1], 0.0), t2 = fma(d0, A[2], 0.0);
+            t0 = fma(d1, A[3], t0);
+            t1 = fma(d1, A[4], t1);
+            t2 = fma(d1, A[5], t2);
+            t0 = fma(d2, A[6], t0);
+            t1 = fma(d2, A[7], t1);
+            t2 = fma(d2, A[8], t2);
+            double dist = fma(t0, d0, 0.0);
+            dist = fma(t1, d1, dist);
+            dist = fma(t2, d2, dist);
+            if (dist < best) {
+                best = dist;
+                cls = c;
+            }
+        }
+        img[i] = (p & 0x00ffffffu) | ((uint32_t)(uint8_t)cls << 24);
+    }
+}
+
+double mpx_cpu_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1) {
+    double res = 0.0;
+    int i;
+#pragma omp parallel for schedule(static) reduction(max : res)
+    for (i = r0; i < r1; ++i) {
+        const double *up = u + (int64_t)(i - 1) * pitch;
+        const double *uc = u + (int64_t)i * pitch;
+        const double *ud = u + (int64_t)(i + 1) * pitch;
+        double *o = un + (int64_t)i * pitch;
+        o[0] = uc[0];
+        o[cols - 1] = uc[cols - 1];
+        for (int j = 1; j < cols - 1; ++j) {
+            const double s = ((up[j] + ud[j]) + (uc[j - 1] + uc[j + 1])) * 0.25;
+            const double d = fabs(s - uc[j]);
+            res = d > res ? d : res;
+            o[j] = s;
+        }
+    }
+    return res;
+}
+
+/* Host statistics with the reference's exact operation order
+ * (reference lab3/src/main.cu:102-152): mean, unbiased covariance, cofactor
+ * determinant and the modular-index adjugate inverse. */
+int mpx_cpu_class_stats(const uint32_t *img, int w, int h, int nc, const int *np,
+                        const int *coords, double *mu, double *inv) {
+    const int *pts = coords;
+    for (int c = 0; c < nc; ++c) {
+        const int n = np[c];
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int i = 0; i < n; ++i) {
+            const int x = pts[2 * i], y = pts[2 * i + 1];
+            if (x < 0 || y < 0 || x >= w || y >= h) return -1;
+            const uint32_t px = img[(int64_t)y * w + x];
+            sum[0] += (double)mpx_px_r(px);
+            sum[1] += (double)mpx_px_g(px);
+            sum[2] += (double)mpx_px_b(px);
+        }
+        double avg[3] = {sum[0] / n, sum[1] / n, sum[2] / n};
+        double cov[3][3];
+        memset(cov, 0, sizeof(cov));
+        for (int i = 0; i < n; ++i) {
+            const uint32_t px = img[(int64_t)pts[2 * i + 1] * w + pts[2 * i]];
+            const double d[3] = {(double)mpx_px_r(px) - avg[0], (double)mpx_px_g(px) - avg[1],
+                                 (double)mpx_px_b(px) - avg[2]};
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    const double prod = d[a] * d[b];
+                    cov[a][b] += prod;
+                }
+        }
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) cov[a][b] /= (n - 1);
+        const double m0 = cov[1][1] * cov[2][2] - cov[2][1] * cov[1][2];
+        const double m1 = cov[1][0] * cov[2][2] - cov[1][2] * cov[2][0];
+        const double m2 = cov[1][0] * cov[2][1] - cov[1][1] * cov[2][0];
+        const double det = cov[0][0] * m0 - cov[0][1] * m1 + cov[0][2] * m2;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                const double p1 = cov[(b + 1) % 3][(a + 1) % 3] * cov[(b + 2) % 3][(a + 2) % 3];
+                const double p2 = cov[(b + 1) % 3][(a + 2) % 3] * cov[(b + 2) % 3][(a + 1) % 3];
+                inv[9 * c + 3 * a + b] = (p1 - p2) / det;
+            }
+        mu[3 * c + 0] = avg[0];
+        mu[3 * c + 1] = avg[1];
+        mu[3 * c + 2] = avg[2];
+        pts += 2 * n;
+    }
+    return 0;
+}

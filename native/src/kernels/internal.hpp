@@ -1,0 +1,54 @@
+// Internal helpers shared by the HIP kernel translation units of libmpx.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "mpx/capi.h"
+#include "mpx/common.h"
+
+namespace mpx {
+
+// MI355X (gfx950) launch constants: 256 CUs in 8 XCDs, 64-wide waves.
+constexpr int kNumCUs = 256;
+constexpr int kNumXCDs = 8;
+constexpr int kWave = 64;
+
+void set_error(const char *fmt, ...);
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch-status check used by every entry point: returns MPX_ERR_HIP with the
+// HIP message recorded for mpx_last_error().
+#define MPX_RETURN_IF_HIP_ERROR(expr)                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            ::mpx::set_error("%s:%d: %s", __FILE__, __LINE__, hipGetErrorString(_e));   \
+            return MPX_ERR_HIP;                                                         \
+        }                                                                               \
+    } while (0)
+
+#define MPX_CHECK_ARG(cond, msg)                                                        \
+    do {                                                                                \
+        if (!(cond)) {                                                                  \
+            ::mpx::set_error("invalid argument: %s", msg);                              \
+            return MPX_ERR_ARG;                                                         \
+        }                                                                               \
+    } while (0)
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md
+// T1): blocks b and b+8 share an XCD under round-robin dispatch, so give each
+// XCD a contiguous range of tiles. Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg / kNumXCDs, r = nwg % kNumXCDs;
+    const int xcd = b % kNumXCDs, k = b / kNumXCDs;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace mpx

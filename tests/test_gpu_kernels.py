@@ -1,0 +1,186 @@
+"""Numerics of the hand-written gfx950 kernels (run on a real MI355X).
+
+Each HIP kernel is compared against (a) the native CPU reference, bit for bit,
+and (b) a plain-PyTorch reference of the same op (fp32 for image ops, fp64
+for lab1/lab3/Jacobi), per the test strategy of SURVEY §4.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cuda_mpi_openmp_amd import ops
+from cuda_mpi_openmp_amd.ops import reference as ref
+
+from .helpers import LAB2_DATA, LAB2_GT, LAB3_CLASSES, LAB3_DATA, LAB3_GT, bytes_to_img, hex_bytes, img_to_bytes, rand_img, smooth_img
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [None, ((32, 32), (16, 16)), ((16, 16), (32, 32)), ((2, 2), (16, 16)), ((32, 32), (64, 64)),
+         ((16, 16), (1024, 1024)), ((64, 4), (8, 8)), ((1, 1), (1, 1))]
+
+
+@pytest.mark.parametrize("name", ["test_01", "test_02"])
+@pytest.mark.parametrize("geom", GEOMS)
+def test_roberts_ground_truth(gpu, name, geom):
+    img = bytes_to_img(hex_bytes(os.path.join(LAB2_DATA, name + ".txt")))
+    out = ops.roberts(img.to(gpu), geometry=geom)
+    torch.cuda.synchronize()
+    assert img_to_bytes(out) == hex_bytes(os.path.join(LAB2_GT, name + ".txt"))
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (1, 5), (5, 1), (3, 3), (4, 4), (17, 33), (64, 128), (129, 257), (480, 640),
+                                (1000, 1003)])
+@pytest.mark.parametrize("geom", [None, ((32, 8), (8, 8)), ((16, 16), (4, 4))])
+def test_roberts_matches_cpu_and_torch(gpu, hw, geom):
+    img = smooth_img(*hw, seed=hw[0] * 7 + hw[1])
+    gpu_out = ops.roberts(img.to(gpu), geometry=geom).cpu()
+    assert torch.equal(gpu_out, ops.roberts(img))  # native CPU, bit-exact
+    assert torch.equal(gpu_out, ref.roberts(img))  # plain torch fp32, same op order
+
+
+@pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "box3", "sharpen3", "sobel5",
+                                  "gauss5", "log5"])
+@pytest.mark.parametrize("hw", [(1, 1), (2, 7), (7, 2), (31, 129), (64, 128), (200, 300), (257, 260)])
+def test_conv_matches_cpu_exact_and_torch(gpu, filt, hw):
+    f = ops.get_filter(filt)
+    img = smooth_img(*hw, seed=11)
+    g = ops.conv(img.to(gpu), f).cpu()
+    c = ops.conv(img, f)
+    assert torch.equal(g, c)
+    d = ops.conv(img.to(gpu), f, direct=True).cpu()
+    assert torch.equal(d, c)
+    t = ref.conv(img, f)
+    diff = (g[..., :3].int() - t[..., :3].int()).abs()
+    assert int(diff.max()) <= 1
+    assert torch.equal(g[..., 3], img[..., 3])
+
+
+def test_conv_roberts_equals_roberts_kernel(gpu):
+    img = rand_img(333, 517, seed=3)
+    a = ops.conv(img.to(gpu), "roberts").cpu()
+    b = ops.roberts(img.to(gpu), geometry=((32, 8), (4, 4))).cpu()
+    assert torch.equal(a, b)
+
+
+def test_conv_custom_7x7_and_odd_anchor(gpu):
+    rng = np.random.default_rng(0)
+    f7 = ops.Filter.custom(7, rng.standard_normal(49).tolist(), rng.standard_normal(49).tolist())
+    f4 = ops.Filter.custom(4, rng.standard_normal(16).tolist(), anchor=1, mode="abs1")
+    img = smooth_img(150, 201, seed=5)
+    for f in (f7, f4):
+        assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f))
+
+
+@pytest.mark.parametrize("filt", ["roberts", "sobel5", "sobel3"])
+def test_conv_rows_slab_equals_full_image(gpu, filt):
+    """A slab with resident halo rows reproduces the full-image result."""
+    f = ops.get_filter(filt)
+    H, W = 300, 260
+    img = smooth_img(H, W, seed=9)
+    full = ops.conv(img, f)
+    for r0, r1 in ((0, 100), (100, 217), (217, 300)):
+        up = f.halo_up if r0 > 0 else 0
+        dn = f.halo_down if r1 < H else 0
+        buf = img[r0 - up: r1 + dn].contiguous().to(gpu)
+        out = torch.empty((r1 - r0, W, 4), dtype=torch.uint8, device=gpu)
+        ops.conv_rows(buf, out, f, src_row0=up, out_row0=0, oy0=0, oy1=r1 - r0, y_lo=-up, y_hi=r1 - r0 - 1 + dn)
+        assert torch.equal(out.cpu(), full[r0:r1])
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n", [0, 1, 3, 1000, 4097, 1 << 20])
+@pytest.mark.parametrize("geom", [(0, 0), (1, 32), (4, 64), (32, 128), (512, 512), (1024, 1024)])
+def test_vsub(gpu, dtype, n, geom):
+    g = torch.Generator().manual_seed(n)
+    a = (torch.rand(n, generator=g, dtype=torch.float64) * 2e100 - 1e100).to(dtype)
+    b = (torch.rand(n, generator=g, dtype=torch.float64) * 2e100 - 1e100).to(dtype)
+    if dtype == torch.float32:
+        a, b = a.clamp(-1e30, 1e30), b.clamp(-1e30, 1e30)
+    out = ops.vsub(a.to(gpu), b.to(gpu), grid=geom[0], block=geom[1]).cpu()
+    assert torch.equal(out, a - b)
+
+
+def test_vsub_unaligned_views(gpu):
+    a = torch.arange(1001, dtype=torch.float64, device=gpu)[1:]
+    b = torch.ones(1001, dtype=torch.float64, device=gpu)[1:]
+    assert torch.equal(ops.vsub(a, b).cpu(), (a - b).cpu())
+
+
+def test_classify_ground_truth(gpu):
+    img = bytes_to_img(hex_bytes(os.path.join(LAB3_DATA, "test_01_lab3.txt")))
+    mu, inv = ops.class_stats(img, LAB3_CLASSES)
+    gt = hex_bytes(os.path.join(LAB3_GT, "test_01_lab3.txt"))
+    for path in ("direct", "mfma", "auto"):
+        d = img.to(gpu)
+        ops.classify_(d, mu, inv, path=path)
+        assert img_to_bytes(d) == gt, path
+
+
+def _random_classes(img, nc, npts, seed):
+    rng = np.random.default_rng(seed)
+    h, w = img.shape[:2]
+    return [np.stack([rng.integers(0, w, npts), rng.integers(0, h, npts)], 1) for _ in range(nc)]
+
+
+@pytest.mark.parametrize("nc", [1, 2, 5, 16, 17, 32])
+@pytest.mark.parametrize("path", ["direct", "mfma"])
+def test_classify_matches_cpu(gpu, nc, path):
+    img = smooth_img(193, 211, seed=nc)
+    mu, inv = ops.class_stats(img, _random_classes(img, nc, 40, nc))
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    d = img.to(gpu)
+    ops.classify_(d, mu, inv, path=path)
+    assert torch.equal(d.cpu(), cpu)
+    t = ref.classify(img, mu, inv)
+    assert (t[..., 3] != cpu[..., 3]).float().mean() < 1e-3  # torch's summation order differs on near-ties
+
+
+def test_classify_near_ties_fall_back_exactly(gpu):
+    """Two nearly identical classes: the MFMA path must reproduce the direct chain."""
+    img = smooth_img(128, 128, seed=1)
+    pts = _random_classes(img, 1, 50, 0)[0]
+    mu, inv = ops.class_stats(img, [pts, pts, pts[:-1]])
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    d = img.to(gpu)
+    ops.classify_(d, mu, inv, path="mfma")
+    assert torch.equal(d.cpu(), cpu)
+
+
+def test_classify_single_point_class_nan(gpu):
+    """np = 1 -> zero covariance -> inf/NaN statistics; reference semantics kept."""
+    img = smooth_img(32, 32, seed=2)
+    mu, inv = ops.class_stats(img, [np.array([[0, 0]]), np.array([[1, 1], [2, 2], [5, 7]])])
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    for path in ("direct", "mfma"):
+        d = img.to(gpu)
+        ops.classify_(d, mu, inv, path=path)
+        assert torch.equal(d.cpu(), cpu)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("shape", [(3, 3), (10, 7), (66, 130), (257, 1001)])
+def test_jacobi_sweep(gpu, dtype, shape):
+    rows, cols = shape
+    g = torch.Generator().manual_seed(rows)
+    u = torch.rand((rows + 2, cols), generator=g, dtype=torch.float64)
+    un_ref = ref.jacobi(u, 1, rows + 1)
+    ud = u.to(dtype).to(gpu)
+    un = torch.zeros_like(ud)
+    res = torch.zeros(1, dtype=dtype, device=gpu)
+    ops.jacobi_sweep(ud, un, 1, rows + 1, res)
+    torch.cuda.synchronize()
+    got = un.cpu()[1:rows + 1]
+    if dtype == torch.float64:
+        assert torch.equal(got, un_ref[1:rows + 1])
+        uc = u.clone()
+        unc = torch.zeros_like(uc)
+        r_cpu = ops.jacobi_sweep(uc, unc, 1, rows + 1)
+        assert float(res.item()) == r_cpu
+    else:
+        assert torch.allclose(got.double(), un_ref[1:rows + 1], rtol=1e-6, atol=1e-6)
