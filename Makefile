@@ -47,6 +47,10 @@ $(B):
 $(B)/k_%.o: native/src/kernels/%.hip $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# the lab2 kernels keep scalar v_fmac chains: SLP packing into v_pk_fma_f32 costs
+# hazard NOPs and ~40 VGPRs (8 -> 4 waves per SIMD) for no extra FLOP rate
+$(B)/k_edge.o: HIPFLAGS += -fno-slp-vectorize
+
 $(B)/capi.o: native/src/core/capi.cpp $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -48,6 +48,8 @@ _SIGNATURES = {
         c_int,
         [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
     ),
+    "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
+    "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_vp]),
     "mpx_filter_lookup": (c_int, [c_char_p, _ip, _ip, _ip, _fp, _fp]),
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),

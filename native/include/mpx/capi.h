@@ -73,6 +73,16 @@ int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0
                     int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
                     void *stream);
 
+/* Tuning-harness entry (tools/kbench.py): kernel variants for k in {2, 5}, MAG2,
+ * whole image. kind 0 = LDS streaming kernel (p1 = rows per wave 4/8/16,
+ * p2 = tiles per workgroup, 0 = auto); kind 1 = wave-streaming kernel
+ * (p1 = rows per wave segment). fast selects the fast magnitude path. */
+int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h, int k, int kind, int p1, int p2, int fast,
+                     const float *wx, const float *wy, void *stream);
+/* Exhaustive check of the fast magnitude path over every float in [0, 65025];
+ * adds the number of disagreements with correctly rounded sqrtf to *bad_device. */
+int mpx_selftest_fast_sqrt(unsigned long long *bad_device, void *stream);
+
 /* Named filter table (native/include/mpx/filters.h). Returns MPX_ERR_ARG for an
  * unknown name; wx/wy receive k*k taps (wy zero-filled for one-filter modes).
  * mpx_filter_name(i) enumerates the table (NULL past the end). */

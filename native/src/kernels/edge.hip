@@ -12,175 +12,13 @@
 // bit: luminance and the gradient magnitude without FMA contraction (this TU
 // is compiled with -ffp-contract=off), correctly rounded sqrtf (hipcc default),
 // taps accumulated with one explicit fmaf each in (dy, dx) row-major order.
-#include "internal.hpp"
+#include <algorithm>
+
+#include "edge_kernels.hpp"
 
 namespace mpx {
+using edge::Taps;
 namespace {
-
-struct Taps {
-    float wx[MPX_MAX_K * MPX_MAX_K];
-    float wy[MPX_MAX_K * MPX_MAX_K];
-};
-
-template <int MODE>
-__device__ __forceinline__ float conv_finish(float gx, float gy) {
-    if constexpr (MODE == MPX_CONV_MAG2) {
-        const float a = gx * gx;
-        const float b = gy * gy;
-        return sqrtf(a + b);
-    } else if constexpr (MODE == MPX_CONV_ABS1) {
-        return fabsf(gx);
-    } else {
-        return gx;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Tiled KxK kernel (the tuned path).
-//   workgroup = 256 threads = 4 waves; wave `ty` owns RPT output rows, lane
-//   `tx` owns CPT = 2 adjacent columns, so a tile is 128 x (4*RPT) outputs.
-//   LDS holds the tile's luminance with a 4-column (one 16-B vector) halo on
-//   both sides and K-1 halo rows, plus the interior alpha bytes.
-//   Each lane slides down its 2-column strip keeping RPT x 2 accumulators per
-//   filter in registers, so an LDS luminance value is read by K rows' worth of
-//   FMAs without being re-read.
-// ---------------------------------------------------------------------------
-constexpr int kTX = 64;
-constexpr int kTY = 4;
-constexpr int kCPT = 2;
-constexpr int kTW = kTX * kCPT;  // 128 output columns per tile
-constexpr int kHL = 4;           // halo columns loaded on each side (vector granularity)
-constexpr int kLW = kTW + 2 * kHL;  // 136 floats per LDS row
-
-template <int K, int A, int MODE, int RPT, bool VEC>
-__global__ __launch_bounds__(256) void conv_tiled_kernel(const uint32_t *__restrict__ in,
-                                                         uint32_t *__restrict__ out, int w, int pitch,
-                                                         int oy0, int oy1, int y_lo, int y_hi,
-                                                         int tiles_x, Taps taps) {
-    constexpr int TH = kTY * RPT;
-    constexpr int LH = TH + K - 1;
-    constexpr int NVROW = kLW / 4;        // 16-B vectors per LDS row
-    constexpr int NVEC = LH * NVROW;      // vectors per tile
-    constexpr int ITERS = (NVEC + 255) / 256;
-    constexpr int LUM_FLOATS = LH * kLW;  // multiple of 4 -> alpha region stays 16-B aligned
-    static_assert(A <= kHL && (K - 1 - A) <= kHL, "window exceeds loaded halo");
-    __shared__ __attribute__((aligned(16))) float smem[LUM_FLOATS + TH * kTW / 4];
-    float *lum = smem;
-    uint8_t *alpha = reinterpret_cast<uint8_t *>(smem + LUM_FLOATS);
-
-    const int tid = threadIdx.x;
-    const int b = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile_y = b / tiles_x;
-    const int tile_x = b - tile_y * tiles_x;
-    const int x0 = tile_x * kTW;
-    const int y0 = oy0 + tile_y * TH;
-
-    // ---- stage: RGBA8 -> fp32 luminance (once per input pixel) ----
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int i = tid + it * 256;
-        if (NVEC % 256 == 0 || i < NVEC) {
-            const int r = i / NVROW;
-            const int v = i - r * NVROW;
-            const int gy = mpx_clampi(y0 - A + r, y_lo, y_hi);
-            const int gx = x0 - kHL + 4 * v;
-            const uint32_t *row = in + (int64_t)gy * pitch;
-            uint32_t p0, p1, p2, p3;
-            if constexpr (VEC) {
-                // w % 4 == 0: a vector is fully inside, fully left or fully right
-                const int gxc = mpx_clampi(gx, 0, w - 4);
-                const uint4 q = *reinterpret_cast<const uint4 *>(row + gxc);
-                const bool left = gx < 0, right = gx >= w;
-                p0 = right ? q.w : q.x;
-                p1 = left ? q.x : (right ? q.w : q.y);
-                p2 = left ? q.x : (right ? q.w : q.z);
-                p3 = left ? q.x : q.w;
-            } else {
-                p0 = row[mpx_clampi(gx + 0, 0, w - 1)];
-                p1 = row[mpx_clampi(gx + 1, 0, w - 1)];
-                p2 = row[mpx_clampi(gx + 2, 0, w - 1)];
-                p3 = row[mpx_clampi(gx + 3, 0, w - 1)];
-            }
-            *reinterpret_cast<float4 *>(&lum[r * kLW + 4 * v]) =
-                make_float4(mpx_luma(p0), mpx_luma(p1), mpx_luma(p2), mpx_luma(p3));
-            if (r >= A && r < A + TH && v >= 1 && v <= kTW / 4) {
-                const uint32_t av = (p0 >> 24) | ((p1 >> 24) << 8) | ((p2 >> 24) << 16) | (p3 & 0xff000000u);
-                *reinterpret_cast<uint32_t *>(&alpha[(r - A) * kTW + 4 * (v - 1)]) = av;
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- compute: sliding RPT-row window per 2-column strip ----
-    const int tx = tid & (kTX - 1);
-    const int ty = tid >> 6;  // wave index (wave-uniform)
-    const int c0 = kCPT * tx;
-    constexpr int OFF = (kHL - A) & 1;
-    constexpr int NW = (OFF + kCPT + K - 1 + 1) / 2;  // float2 reads per LDS row
-    const int wbase = c0 + kHL - A - OFF;             // even -> 8-B aligned ds_read_b64
-    constexpr bool TWO = (MODE == MPX_CONV_MAG2);
-
-    float ax[RPT][kCPT], ay[RPT][kCPT];
-#pragma unroll
-    for (int o = 0; o < RPT; ++o)
-#pragma unroll
-        for (int j = 0; j < kCPT; ++j) {
-            ax[o][j] = 0.0f;
-            ay[o][j] = 0.0f;
-        }
-
-#pragma unroll
-    for (int r = 0; r < RPT + K - 1; ++r) {
-        const float *lrow = &lum[(ty * RPT + r) * kLW + wbase];
-        float wnd[2 * NW];
-#pragma unroll
-        for (int q = 0; q < NW; ++q) {
-            const float2 t = *reinterpret_cast<const float2 *>(lrow + 2 * q);
-            wnd[2 * q] = t.x;
-            wnd[2 * q + 1] = t.y;
-        }
-#pragma unroll
-        for (int o = 0; o < RPT; ++o) {
-            const int dy = r - o;
-            if (dy < 0 || dy >= K) continue;
-#pragma unroll
-            for (int dx = 0; dx < K; ++dx) {
-                const float cx = taps.wx[dy * K + dx];
-#pragma unroll
-                for (int j = 0; j < kCPT; ++j) ax[o][j] = fmaf(cx, wnd[OFF + j + dx], ax[o][j]);
-                if constexpr (TWO) {
-                    const float cy = taps.wy[dy * K + dx];
-#pragma unroll
-                    for (int j = 0; j < kCPT; ++j) ay[o][j] = fmaf(cy, wnd[OFF + j + dx], ay[o][j]);
-                }
-            }
-        }
-    }
-
-    // ---- epilogue: magnitude, clamp, gray + source alpha, 8-B stores ----
-    const int gx0 = x0 + c0;
-#pragma unroll
-    for (int o = 0; o < RPT; ++o) {
-        const int ly = ty * RPT + o;
-        const int gy = y0 + ly;
-        if (gy >= oy1) break;
-        const uint8_t *arow = &alpha[ly * kTW + c0];
-        uint32_t v[kCPT];
-#pragma unroll
-        for (int j = 0; j < kCPT; ++j) {
-            const float g = conv_finish<MODE>(ax[o][j], ay[o][j]);
-            v[j] = mpx_px_gray(mpx_sat_u8(g), arow[j]);
-        }
-        uint32_t *orow = out + (int64_t)gy * pitch;
-        if (VEC && gx0 + 1 < w) {
-            *reinterpret_cast<uint2 *>(orow + gx0) = make_uint2(v[0], v[1]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < kCPT; ++j)
-                if (gx0 + j < w) orow[gx0 + j] = v[j];
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Generic direct kernel: any K <= MPX_MAX_K and any anchor, one output pixel
@@ -203,8 +41,7 @@ __global__ void conv_direct_kernel(const uint32_t *__restrict__ in, uint32_t *__
             if (MODE == MPX_CONV_MAG2) ay = fmaf(taps.wy[dy * k + dx], l, ay);
         }
     }
-    const float g = conv_finish<MODE>(ax, ay);
-    out[(int64_t)y * pitch + x] = mpx_px_gray(mpx_sat_u8(g), mpx_px_a(in[(int64_t)y * pitch + x]));
+    out[(int64_t)y * pitch + x] = edge::gray_px<MODE, false>(ax, ay, mpx_px_a(in[(int64_t)y * pitch + x]));
 }
 
 // ---------------------------------------------------------------------------
@@ -294,24 +131,90 @@ Taps make_taps(int k, const float *wx, const float *wy, bool two) {
     return t;
 }
 
-// rows per thread of the tiled kernel (tile height = 4 * kRPT)
+// Production tile: RPT = 8 rows per wave -> 128 x 32 output tiles.
 constexpr int kRPT = 8;
+// resident workgroups per CU the chunking targets (VGPR-limited to 4 at ~100 VGPRs)
+constexpr int kBlocksPerCU = 4;
+
+template <int K, int A, int MODE, int RPT, bool FAST>
+int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                  const Taps &taps, bool vec, hipStream_t s, int chunk_override = 0) {
+    constexpr int TH = edge::kTY * RPT;
+    const int strips = (w + edge::kTW - 1) / edge::kTW;
+    const int tiles_y = (oy1 - oy0 + TH - 1) / TH;
+    const int64_t total = (int64_t)strips * tiles_y;
+    const int64_t target = (int64_t)kNumCUs * kBlocksPerCU;
+    int chunk = chunk_override > 0 ? chunk_override : (int)std::max<int64_t>(1, (total + target - 1) / target);
+    chunk = std::min(chunk, tiles_y);
+    const int cps = (tiles_y + chunk - 1) / chunk;
+    const int64_t nblk = (int64_t)strips * cps;
+    MPX_CHECK_ARG(nblk < (int64_t)1 << 31, "image too large for one launch");
+    if (vec)
+        hipLaunchKernelGGL((edge::conv_stream_kernel<K, A, MODE, RPT, true, FAST>), dim3((unsigned)nblk), dim3(256), 0,
+                           s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_y, chunk, cps, taps);
+    else
+        hipLaunchKernelGGL((edge::conv_stream_kernel<K, A, MODE, RPT, false, FAST>), dim3((unsigned)nblk), dim3(256), 0,
+                           s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_y, chunk, cps, taps);
+    return MPX_OK;
+}
+
+// rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
+constexpr int kSegRows = 8;
+
+template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0>
+int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1) {
+    using G = edge::WaveGeom<K, A, OWX>;
+    const int strips = (w + G::OW - 1) / G::OW;
+    const int segs = (oy1 - oy0 + seg - 1) / seg;
+    const int64_t nwaves = (int64_t)strips * segs;
+    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
+    const unsigned nblk = (unsigned)((nwaves + 3) / 4);
+    if (vec)
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+    else
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+    return MPX_OK;
+}
+
+// Named filters whose taps are compiled in (zero taps disappear); selected
+// whenever the caller's taps are bit-identical to them.
+template <class F, int N>
+bool same_taps(const Taps &t) {
+    for (int i = 0; i < N; ++i)
+        if (__builtin_bit_cast(uint32_t, t.wx[i]) != __builtin_bit_cast(uint32_t, F::wx[i]) ||
+            __builtin_bit_cast(uint32_t, t.wy[i]) != __builtin_bit_cast(uint32_t, F::wy[i]))
+            return false;
+    return true;
+}
 
 template <int K, int A, int MODE>
 int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                  const Taps &taps, bool vec, hipStream_t s) {
-    constexpr int TH = kTY * kRPT;
-    const int tiles_x = (w + kTW - 1) / kTW;
-    const int tiles_y = (oy1 - oy0 + TH - 1) / TH;
-    const int64_t nblk = (int64_t)tiles_x * tiles_y;
-    MPX_CHECK_ARG(nblk < (int64_t)1 << 31, "image too large for one launch");
-    if (vec)
-        hipLaunchKernelGGL((conv_tiled_kernel<K, A, MODE, kRPT, true>), dim3((unsigned)nblk), dim3(256), 0, s,
-                           in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_x, taps);
-    else
-        hipLaunchKernelGGL((conv_tiled_kernel<K, A, MODE, kRPT, false>), dim3((unsigned)nblk), dim3(256), 0, s,
-                           in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_x, taps);
-    return MPX_OK;
+    if constexpr (K == 2 && A == 0 && MODE == MPX_CONV_MAG2) {
+        if (same_taps<edge::RobertsTaps, 4>(taps))
+            return launch_wave<K, A, MODE, true, edge::RobertsTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
+        if (same_taps<edge::Sobel5Taps, 25>(taps))
+            return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+}
+
+// Exhaustive self-test of the fast magnitude path: every float s in
+// [0, 65025] (bit patterns 0 .. 0x477E0100) must map to the same gray level as
+// the correctly rounded sqrtf. Counts mismatches into *bad.
+__global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigned long long *bad) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long nbad = 0;
+    for (uint32_t u = first + blockIdx.x * blockDim.x + threadIdx.x; u <= last && u >= first; u += stride) {
+        const float s = __builtin_bit_cast(float, u);
+        nbad += edge::mag_to_gray<true>(s) != edge::mag_to_gray<false>(s);
+    }
+    if (nbad) atomicAdd(bad, nbad);
 }
 
 template <int MODE>
@@ -340,7 +243,8 @@ int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int 
     MPX_CHECK_ARG(y_lo <= y_hi && oy0 >= 0, "bad row range");
     if (oy1 <= oy0) return MPX_OK;
     const Taps taps = make_taps(k, wx, wy, mode == MPX_CONV_MAG2);
-    const bool vec = (w % 4 == 0) && (pitch % 4 == 0) && aligned16(in) && aligned16(out) && w >= 4;
+    // 8-B pair loads/stores of the wave kernel: even width and pitch, 8-B aligned rows
+    const bool vec = (w % 2 == 0) && (pitch % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
     hipStream_t s = as_stream(stream);
     int rc;
     if (force_direct) {
@@ -410,4 +314,52 @@ extern "C" int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pit
                                int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
                                void *stream) {
     return mpx::conv_impl(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy, stream, true);
+}
+
+// Variant entry for the tuning harness (tools/kbench.py), k in {2, 5}, MAG2,
+// whole image, fast magnitude path unless fast == 0:
+//   kind 0: LDS streaming kernel, p1 = rows per wave (4, 8, 16), p2 = tiles per workgroup (0 = auto)
+//   kind 1: wave-streaming kernel, p1 = rows per wave segment
+extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h, int k, int kind, int p1, int p2,
+                                int fast, const float *wx, const float *wy, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(in && out && wx && wy && w > 0 && h > 0, "bad arguments");
+    MPX_CHECK_ARG(k == 2 || k == 5, "variant harness covers k = 2 and k = 5");
+    const Taps taps = make_taps(k, wx, wy, true);
+    hipStream_t s = as_stream(stream);
+    if (kind == 1 || kind == 2) {
+        // kind 1: runtime taps, kind 2: compiled-in taps of the named filter;
+        // p1 = segment rows; p2 >= 1000 orders waves strip-major
+        MPX_CHECK_ARG(p1 >= 1, "segment rows must be positive");
+        const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
+        const int sm = p2 >= 1000 ? 0 : 1;
+        if (k == 5) {
+            if (kind == 2)
+                return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm);
+            return fast ? launch_wave<5, 2, MPX_CONV_MAG2, true>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm)
+                        : launch_wave<5, 2, MPX_CONV_MAG2, false>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm);
+        }
+        if (kind == 2)
+            return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm);
+        return fast ? launch_wave<2, 0, MPX_CONV_MAG2, true>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm)
+                    : launch_wave<2, 0, MPX_CONV_MAG2, false>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm);
+    }
+    const bool vec = (w % 4 == 0) && aligned16(in) && aligned16(out);
+#define MPX_VAR(KK, AA, R, F)                                                                                  \
+    if (k == KK && p1 == R && (fast != 0) == F)                                                                 \
+        return launch_stream<KK, AA, MPX_CONV_MAG2, R, F>(in, out, w, w, 0, h, 0, h - 1, taps, vec, s, p2);
+    MPX_VAR(5, 2, 4, true) MPX_VAR(5, 2, 8, true) MPX_VAR(5, 2, 16, true) MPX_VAR(5, 2, 8, false)
+    MPX_VAR(2, 0, 4, true) MPX_VAR(2, 0, 8, true) MPX_VAR(2, 0, 16, true) MPX_VAR(2, 0, 8, false)
+#undef MPX_VAR
+    set_error("unsupported variant k=%d kind=%d p1=%d fast=%d", k, kind, p1, fast);
+    return MPX_ERR_ARG;
+}
+
+extern "C" int mpx_selftest_fast_sqrt(unsigned long long *bad_device, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(bad_device, "null counter");
+    hipLaunchKernelGGL(fast_sqrt_selftest_kernel, dim3(kNumCUs * 16), dim3(256), 0, as_stream(stream), 0u,
+                       0x477E0100u, bad_device);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
 }

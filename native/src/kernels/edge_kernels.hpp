@@ -1,0 +1,544 @@
+// Device code of the lab2 convolution family (included by edge.hip and by the
+// tools/kbench variant harness). See edge.hip for the design notes.
+#pragma once
+
+#include "internal.hpp"
+
+namespace mpx {
+namespace edge {
+
+struct Taps {
+    float wx[MPX_MAX_K * MPX_MAX_K];
+    float wy[MPX_MAX_K * MPX_MAX_K];
+};
+
+// Exact magnitude -> gray level: trunc(min(sqrt_rn(s), 255)) with s = gx*gx + gy*gy.
+//   FAST: hardware v_sqrt_f32 (not correctly rounded) decides the integer part
+//   whenever its result is further than kSqrtMargin from an integer; otherwise
+//   (and only then) the correctly rounded sqrtf runs. tests/test_gpu_kernels.py
+//   checks the equivalence exhaustively for every float s in [0, 65025].
+constexpr float kSqrtMargin = 1.0f / 16384.0f;  // 2^-14 = 4 ulp at 255
+
+template <bool FAST>
+__device__ __forceinline__ uint32_t mag_to_gray(float s) {
+    if constexpr (!FAST) {
+        return mpx_sat_u8(sqrtf(s));
+    } else {
+        if (s >= 65025.0f) return 255u;  // sqrt_rn is monotone and sqrt_rn(255^2) == 255
+        const float r = __builtin_amdgcn_sqrtf(s);
+        const float n = truncf(r);
+        const float fr = r - n;
+        if (fr > kSqrtMargin && fr < 1.0f - kSqrtMargin) return (uint32_t)n;
+        return mpx_sat_u8(sqrtf(s));
+    }
+}
+
+template <int MODE, bool FAST>
+__device__ __forceinline__ uint32_t finish_gray(float gx, float gy) {
+    if constexpr (MODE == MPX_CONV_MAG2) {
+        const float a = gx * gx;
+        const float b = gy * gy;
+        return mag_to_gray<FAST>(a + b);
+    } else if constexpr (MODE == MPX_CONV_ABS1) {
+        return mpx_sat_u8(fabsf(gx));
+    } else {
+        return mpx_sat_u8(gx);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Geometry shared by the tiled kernels: 256 threads = 4 waves; wave `ty`
+// owns RPT output rows of the tile, lane `tx` two adjacent columns.
+// ---------------------------------------------------------------------------
+constexpr int kTX = 64;
+constexpr int kTY = 4;
+constexpr int kCPT = 2;
+constexpr int kTW = kTX * kCPT;     // 128 output columns per tile
+constexpr int kHL = 4;              // halo columns loaded on each side (one 16-B vector)
+constexpr int kLW = kTW + 2 * kHL;  // 136 floats per LDS luminance row
+constexpr int kNVROW = kLW / 4;     // 34 vectors per row
+
+// Fetch one 16-B vector (4 pixels) of row `row` starting at column gx with
+// clamp-to-edge in x. VEC: w % 4 == 0, so the vector is entirely inside,
+// entirely left (gx < 0) or entirely right (gx >= w) of the image.
+template <bool VEC>
+__device__ __forceinline__ uint4 fetch4(const uint32_t *__restrict__ row, int gx, int w) {
+    if constexpr (VEC) {
+        const int gxc = mpx_clampi(gx, 0, w - 4);
+        const uint4 q = *reinterpret_cast<const uint4 *>(row + gxc);
+        const bool left = gx < 0, right = gx >= w;
+        uint4 p;
+        p.x = right ? q.w : q.x;
+        p.y = left ? q.x : (right ? q.w : q.y);
+        p.z = left ? q.x : (right ? q.w : q.z);
+        p.w = left ? q.x : q.w;
+        return p;
+    } else {
+        uint4 p;
+        p.x = row[mpx_clampi(gx + 0, 0, w - 1)];
+        p.y = row[mpx_clampi(gx + 1, 0, w - 1)];
+        p.z = row[mpx_clampi(gx + 2, 0, w - 1)];
+        p.w = row[mpx_clampi(gx + 3, 0, w - 1)];
+        return p;
+    }
+}
+
+__device__ __forceinline__ float4 luma4(uint4 p) {
+    return make_float4(mpx_luma(p.x), mpx_luma(p.y), mpx_luma(p.z), mpx_luma(p.w));
+}
+
+__device__ __forceinline__ uint32_t alpha4(uint4 p) {
+    return (p.x >> 24) | ((p.y >> 24) << 8) | ((p.z >> 24) << 16) | (p.w & 0xff000000u);
+}
+
+// Sliding-window compute of one tile from LDS: RPT x 2 outputs per lane, taps
+// accumulated with one fmaf each in (dy, dx) order. lum rows: tile row 0 of
+// the window at LDS row 0. Writes gray pixels through `emit(o, j, value)`.
+template <int K, int A, int MODE, int RPT, bool FAST>
+__device__ __forceinline__ void tile_compute(const float *__restrict__ lum, const Taps &taps, int tx, int ty,
+                                             uint32_t (&res)[RPT][kCPT]) {
+    constexpr int OFF = (kHL - A) & 1;
+    constexpr int NW = (OFF + kCPT + K - 1 + 1) / 2;
+    constexpr bool TWO = (MODE == MPX_CONV_MAG2);
+    const int wbase = kCPT * tx + kHL - A - OFF;
+    float ax[RPT][kCPT], ay[RPT][kCPT];
+#pragma unroll
+    for (int o = 0; o < RPT; ++o)
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j) {
+            ax[o][j] = 0.0f;
+            ay[o][j] = 0.0f;
+        }
+#pragma unroll
+    for (int r = 0; r < RPT + K - 1; ++r) {
+        const float *lrow = lum + (ty * RPT + r) * kLW + wbase;
+        float wnd[2 * NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const float2 t = *reinterpret_cast<const float2 *>(lrow + 2 * q);
+            wnd[2 * q] = t.x;
+            wnd[2 * q + 1] = t.y;
+        }
+#pragma unroll
+        for (int o = 0; o < RPT; ++o) {
+            const int dy = r - o;
+            if (dy < 0 || dy >= K) continue;
+#pragma unroll
+            for (int dx = 0; dx < K; ++dx) {
+                const float cx = taps.wx[dy * K + dx];
+#pragma unroll
+                for (int j = 0; j < kCPT; ++j) ax[o][j] = fmaf(cx, wnd[OFF + j + dx], ax[o][j]);
+                if constexpr (TWO) {
+                    const float cy = taps.wy[dy * K + dx];
+#pragma unroll
+                    for (int j = 0; j < kCPT; ++j) ay[o][j] = fmaf(cy, wnd[OFF + j + dx], ay[o][j]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < RPT; ++o)
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j) res[o][j] = finish_gray<MODE, FAST>(ax[o][j], ay[o][j]);
+}
+
+// ---------------------------------------------------------------------------
+// Streaming kernel (production path). A workgroup walks DOWN a 128-column
+// strip through `chunk` consecutive tiles of TH = 4*RPT rows:
+//   * luminance is computed once per input pixel and the K-1 window rows
+//     shared by consecutive tiles stay resident in LDS (moved to the top of
+//     the buffer) instead of being re-read from memory;
+//   * the next tile's TH new rows are fetched into registers BEFORE the
+//     current tile is computed, so HBM traffic overlaps the FMA work inside
+//     every workgroup, not only across workgroups;
+//   * workgroups of one XCD take contiguous chunk ids (xcd_remap), so strips
+//     and their neighbours' halo columns share an L2.
+// LDS: (TH+K-1) x 136 fp32 luminance + (TH+K-1) x 128 alpha bytes.
+// ---------------------------------------------------------------------------
+template <int K, int A, int MODE, int RPT, bool VEC, bool FAST>
+__global__ __launch_bounds__(256) void conv_stream_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                                                          int tiles_y, int chunk, int chunks_per_strip, Taps taps) {
+    constexpr int TH = kTY * RPT;
+    constexpr int LH = TH + K - 1;
+    constexpr int HALO = K - 1;
+    constexpr int NEWV = TH * kNVROW;   // vectors fetched per steady-state tile
+    constexpr int ITN = (NEWV + 255) / 256;
+    constexpr int LUMF = LH * kLW;      // floats; multiple of 4
+    static_assert(A <= kHL && (K - 1 - A) <= kHL, "window exceeds loaded halo");
+    static_assert(TH >= HALO, "tile shorter than the window");
+    __shared__ __attribute__((aligned(16))) float smem[LUMF + LH * kTW / 4];
+    float *lum = smem;
+    uint8_t *alpha = reinterpret_cast<uint8_t *>(smem + LUMF);
+
+    const int tid = threadIdx.x;
+    const int tx = tid & (kTX - 1);
+    const int ty = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = b / chunks_per_strip;
+    const int t0 = (b - strip * chunks_per_strip) * chunk;
+    const int t1 = min(t0 + chunk, tiles_y);
+    if (t0 >= t1) return;  // uniform per workgroup
+    const int x0 = strip * kTW;
+    const bool full_x = (x0 + kTW <= w);
+
+    // per-thread fetch slots: slot `it` covers vector i = tid + 256*it of a
+    // block of rows, i.e. row r = i / 34 and vector v = i % 34 (fixed per thread)
+    auto fetch_rows = [&](uint4 (&regs)[ITN], int gy_first, int nrows_total) {
+#pragma unroll
+        for (int it = 0; it < ITN; ++it) {  // unconditional (see conv_wave_kernel)
+            const int i = min(tid + it * 256, nrows_total * kNVROW - 1);
+            const int r = i / kNVROW;
+            const int v = i - r * kNVROW;
+            const int gy = mpx_clampi(gy_first + r, y_lo, y_hi);
+            regs[it] = fetch4<VEC>(in + (int64_t)gy * pitch, x0 - kHL + 4 * v, w);
+        }
+    };
+    auto store_rows = [&](const uint4 (&regs)[ITN], int lrow_first, int nrows_total) {
+#pragma unroll
+        for (int it = 0; it < ITN; ++it) {
+            const int i = tid + it * 256;
+            if (i < nrows_total * kNVROW) {
+                const int r = i / kNVROW;
+                const int v = i - r * kNVROW;
+                const int lr = lrow_first + r;
+                *reinterpret_cast<float4 *>(&lum[lr * kLW + 4 * v]) = luma4(regs[it]);
+                if (v >= 1 && v <= kTW / 4) *reinterpret_cast<uint32_t *>(&alpha[lr * kTW + 4 * (v - 1)]) = alpha4(regs[it]);
+            }
+        }
+    };
+
+    // ---- prologue: the whole window of the first tile (LH rows) ----
+    {
+        constexpr int ITP = (LH * kNVROW + 255) / 256;
+        uint4 pre[ITP];
+        const int ytop = oy0 + t0 * TH - A;
+#pragma unroll
+        for (int it = 0; it < ITP; ++it) {
+            const int i = min(tid + it * 256, LH * kNVROW - 1);
+            const int r = i / kNVROW;
+            const int v = i - r * kNVROW;
+            pre[it] = fetch4<VEC>(in + (int64_t)mpx_clampi(ytop + r, y_lo, y_hi) * pitch, x0 - kHL + 4 * v, w);
+        }
+#pragma unroll
+        for (int it = 0; it < ITP; ++it) {
+            const int i = tid + it * 256;
+            if (i < LH * kNVROW) {
+                const int r = i / kNVROW;
+                const int v = i - r * kNVROW;
+                *reinterpret_cast<float4 *>(&lum[r * kLW + 4 * v]) = luma4(pre[it]);
+                if (v >= 1 && v <= kTW / 4) *reinterpret_cast<uint32_t *>(&alpha[r * kTW + 4 * (v - 1)]) = alpha4(pre[it]);
+            }
+        }
+    }
+    __syncthreads();
+
+    uint4 nxt[ITN];
+    for (int t = t0; t < t1; ++t) {
+        const int y0 = oy0 + t * TH;
+        const bool more = (t + 1 < t1);
+        // prefetch the TH new rows of tile t+1 (window rows HALO .. LH-1)
+        fetch_rows(nxt, y0 + TH - A + HALO, TH);  // unconditional; unused after the last tile
+
+        uint32_t res[RPT][kCPT];
+        tile_compute<K, A, MODE, RPT, FAST>(lum, taps, tx, ty, res);
+
+        const int gx0 = x0 + kCPT * tx;
+#pragma unroll
+        for (int o = 0; o < RPT; ++o) {
+            const int ly = ty * RPT + o;
+            const int gy = y0 + ly;
+            if (gy >= oy1) break;  // wave-uniform
+            const uint8_t *arow = &alpha[(ly + A) * kTW + kCPT * tx];
+            const uint32_t v0 = mpx_px_gray(res[o][0], arow[0]);
+            const uint32_t v1 = mpx_px_gray(res[o][1], arow[1]);
+            uint32_t *orow = out + (int64_t)gy * pitch;
+            if (VEC && full_x) {
+                *reinterpret_cast<uint2 *>(orow + gx0) = make_uint2(v0, v1);
+            } else {
+                if (gx0 < w) orow[gx0] = v0;
+                if (gx0 + 1 < w) orow[gx0 + 1] = v1;
+            }
+        }
+        if (!more) break;
+        // slide: window rows TH .. LH-1 become rows 0 .. HALO-1. The sources are
+        // read before the barrier (nobody writes LDS until after it), written
+        // after it, together with the prefetched rows HALO .. LH-1.
+        static_assert(HALO * kNVROW <= 256 && HALO * (kTW / 16) <= 256, "slide must fit one pass");
+        const int sr = tid / kNVROW, sv = tid - (tid / kNVROW) * kNVROW;
+        const int ar = tid / (kTW / 16), ac = tid - ar * (kTW / 16);
+        float4 slum;
+        uint4 salp;
+        if (tid < HALO * kNVROW) slum = *reinterpret_cast<const float4 *>(&lum[(TH + sr) * kLW + 4 * sv]);
+        if (tid < HALO * (kTW / 16)) salp = *reinterpret_cast<const uint4 *>(&alpha[(TH + ar) * kTW + 16 * ac]);
+        __syncthreads();  // every wave is done reading the window
+        if (tid < HALO * kNVROW) *reinterpret_cast<float4 *>(&lum[sr * kLW + 4 * sv]) = slum;
+        if (tid < HALO * (kTW / 16)) *reinterpret_cast<uint4 *>(&alpha[ar * kTW + 16 * ac]) = salp;
+        store_rows(nxt, HALO, TH);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-streaming kernel (production path for K in {2, 3, 5, 7}).
+//
+// Every wave is independent: no LDS, no barrier. A wave owns a strip of
+// OW = 128 - P - R2 output columns (P = anchor rounded up to even, R2 = right
+// reach rounded up to even) and a segment of SEG output rows. Lane l holds
+// input columns x0 - P + 2l and +1 (one 8-B load per row), so the 64 lanes
+// cover the strip plus its horizontal halo; lanes whose window would leave
+// the 128 loaded columns produce no output. Per input row a lane converts its
+// two pixels to luminance once and assembles the horizontal window from its
+// neighbours with DPP wave shifts (pure VALU, no LDS traffic). The last K
+// rows' windows stay in registers (a ring indexed statically by unrolling the
+// row loop K times), and the loads run K rows ahead of their use, so each wave
+// keeps K x 512 B in flight with no synchronisation at all. Registers stay low
+// enough for 6-8 waves per SIMD, which is what hides HBM latency here.
+// ---------------------------------------------------------------------------
+constexpr int kDppShr1 = 0x138;  // wave_shr:1 -> lane i reads lane i-1
+constexpr int kDppShl1 = 0x130;  // wave_shl:1 -> lane i reads lane i+1
+
+__device__ __forceinline__ float from_prev(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), kDppShr1, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float from_next(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), kDppShl1, 0xf, 0xf, true));
+}
+
+template <int K, int A, int OWX = 0>
+struct WaveGeom {
+    static constexpr int R = K - 1 - A;            // right reach
+    static constexpr int P = A + (A & 1);          // left pad, even
+    static constexpr int R2 = R + (R & 1);         // right pad, even
+    static constexpr int OW = OWX ? OWX : 128 - P - R2;  // output columns per strip
+    static constexpr int NV = 2 + A + R;           // window values per lane and row
+    static constexpr int LANE0 = P / 2;            // first producing lane
+    static constexpr int NLANES = OW / 2;          // producing lanes
+};
+
+// ---- tap sources: runtime (kernel-argument SGPRs) or compile-time (named filters) ----
+struct RuntimeTaps {
+    static constexpr bool kConst = false;
+};
+// Reference Roberts operator (filters.h "roberts").
+struct RobertsTaps {
+    static constexpr bool kConst = true;
+    static constexpr float wx[4] = {-1.0f, 0.0f, 0.0f, 1.0f};
+    static constexpr float wy[4] = {0.0f, 1.0f, -1.0f, 0.0f};
+};
+// 5x5 Sobel / 48 (filters.h "sobel5"); bit-identical constants: (float)k / 48.0f
+struct Sobel5Taps {
+    static constexpr bool kConst = true;
+    static constexpr float wx[25] = {-1.0f / 48, -2.0f / 48, 0, 2.0f / 48, 1.0f / 48,
+                                     -4.0f / 48, -8.0f / 48, 0, 8.0f / 48, 4.0f / 48,
+                                     -6.0f / 48, -12.0f / 48, 0, 12.0f / 48, 6.0f / 48,
+                                     -4.0f / 48, -8.0f / 48, 0, 8.0f / 48, 4.0f / 48,
+                                     -1.0f / 48, -2.0f / 48, 0, 2.0f / 48, 1.0f / 48};
+    static constexpr float wy[25] = {-1.0f / 48, -4.0f / 48, -6.0f / 48, -4.0f / 48, -1.0f / 48,
+                                     -2.0f / 48, -8.0f / 48, -12.0f / 48, -8.0f / 48, -2.0f / 48,
+                                     0, 0, 0, 0, 0,
+                                     2.0f / 48, 8.0f / 48, 12.0f / 48, 8.0f / 48, 2.0f / 48,
+                                     1.0f / 48, 4.0f / 48, 6.0f / 48, 4.0f / 48, 1.0f / 48};
+};
+
+template <class F>
+__device__ __forceinline__ float tap_x(const Taps &t, int i) {
+    if constexpr (F::kConst) return F::wx[i];
+    else return t.wx[i];
+}
+template <class F>
+__device__ __forceinline__ float tap_y(const Taps &t, int i) {
+    if constexpr (F::kConst) return F::wy[i];
+    else return t.wy[i];
+}
+
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// Luminance of two pixels with packed fp32 (v_pk_mul_f32 / v_pk_add_f32): the
+// same three products and two sums per pixel as mpx_luma, rounded per element.
+__device__ __forceinline__ f2_t luma2(uint32_t p0, uint32_t p1) {
+    const f2_t r = {(float)mpx_px_r(p0), (float)mpx_px_r(p1)};
+    const f2_t g = {(float)mpx_px_g(p0), (float)mpx_px_g(p1)};
+    const f2_t b = {(float)mpx_px_b(p0), (float)mpx_px_b(p1)};
+    const f2_t t0 = r * f2_t{0.299f, 0.299f};
+    const f2_t t1 = g * f2_t{0.587f, 0.587f};
+    const f2_t t2 = b * f2_t{0.114f, 0.114f};
+    return (t0 + t1) + t2;
+}
+
+template <int K, int A, int MODE, bool VEC, bool FAST, class F = RuntimeTaps, int OWX = 0>
+__global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                        int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                                                        int seg, int segs_per_strip, int nwaves, int strips,
+                                                        int strip_minor, Taps taps) {
+    using G = WaveGeom<K, A, OWX>;
+    static_assert(G::P + G::OW + G::R2 <= 128, "strip plus halo exceeds one wave's 128 columns");
+    constexpr int NV = G::NV;
+    constexpr int NE = (NV + 1) / 2;  // even-aligned pairs (w[2q], w[2q+1])
+    constexpr int NO = NV / 2;        // odd pairs (w[2q+1], w[2q+2])
+    constexpr bool TWO = (MODE == MPX_CONV_MAG2);
+    const int lane = threadIdx.x & 63;
+    // readfirstlane: make the wave index (and everything derived from it: the
+    // segment bounds and the row-loop exits) provably wave-uniform, so the loop
+    // branches are scalar and hipcc keeps counted vmcnt waits across them
+    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (gw >= nwaves) return;  // wave-uniform
+    // strip_minor: consecutive waves take horizontally adjacent strips of the
+    // same rows, so the waves running together stream contiguous row pieces
+    // (DRAM-page friendly, like a copy); otherwise they walk one strip downwards.
+    const int strip = strip_minor ? gw % strips : gw / segs_per_strip;
+    const int sg = strip_minor ? gw / strips : gw - strip * segs_per_strip;
+    const int ys = oy0 + sg * seg;
+    const int ye = min(ys + seg, oy1);
+    const int x0 = strip * G::OW;
+    const int cin = x0 - G::P + 2 * lane;  // this lane's first input column
+    const bool producer = lane >= G::LANE0 && lane < G::LANE0 + G::NLANES;
+    const int ox = cin;                    // output column of element 0 (producers only)
+    const bool st0 = producer && ox < w;
+    const bool st1 = producer && ox + 1 < w;
+    const int iy0 = ys - A;                // first input row
+
+    // Raw loads only: the edge fix-up (clamp-to-edge of a pair lying left or
+    // right of the image) is applied when a row is CONSUMED, D rows later. Any
+    // VALU use of a loaded register right after the load makes hipcc wait for it
+    // there, which would drain the prefetch ring every iteration.
+    const int cc = VEC ? mpx_clampi(cin, 0, w - 2) : 0;
+    const bool pair_left = cin < 0, pair_right = cin >= w;
+    // The sched_barrier pins every load at its program position: left alone the
+    // scheduler sinks prefetches towards their first use (lower register
+    // pressure), which turns the ring back into load-then-wait.
+    auto load_row = [&](int i) -> uint2 {
+        const int gy = mpx_clampi(iy0 + i, y_lo, y_hi);
+        const uint32_t *row = in + (int64_t)gy * pitch;
+        uint2 r;
+        if constexpr (VEC) {  // w even: the pair is entirely inside, left or right
+            r = *reinterpret_cast<const uint2 *>(row + cc);
+        } else {
+            r = make_uint2(row[mpx_clampi(cin, 0, w - 1)], row[mpx_clampi(cin + 1, 0, w - 1)]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return r;
+    };
+    auto fix_pair = [&](uint2 q) -> uint2 {
+        if constexpr (VEC) {
+            uint2 p;
+            p.x = pair_right ? q.y : q.x;
+            p.y = pair_left ? q.x : q.y;
+            return p;
+        } else {
+            return q;
+        }
+    };
+
+    // Prefetch ring of D >= 4 rows (a multiple of K so both rings keep
+    // compile-time slots when the row loop is unrolled D times).
+    constexpr int D = K * ((4 + K - 1) / K);
+    uint2 pre[D];         // prefetch ring: raw pixels of input rows i .. i+D-1
+    f2_t we[K][NE];       // window ring, even pairs (register-pair aligned for v_pk_fma_f32)
+    f2_t wo[K][NO > 0 ? NO : 1];  // window ring, odd pairs
+    uint32_t alp[K];      // alpha pair ring (bits 0-7: element 0, 8-15: element 1)
+
+    // consume the input row in window slot u: luminance (packed), alpha, and the
+    // horizontal window w[0 .. NV-1] = columns cin-A .. cin+1+R from the
+    // neighbouring lanes by DPP wave shifts
+    auto consume = [&](int u, uint2 px) {
+        const f2_t l = luma2(px.x, px.y);
+        alp[u] = (px.x >> 24) | ((px.y >> 24) << 8);
+        float wv[NV];
+        wv[A] = l.x;
+        wv[A + 1] = l.y;
+        if constexpr (A >= 1) wv[A - 1] = from_prev(l.y);
+        if constexpr (A >= 2) wv[A - 2] = from_prev(l.x);
+        if constexpr (A >= 3) wv[A - 3] = from_prev(wv[A - 1]);
+        if constexpr (G::R >= 1) wv[A + 2] = from_next(l.x);
+        if constexpr (G::R >= 2) wv[A + 3] = from_next(l.y);
+        if constexpr (G::R >= 3) wv[A + 4] = from_next(wv[A + 2]);
+#pragma unroll
+        for (int q = 0; q < NE; ++q) we[u][q] = f2_t{wv[2 * q], 2 * q + 1 < NV ? wv[2 * q + 1] : 0.0f};
+#pragma unroll
+        for (int q = 0; q < NO; ++q) wo[u][q] = f2_t{wv[2 * q + 1], wv[2 * q + 2]};
+    };
+
+#pragma unroll
+    for (int q = 0; q < D; ++q) pre[q] = load_row(q);
+    // warm-up: rows 0 .. K-2 only fill the window
+#pragma unroll
+    for (int u = 0; u < K - 1; ++u) {
+        const uint2 px = fix_pair(pre[u]);
+        pre[u] = load_row(u + D);
+        consume(u, px);
+    }
+    // steady state: every input row completes one output row. The row loop runs
+    // in whole groups of D (ring slots are then compile-time constants) with no
+    // branch around any memory operation; output rows past the segment end are
+    // computed and dropped by the store's bounds check.
+    const int ngroups = (ye - ys + D - 1) / D;
+    for (int g = 0; g < ngroups; ++g) {
+#pragma unroll
+        for (int v = 0; v < D; ++v) {
+            const int u = (K - 1 + v) % K;      // window slot of the newest row
+            const int q = (K - 1 + v) % D;      // its prefetch slot
+            const int i = K - 1 + g * D + v;    // its input row index
+            const uint2 px = fix_pair(pre[q]);
+            pre[q] = load_row(i + D);
+            consume(u, px);
+            const int y = ys + g * D + v;       // output row completed by row i
+            // both output columns at once: packed FMAs over the (w[dx], w[dx+1]) pairs
+            f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
+#pragma unroll
+            for (int dy = 0; dy < K; ++dy) {
+                const int r = (u + 1 + dy) % K;
+#pragma unroll
+                for (int dx = 0; dx < K; ++dx) {
+                    const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
+                    const float cx = tap_x<F>(taps, dy * K + dx);
+                    if (!F::kConst || cx != 0.0f)  // compile-time for named filters: a zero tap adds exactly 0
+                        gx = __builtin_elementwise_fma(f2_t{cx, cx}, pv, gx);
+                    if constexpr (TWO) {
+                        const float cy = tap_y<F>(taps, dy * K + dx);
+                        if (!F::kConst || cy != 0.0f) gy = __builtin_elementwise_fma(f2_t{cy, cy}, pv, gy);
+                    }
+                }
+            }
+            uint32_t g0, g1;
+            if constexpr (TWO) {
+                const f2_t sq = gx * gx + gy * gy;  // v_pk_mul x2, v_pk_add: no contraction (-ffp-contract=off)
+                g0 = mag_to_gray<FAST>(sq.x);
+                g1 = mag_to_gray<FAST>(sq.y);
+            } else {
+                g0 = finish_gray<MODE, FAST>(gx.x, 0.0f);
+                g1 = finish_gray<MODE, FAST>(gx.y, 0.0f);
+            }
+            const uint32_t ap = alp[(u + 1 + A) % K];
+            const uint32_t v0 = mpx_px_gray(g0, ap & 0xffu);
+            const uint32_t v1 = mpx_px_gray(g1, (ap >> 8) & 0xffu);
+            // Branch-free stores: a buffer descriptor spanning exactly this
+            // output row; lanes (or padded rows) with nothing to store get an
+            // out-of-range offset and the hardware bounds check drops them.
+            // Stores under a branch would make the outstanding-op count
+            // unknowable to hipcc and cost a vmcnt(0) drain of the ring.
+            const bool row_ok = y < ye;
+            const int yc = row_ok ? y : ys;
+            const __amdgpu_buffer_rsrc_t orow =
+                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, w * 4, 0x00020000);
+            constexpr int kDrop = 0x7ffffff0;
+            if constexpr (VEC) {
+                typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+                const u32x2_t pv = {v0, v1};
+                __builtin_amdgcn_raw_buffer_store_b64(pv, orow, (st0 && row_ok) ? ox * 4 : kDrop, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(v0, orow, (st0 && row_ok) ? ox * 4 : kDrop, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(v1, orow, (st1 && row_ok) ? ox * 4 + 4 : kDrop, 0, 0);
+            }
+        }
+    }
+}
+
+// Gray value packing helper for the non-stream kernels.
+template <int MODE, bool FAST>
+__device__ __forceinline__ uint32_t gray_px(float gx, float gy, uint32_t a) {
+    return mpx_px_gray(finish_gray<MODE, FAST>(gx, gy), a);
+}
+
+}  // namespace edge
+}  // namespace mpx

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Kernel tuning harness: times lab2 conv kernel variants in ONE process with
+interleaved rounds (cdna_hip_programming.md §5.4 rule 24) on random 4096^2
+RGBA8 data, and checks every variant bit-exact against the production kernel.
+
+  python tools/kbench.py [--size 4096] [--rounds 5] [--iters 20]
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cuda_mpi_openmp_amd import _native, ops  # noqa: E402
+
+
+def time_launch(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters  # us
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--size", type=int, default=4096)
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--iters", type=int, default=20)
+    args = p.parse_args()
+    L = _native.lib()
+    dev = torch.device("cuda:0")
+    n = args.size
+    img = torch.randint(0, 256, (n, n, 4), dtype=torch.uint8, device=dev)
+    out = torch.empty_like(img)
+    bytes_moved = 2 * img.numel()
+
+    # exhaustive fast-sqrt equivalence check
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), 0))
+    torch.cuda.synchronize()
+    print(json.dumps({"fast_sqrt_selftest_mismatches": int(bad.item())}), flush=True)
+
+    variants = {}
+    for fname, k in (("sobel5", 5), ("roberts", 2)):
+        f = ops.get_filter(fname)
+        wx, wy = f.c_taps()
+        ref = ops.conv(img, f)
+
+        def mk(kind, p1, p2, fast, wx=wx, wy=wy, k=k):
+            return lambda: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, k, kind, p1, p2, fast,
+                                                            wx, wy, 0))
+
+        for seg in (8, 16, 32, 64):
+            variants[f"{fname}/wave-rt/seg{seg}"] = (mk(1, seg, 0, 1), ref)
+            variants[f"{fname}/wave-const/seg{seg}"] = (mk(2, seg, 0, 1), ref)
+        variants[f"{fname}/lds-stream/rpt4"] = (mk(0, 4, 0, 1), ref)
+        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ref)
+        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ref)
+    variants["copy/torch"] = ((lambda: out.copy_(img)), img)
+    rob_ref = ops.roberts(img)
+    for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
+        variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(img, out, geometry=g)), rob_ref)
+
+    # correctness first
+    cpu_img = img.cpu()
+    for fname in ("sobel5", "roberts"):
+        cpu = ops.conv(cpu_img, fname)
+        print(json.dumps({"production_vs_cpu": fname, "bit_exact": bool(torch.equal(ops.conv(img, fname).cpu(), cpu))}),
+              flush=True)
+    for name, (fn, ref) in variants.items():
+        out.zero_()
+        fn()
+        torch.cuda.synchronize()
+        ok = torch.equal(out, ref)
+        if not ok:
+            print(json.dumps({"variant": name, "ERROR": "mismatch vs production"}), flush=True)
+    times = {k: [] for k in variants}
+    for _ in range(args.rounds):
+        for name, (fn, _) in variants.items():
+            times[name].append(time_launch(fn, args.iters))
+    for name, ts in times.items():
+        med = statistics.median(ts)
+        print(json.dumps({"variant": name, "us_median": round(med, 2), "us_min": round(min(ts), 2),
+                          "TBps": round(bytes_moved / med / 1e6, 3), "Gpix_s": round(n * n / med / 1e3, 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
