@@ -33,6 +33,23 @@ __device__ __forceinline__ uint32_t mag_to_gray(float s) {
     }
 }
 
+// Fast path for two magnitudes at once: r = v_sqrt(min(s, 255^2)) decides
+// trunc(sqrt_rn(s)) unless fract(r) is within kSqrtMargin of an integer; one
+// wave-level branch then recomputes both lanes' pair exactly (rare).
+__device__ __forceinline__ void mag2_to_gray(float s0, float s1, uint32_t &g0, uint32_t &g1) {
+    const float c0 = fminf(s0, 65025.0f), c1 = fminf(s1, 65025.0f);
+    const float r0 = __builtin_amdgcn_sqrtf(c0), r1 = __builtin_amdgcn_sqrtf(c1);
+    const float f0 = __builtin_amdgcn_fractf(r0), f1 = __builtin_amdgcn_fractf(r1);
+    constexpr float kHalfOpen = 0.5f - kSqrtMargin;
+    const bool ok = (fabsf(f0 - 0.5f) < kHalfOpen) && (fabsf(f1 - 0.5f) < kHalfOpen);
+    g0 = (uint32_t)r0;
+    g1 = (uint32_t)r1;
+    if (!ok) {
+        g0 = mpx_sat_u8(sqrtf(s0));
+        g1 = mpx_sat_u8(sqrtf(s1));
+    }
+}
+
 template <int MODE, bool FAST>
 __device__ __forceinline__ uint32_t finish_gray(float gx, float gy) {
     if constexpr (MODE == MPX_CONV_MAG2) {
@@ -436,14 +453,15 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     uint2 pre[D];         // prefetch ring: raw pixels of input rows i .. i+D-1
     f2_t we[K][NE];       // window ring, even pairs (register-pair aligned for v_pk_fma_f32)
     f2_t wo[K][NO > 0 ? NO : 1];  // window ring, odd pairs
-    uint32_t alp[K];      // alpha pair ring (bits 0-7: element 0, 8-15: element 1)
+    uint32_t alp0[K], alp1[K];  // alpha ring, kept in place (bits 24-31)
 
     // consume the input row in window slot u: luminance (packed), alpha, and the
     // horizontal window w[0 .. NV-1] = columns cin-A .. cin+1+R from the
     // neighbouring lanes by DPP wave shifts
     auto consume = [&](int u, uint2 px) {
         const f2_t l = luma2(px.x, px.y);
-        alp[u] = (px.x >> 24) | ((px.y >> 24) << 8);
+        alp0[u] = px.x & 0xff000000u;
+        alp1[u] = px.y & 0xff000000u;
         float wv[NV];
         wv[A] = l.x;
         wv[A + 1] = l.y;
@@ -503,15 +521,19 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             uint32_t g0, g1;
             if constexpr (TWO) {
                 const f2_t sq = gx * gx + gy * gy;  // v_pk_mul x2, v_pk_add: no contraction (-ffp-contract=off)
-                g0 = mag_to_gray<FAST>(sq.x);
-                g1 = mag_to_gray<FAST>(sq.y);
+                if constexpr (FAST) {
+                    mag2_to_gray(sq.x, sq.y, g0, g1);
+                } else {
+                    g0 = mag_to_gray<false>(sq.x);
+                    g1 = mag_to_gray<false>(sq.y);
+                }
             } else {
                 g0 = finish_gray<MODE, FAST>(gx.x, 0.0f);
                 g1 = finish_gray<MODE, FAST>(gx.y, 0.0f);
             }
-            const uint32_t ap = alp[(u + 1 + A) % K];
-            const uint32_t v0 = mpx_px_gray(g0, ap & 0xffu);
-            const uint32_t v1 = mpx_px_gray(g1, (ap >> 8) & 0xffu);
+            // gray = g * 0x010101 + alpha: one v_mad_u32_u24 per pixel
+            const uint32_t v0 = __umul24(g0, 0x010101u) + alp0[(u + 1 + A) % K];
+            const uint32_t v1 = __umul24(g1, 0x010101u) + alp1[(u + 1 + A) % K];
             // Branch-free stores: a buffer descriptor spanning exactly this
             // output row; lanes (or padded rows) with nothing to store get an
             // out-of-range offset and the hardware bounds check drops them.
