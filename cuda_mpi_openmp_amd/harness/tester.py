@@ -1,0 +1,166 @@
+"""Experiment driver: k_times x kernel_sizes runs of the GPU binary (and of the
+CPU binary without geometry), statistics, CSV files and the median-time plot
+(reference tester.py:169-407, re-designed).
+
+* Runs are executed strictly sequentially — which is what the reference's
+  asyncio code effectively did — so GPU runs never
+  contend; every run has an optional timeout (new).
+* CSV: ``stats_<bin>.csv`` when every run verified, else ``failed_<bin>.csv``,
+  in the GPU binary's directory, with the reference's columns plus ``device``,
+  ``wall_ms`` and throughput columns (``gpixel_per_s`` for image labs,
+  ``gb_per_s`` for lab1). A CPU binary sharing the GPU binary's name gets a
+  ``cpu_`` prefix instead of overwriting its CSV.
+* Plot: ``median_execution_time.png`` — median kernel ms per (device,
+  kernel_size), legend listing ``metadata_columns2plot`` values and sample
+  counts; the CPU/GPU speedup of every GPU group is printed as well.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Any, Dict, List, Optional
+
+import pandas as pd
+
+from .core import RunRecord, print_stats, run_binary
+
+
+def _kernel_key(ks) -> str:
+    return json.dumps(ks)
+
+
+class Tester:
+    def __init__(self, binary_path_gpu: str, k_times: int, kernel_sizes: List[List[Any]],
+                 metadata_columns2plot: Optional[List[str]] = None, binary_path_cpu: Optional[str] = None,
+                 return_inp: bool = False, return_task_res: bool = False, timeout: Optional[float] = None,
+                 gpu_env: Optional[Dict[str, str]] = None, gpu_label: str = "HIP"):
+        self.binary_path_gpu = binary_path_gpu
+        self.binary_path_cpu = binary_path_cpu
+        self.k_times = int(k_times)
+        self.kernel_sizes = kernel_sizes or [[None, None]]
+        self.metadata_columns2plot = list(metadata_columns2plot or [])
+        self.return_inp = return_inp
+        self.return_task_res = return_task_res
+        self.timeout = timeout
+        self.gpu_env = gpu_env
+        self.gpu_label = gpu_label
+        self.dir2save = os.path.dirname(os.path.abspath(binary_path_gpu))
+
+    # ------------------------------------------------------------------
+    def run_experiment(self, binary_path: str, kernel_sizes, processor, device: str) -> pd.DataFrame:
+        bin_name = os.path.splitext(os.path.basename(binary_path))[0]
+        print(f"[Experiment bin_name=<{bin_name}>] START")
+        t_start = time.time()
+        rows: List[Dict[str, Any]] = []
+        env = self.gpu_env if device == self.gpu_label else None
+        for i in range(self.k_times):
+            for k1, k2 in kernel_sizes:
+                print(f"[Experiment bin_name=<{bin_name}> task={i} kernel_size=<{[k1, k2]}>] started")
+                rec: RunRecord = run_binary(binary_path, processor, k1, k2, self.return_inp, self.timeout, env)
+                row: Dict[str, Any] = {
+                    "idx_run_time": i,
+                    "bin_name": bin_name,
+                    "kernel_size": [k1, k2],
+                    "test_verification_result": rec.test_verification_result,
+                    "time_kernel_exe_ms": rec.time_kernel_exe_ms,
+                    "status": rec.status,
+                    "err": rec.err,
+                }
+                if self.return_task_res:
+                    row["task_result"] = rec.task_result
+                row.update(processor.get_attr())
+                row.update(rec.debug_data)
+                row["time_exe_ms_from_start_run_time_bin_name"] = (time.time() - t_start) * 1e3
+                row["wall_ms"] = rec.wall_ms
+                row["device"] = device
+                self._throughput(row)
+                rows.append(row)
+                print(f"[Experiment bin_name=<{bin_name}> task={i} kernel_size=<{[k1, k2]}>] finished with "
+                      f"`time_kernel_exe_ms`: {rec.time_kernel_exe_ms} ms")
+        df = pd.DataFrame(rows)
+        ok = bool(rows) and all(bool(r["test_verification_result"]) for r in rows)
+        prefix = "cpu_" if (device != self.gpu_label and self.binary_path_gpu and
+                            os.path.basename(binary_path) == os.path.basename(self.binary_path_gpu)) else ""
+        if ok:
+            print_stats([r["time_kernel_exe_ms"] for r in rows])
+            df.to_csv(os.path.join(self.dir2save, f"stats_{prefix}{bin_name}.csv"), index=False)
+            print(f"[Experiment bin_name=<{bin_name}>] SUCCESS!")
+            return df
+        failed = df[~df["test_verification_result"].fillna(False).astype(bool)] if len(df) else df
+        print(f"[Experiment bin_name=<{bin_name}>] FAILED: len={len(failed)}!")
+        failed.to_csv(os.path.join(self.dir2save, f"failed_{prefix}{bin_name}.csv"), index=False)
+        return pd.DataFrame()
+
+    @staticmethod
+    def _throughput(row: Dict[str, Any]) -> None:
+        t = row.get("time_kernel_exe_ms")
+        if not t:
+            return
+        if row.get("pixels"):
+            row["gpixel_per_s"] = row["pixels"] / (t * 1e-3) / 1e9
+        if row.get("vector_size"):
+            row["gb_per_s"] = 24.0 * row["vector_size"] / (t * 1e-3) / 1e9  # 2 reads + 1 write of fp64
+
+    # ------------------------------------------------------------------
+    def run_experiments(self, processor) -> pd.DataFrame:
+        t0 = time.time()
+        print("[Experiments] START")
+        frames = [self.run_experiment(self.binary_path_gpu, self.kernel_sizes, processor, self.gpu_label)]
+        if self.binary_path_cpu:
+            frames.append(self.run_experiment(self.binary_path_cpu, [[None, None]], processor, "CPU"))
+        df = pd.concat([f for f in frames if len(f)], ignore_index=True) if any(len(f) for f in frames) else \
+            pd.DataFrame()
+        if len(df):
+            self.report_speedup(df)
+            self.plot(df)
+        print(f"[Experiments] FINISH time exe: {time.time() - t0}")
+        return df
+
+    def report_speedup(self, df: pd.DataFrame) -> None:
+        if "CPU" not in set(df["device"]) or self.gpu_label not in set(df["device"]):
+            return
+        cpu = df[df["device"] == "CPU"]["time_kernel_exe_ms"].median()
+        g = df[df["device"] == self.gpu_label].copy()
+        g["ks"] = g["kernel_size"].apply(_kernel_key)
+        for ks, grp in g.groupby("ks"):
+            med = grp["time_kernel_exe_ms"].median()
+            if med:
+                print(f"[Speedup] CPU median {cpu:.5f} ms / {self.gpu_label}_{ks} median {med:.5f} ms = "
+                      f"{cpu / med:.1f}x")
+
+    def plot(self, df: pd.DataFrame) -> str:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+
+        d = df.copy()
+        d["kernel_size"] = d["kernel_size"].apply(_kernel_key)
+        grouped = (d.groupby(["device", "kernel_size"])
+                   .agg(median_time=("time_kernel_exe_ms", "median"), sample_count=("time_kernel_exe_ms", "size"))
+                   .reset_index())
+        grouped["label"] = [dev if dev == "CPU" else f"{dev}_{ks}"
+                            for dev, ks in zip(grouped["device"], grouped["kernel_size"])]
+        legend = ""
+        for col in self.metadata_columns2plot:
+            if col in d.columns:
+                legend += f"{col}: [" + ", \n".join(map(str, d[col].unique())) + "]\n"
+        legend += "\nSample Count by Group:\n" + "".join(
+            f"{lab}: {n} samples\n" for lab, n in zip(grouped["label"], grouped["sample_count"]))
+        fig, ax = plt.subplots(figsize=(16, 6))
+        bars = ax.bar(grouped["label"], grouped["median_time"], color="skyblue")
+        for bar, med in zip(bars, grouped["median_time"]):
+            ax.text(bar.get_x() + bar.get_width() / 2, bar.get_height() + 5e-5, f"{med:.5f}", ha="center",
+                    va="bottom")
+        plt.text(1.02, 0.95, legend, transform=ax.transAxes, fontsize=10, verticalalignment="top",
+                 bbox=dict(facecolor="white", alpha=0.5))
+        ax.set_xlabel("Device and Kernel Size")
+        ax.set_ylabel("Median Execution Time (ms)")
+        ax.set_title("Median Execution Time by Device and Kernel Size")
+        plt.tight_layout()
+        path = os.path.join(self.dir2save, "median_execution_time.png")
+        plt.savefig(path, dpi=300, bbox_inches="tight")
+        plt.close(fig)
+        return path

@@ -1,0 +1,169 @@
+"""2-D Jacobi solver for the Laplace equation on a row-slab decomposed grid —
+the distributed-stencil north star of BASELINE.json ("MPI -> RCCL 2D Jacobi
+stencil, 16384^2 grid domain-decomposed across 8 MI355X, halo exchange over
+xGMI"). The reference has no such solver; this is its MI355X-native
+form.
+
+Per iteration and rank:
+  1. sweep the two slab-edge rows (the only rows a neighbour needs);
+  2. post the halo exchange of those freshly computed rows over RCCL
+     (point-to-point on the xGMI link between neighbouring GPUs);
+  3. sweep the interior rows while the exchange is in flight;
+  4. wait for the halos, swap u <-> u_new.
+Every ``check_every`` iterations the sweeps also fold max|u_new - u| into a
+device scalar and one 8-byte all-reduce(MAX) produces the global residual (the
+small-message latency over xGMI is paid once per check, not per iteration).
+
+Global boundary: Dirichlet. Row 0 of rank 0's buffer is the top boundary, the
+last buffer row of the last rank the bottom boundary; columns 0 and cols-1 are
+fixed. A decomposed run is bit-identical to a one-rank run.
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import torch
+
+from .. import ops
+from ..parallel.collectives import all_reduce_max, gather_slabs
+from ..parallel.dist import DistContext
+from ..parallel.halo import HaloExchange
+from ..parallel.slab import Slab
+
+
+class FaultInjected(RuntimeError):
+    """Raised by the MPX_FAULT_INJECT hook (tests of failure detection)."""
+
+
+def _fault_hook(rank: int, it: int) -> None:
+    spec = os.environ.get("MPX_FAULT_INJECT")  # "rank:iteration"
+    if not spec:
+        return
+    r, i = (int(v) for v in spec.split(":"))
+    if r == rank and i == it:
+        raise FaultInjected(f"injected fault on rank {rank} at iteration {it}")
+
+
+class SlabJacobi:
+    def __init__(self, ctx: DistContext, global_rows: int, cols: int, dtype=torch.float64, check_every: int = 10,
+                 overlap: bool = True):
+        if cols < 3:
+            raise ValueError("need at least 3 columns")
+        self.ctx = ctx
+        self.cols = cols
+        self.dtype = dtype
+        self.check_every = max(1, int(check_every))
+        self.overlap = overlap
+        self.slab = Slab(global_rows, ctx.world, ctx.rank, halo_up=1, halo_down=1)
+        self.halo = HaloExchange(self.slab, ctx)
+        shape = (self.slab.buffer_rows, cols)
+        dev = ctx.device
+        self.u = torch.zeros(shape, dtype=dtype, device=dev)
+        self.un = torch.zeros(shape, dtype=dtype, device=dev)
+        self.resid = torch.zeros(1, dtype=dtype, device=dev)
+        self.iteration = 0
+        self.last_residual: Optional[float] = None
+        self._halos_valid = False  # u's halo rows hold the neighbours' current rows
+
+    # ------------------------------------------------------------------ setup
+    def set_boundary(self, top: float = 1.0, bottom: float = 0.0, left: float = 0.0, right: float = 0.0) -> None:
+        for t in (self.u, self.un):
+            t[:, 0] = left
+            t[:, -1] = right
+            if not self.slab.has_up:
+                t[0, :] = top
+            if not self.slab.has_down:
+                t[-1, :] = bottom
+
+    def fill(self, fn: Optional[Callable[[torch.Tensor, torch.Tensor], torch.Tensor]] = None, seed: int = 0) -> None:
+        """Interior initial values: fn(global_row_index, col_index) or seeded noise."""
+        s = self.slab
+        rows = torch.arange(s.row0, s.row0 + s.rows, device=self.u.device).unsqueeze(1)
+        cols = torch.arange(1, self.cols - 1, device=self.u.device).unsqueeze(0)
+        if fn is None:
+            g = torch.Generator(device="cpu").manual_seed(seed + 7919 * self.ctx.rank)
+            vals = torch.rand((s.rows, self.cols - 2), generator=g, dtype=torch.float64).to(self.u.device)
+        else:
+            vals = fn(rows, cols)
+        self.u[1:1 + s.rows, 1:-1] = vals.to(self.dtype)
+        self.un.copy_(self.u)
+        self._halos_valid = False
+
+    def sync_halos(self) -> None:
+        """Exchange u's slab-edge rows (needed once after (re)initialisation;
+        afterwards every step refreshes the halos of the rows it computes)."""
+        self.halo.exchange(self.u)
+        self.un.copy_(self.u)
+        self._halos_valid = True
+
+    @property
+    def owned(self) -> torch.Tensor:
+        return self.u[1:1 + self.slab.rows]
+
+    # ------------------------------------------------------------------ stepping
+    def _sweep(self, r0: int, r1: int, track: bool) -> None:
+        if r1 <= r0:
+            return
+        if self.u.is_cuda:
+            ops.jacobi_sweep(self.u, self.un, r0, r1, self.resid if track else None)
+        else:
+            r = ops.jacobi_sweep(self.u, self.un, r0, r1)
+            if track:
+                self.resid.fill_(max(float(self.resid.item()), r))
+
+    def step(self) -> Optional[float]:
+        _fault_hook(self.ctx.rank, self.iteration)
+        if not self._halos_valid:
+            self.sync_halos()
+        s = self.slab
+        n = s.rows
+        track = (self.iteration + 1) % self.check_every == 0
+        if track:
+            self.resid.zero_()
+        if self.ctx.is_distributed and self.overlap:
+            edge = [1] if n == 1 else [1, n]
+            for r in edge:
+                self._sweep(r, r + 1, track)
+            self.halo.start(self.un)      # RCCL waits for the edge rows only
+            self._sweep(2, n, track)      # interior overlaps the transfer
+            self.halo.wait()
+        else:
+            self._sweep(1, n + 1, track)
+            self.halo.exchange(self.un)
+        self.u, self.un = self.un, self.u
+        self.iteration += 1
+        if track:
+            all_reduce_max(self.resid, self.ctx)
+            self.last_residual = float(self.resid.item())
+            return self.last_residual
+        return None
+
+    def run(self, iters: int, tol: Optional[float] = None) -> int:
+        for _ in range(iters):
+            r = self.step()
+            if tol is not None and r is not None and r < tol:
+                break
+        return self.iteration
+
+    # ------------------------------------------------------------------ I/O
+    def gather(self) -> Optional[torch.Tensor]:
+        return gather_slabs(self.owned.contiguous(), self.slab, self.ctx)
+
+    def save_checkpoint(self, prefix: str) -> str:
+        """One file per rank: owned rows (+ halos), iteration, residual."""
+        path = f"{prefix}.rank{self.ctx.rank}.pt"
+        torch.save({"u": self.u.cpu(), "iteration": self.iteration, "residual": self.last_residual,
+                    "global_rows": self.slab.global_rows, "world": self.ctx.world, "cols": self.cols}, path)
+        return path
+
+    def load_checkpoint(self, prefix: str) -> None:
+        ck = torch.load(f"{prefix}.rank{self.ctx.rank}.pt", weights_only=True)
+        if (ck["global_rows"], ck["world"], ck["cols"]) != (self.slab.global_rows, self.ctx.world, self.cols):
+            raise ValueError("checkpoint geometry does not match this solver")
+        self.u.copy_(ck["u"].to(self.u.device, self.dtype))
+        self.un.copy_(self.u)
+        self.iteration = int(ck["iteration"])
+        self.last_residual = ck["residual"]
+        self._halos_valid = False

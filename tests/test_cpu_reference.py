@@ -1,0 +1,100 @@
+"""CPU-side numerics: the native OpenMP references against the ground truth of
+the reference repository and against plain-PyTorch implementations."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cuda_mpi_openmp_amd import ops
+from cuda_mpi_openmp_amd.ops import reference as ref
+
+from .helpers import LAB2_DATA, LAB2_GT, LAB3_CLASSES, LAB3_DATA, LAB3_GT, bytes_to_img, hex_bytes, img_to_bytes, rand_img, smooth_img
+
+
+@pytest.mark.parametrize("name", ["test_01", "test_02"])
+def test_roberts_cpu_ground_truth(name):
+    img = bytes_to_img(hex_bytes(os.path.join(LAB2_DATA, name + ".txt")))
+    assert img_to_bytes(ops.roberts(img)) == hex_bytes(os.path.join(LAB2_GT, name + ".txt"))
+    assert img_to_bytes(ops.conv(img, "roberts")) == hex_bytes(os.path.join(LAB2_GT, name + ".txt"))
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (1, 5), (3, 3), (40, 61), (128, 130)])
+def test_roberts_cpu_matches_torch_exactly(hw):
+    img = rand_img(*hw, seed=hw[1])
+    assert torch.equal(ops.roberts(img), ref.roberts(img))
+    assert torch.equal(ops.conv(img, "roberts"), ops.roberts(img))
+
+
+@pytest.mark.parametrize("filt", ops.list_filters())
+def test_conv_cpu_within_one_level_of_torch(filt):
+    img = smooth_img(45, 77, seed=4)
+    f = ops.get_filter(filt)
+    a = ops.conv(img, f)
+    b = ref.conv(img, f)
+    assert int((a[..., :3].int() - b[..., :3].int()).abs().max()) <= 1
+    assert torch.equal(a[..., 3], img[..., 3])
+    assert torch.equal(a[..., 0], a[..., 1]) and torch.equal(a[..., 1], a[..., 2])
+
+
+def test_filter_table():
+    names = ops.list_filters()
+    assert {"roberts", "sobel3", "sobel5", "gauss5"} <= set(names)
+    f = ops.get_filter("sobel5")
+    assert (f.k, f.anchor, f.halo_up, f.halo_down) == (5, 2, 2, 2)
+    assert abs(sum(f.wx)) < 1e-6 and f.wx[4] == np.float32(1.0 / 48)
+    with pytest.raises(Exception):
+        ops.get_filter("no-such-filter")
+
+
+def test_conv_rows_slabs_cpu():
+    f = ops.get_filter("sobel5")
+    img = smooth_img(90, 33, seed=8)
+    full = ops.conv(img, f)
+    out = torch.empty((40, 33, 4), dtype=torch.uint8)
+    buf = img[28:72].contiguous()  # rows 30..69 owned, 2 halo rows each side
+    ops.conv_rows(buf, out, f, src_row0=2, out_row0=0, oy0=0, oy1=40, y_lo=-2, y_hi=41)
+    assert torch.equal(out, full[30:70])
+
+
+def test_classify_cpu_ground_truth():
+    img = bytes_to_img(hex_bytes(os.path.join(LAB3_DATA, "test_01_lab3.txt")))
+    mu, inv = ops.class_stats(img, LAB3_CLASSES)
+    out = img.clone()
+    ops.classify_(out, mu, inv)
+    assert img_to_bytes(out) == hex_bytes(os.path.join(LAB3_GT, "test_01_lab3.txt"))
+    assert torch.equal(ref.classify(img, mu, inv), out)
+
+
+def test_class_stats_matches_numpy():
+    img = smooth_img(50, 60, seed=3)
+    rng = np.random.default_rng(1)
+    pts = [np.stack([rng.integers(0, 60, 30), rng.integers(0, 50, 30)], 1) for _ in range(3)]
+    mu, inv = ops.class_stats(img, pts)
+    for c, p in enumerate(pts):
+        px = img.numpy()[p[:, 1], p[:, 0], :3].astype(np.float64)
+        assert np.allclose(mu[c], px.mean(0), rtol=1e-12)
+        assert np.allclose(inv[c], np.linalg.inv(np.cov(px.T)), rtol=1e-9, atol=1e-12)
+
+
+def test_class_stats_rejects_bad_points():
+    img = smooth_img(10, 10)
+    with pytest.raises(Exception):
+        ops.class_stats(img, [np.array([[10, 0], [1, 1]])])
+
+
+def test_vsub_cpu():
+    a = torch.randn(1001, dtype=torch.float64)
+    b = torch.randn(1001, dtype=torch.float64)
+    assert torch.equal(ops.vsub(a, b), a - b)
+    assert torch.equal(ops.vsub(a.float(), b.float()), a.float() - b.float())
+
+
+def test_jacobi_cpu_matches_torch():
+    u = torch.rand((34, 50), dtype=torch.float64)
+    un = torch.zeros_like(u)
+    r = ops.jacobi_sweep(u, un, 1, 33)
+    expect = ref.jacobi(u, 1, 33)
+    assert torch.equal(un[1:33, 1:-1], expect[1:33, 1:-1])
+    assert r == float((expect[1:33, 1:-1] - u[1:33, 1:-1]).abs().max())

@@ -1,0 +1,193 @@
+"""Multi-process decomposition tests on CPU (gloo backend, world sizes 2 and 3):
+every distributed workload must reproduce the single-process result exactly."""
+
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from cuda_mpi_openmp_amd import ops, parallel
+from cuda_mpi_openmp_amd.models import SlabEdgeDetector, SlabJacobi, SlabPixelClassifier, ShardedVectorSub
+from cuda_mpi_openmp_amd.models.classifier import class_points_for, split_rows
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn_name, args, errq):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        torch.set_num_threads(1)
+        ctx = parallel.init(device="cpu")
+        globals()[fn_name](ctx, *args)
+        parallel.shutdown()
+    except Exception:  # noqa: BLE001
+        errq.put(f"rank {rank}: {traceback.format_exc()}")
+
+
+def run_world(world, fn_name, *args):
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, args, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _img(h, w, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, generator=g)
+
+
+# ---------------------------------------------------------------- workers
+def conv_worker(ctx, h, w, filt, overlap, outdir):
+    full = _img(h, w, 5)
+    det = SlabEdgeDetector(ctx, h, w, filt, overlap=overlap)
+    s = det.slab
+    det.load(full[s.row0:s.row0 + s.rows])
+    out = det.step()
+    got = parallel.gather_slabs(out, s, ctx)
+    if ctx.rank == 0:
+        ref = ops.conv(full, filt)
+        assert torch.equal(got, ref), "decomposed conv differs from the single-process result"
+        torch.save(got, os.path.join(outdir, f"conv_{filt}.pt"))
+
+
+def jacobi_worker(ctx, rows, cols, iters, outdir, tag):
+    sol = SlabJacobi(ctx, rows, cols, check_every=5)
+    sol.set_boundary(top=1.0, left=0.5)
+    sol.fill(seed=3)
+    # the initial field must not depend on the decomposition: rebuild from the global one
+    g = torch.Generator().manual_seed(3)
+    field = torch.rand((rows, cols - 2), generator=g, dtype=torch.float64)
+    sol.u[1:1 + sol.slab.rows, 1:-1] = field[sol.slab.row0:sol.slab.row0 + sol.slab.rows]
+    sol.sync_halos()
+    sol.run(iters)
+    full = sol.gather()
+    if ctx.rank == 0:
+        torch.save({"u": full, "res": sol.last_residual}, os.path.join(outdir, f"jacobi_{tag}.pt"))
+
+
+def jacobi_ckpt_worker(ctx, rows, cols, outdir):
+    a = SlabJacobi(ctx, rows, cols, check_every=4)
+    a.set_boundary(top=2.0)
+    a.fill(seed=1)
+    a.run(8)
+    a.save_checkpoint(os.path.join(outdir, "ck"))
+    a.run(8)
+    b = SlabJacobi(ctx, rows, cols, check_every=4)
+    b.set_boundary(top=2.0)
+    b.load_checkpoint(os.path.join(outdir, "ck"))
+    b.run(8)
+    assert b.iteration == a.iteration == 16
+    assert torch.equal(a.u, b.u) and a.last_residual == b.last_residual
+
+
+def classify_worker(ctx, h, w, nc):
+    full = _img(h, w, 9)
+    pts = class_points_for(h, w, nc, 25, seed=2)
+    clf = SlabPixelClassifier(ctx, h, w, path="direct")
+    clf.img.copy_(split_rows(full, clf.slab))
+    clf.fit(pts)
+    mu, inv = ops.class_stats(full, pts)
+    assert np.array_equal(mu, clf.mu) and np.array_equal(inv, clf.inv)
+    clf.classify()
+    got = parallel.gather_slabs(clf.img, clf.slab, ctx)
+    if ctx.rank == 0:
+        ref = full.clone()
+        ops.classify_(ref, mu, inv)
+        assert torch.equal(got, ref)
+
+
+def vsub_worker(ctx, n):
+    m = ShardedVectorSub(ctx, n)
+    m.fill_random(seed=4)
+    m.step()
+    assert torch.equal(m.c, m.a - m.b)
+    got = m.gather()
+    if ctx.rank == 0:
+        assert got.shape == (n,)
+
+
+def collectives_worker(ctx):
+    t = torch.tensor([float(ctx.rank + 1)])
+    parallel.all_reduce_max(t, ctx)
+    assert t.item() == ctx.world
+    assert parallel.max_over_ranks(ctx.rank * 2.0, ctx) == 2.0 * (ctx.world - 1)
+    obj = parallel.broadcast_object({"r": ctx.rank} if ctx.rank == 0 else None, ctx)
+    assert obj == {"r": 0}
+    s = parallel.Slab(10, ctx.world, ctx.rank)
+    full = torch.arange(40, dtype=torch.float32).reshape(10, 4) if ctx.rank == 0 else None
+    mine = parallel.scatter_rows(full, s, ctx, like=torch.empty(0, 4))
+    assert torch.equal(mine, torch.arange(40, dtype=torch.float32).reshape(10, 4)[s.row0:s.row0 + s.rows])
+
+
+# ---------------------------------------------------------------- tests
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("filt", ["sobel5", "roberts", "sobel3"])
+def test_slab_conv_equals_single(world, filt, tmp_path):
+    run_world(world, "conv_worker", 37, 29, filt, True, str(tmp_path))
+
+
+def test_slab_conv_no_overlap(tmp_path):
+    run_world(2, "conv_worker", 20, 16, "sobel5", False, str(tmp_path))
+
+
+def test_slab_jacobi_equals_single(tmp_path):
+    run_world(1, "jacobi_worker", 23, 17, 20, str(tmp_path), "w1")
+    run_world(3, "jacobi_worker", 23, 17, 20, str(tmp_path), "w3")
+    a = torch.load(tmp_path / "jacobi_w1.pt", weights_only=True)
+    b = torch.load(tmp_path / "jacobi_w3.pt", weights_only=True)
+    assert torch.equal(a["u"], b["u"]) and a["res"] == b["res"] and a["res"] is not None
+
+
+def test_slab_jacobi_checkpoint_resume(tmp_path):
+    run_world(2, "jacobi_ckpt_worker", 16, 12, str(tmp_path))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_classifier(world):
+    run_world(world, "classify_worker", 31, 23, 4)
+
+
+def test_sharded_vsub_and_collectives():
+    run_world(3, "vsub_worker", 1001)
+    run_world(2, "collectives_worker")
+
+
+def test_slab_math():
+    s = [parallel.Slab(10, 3, r, 2, 2) for r in range(3)]
+    assert [x.rows for x in s] == [4, 3, 3] and [x.row0 for x in s] == [0, 4, 7]
+    assert s[0].y_lo == 0 and s[0].y_hi == 5 and s[1].y_lo == -2 and s[2].y_hi == 2
+    assert s[0].interior() == (0, 2) and s[0].boundary() == [(2, 4)]
+    assert s[1].interior() == (2, 2) and s[1].boundary() == [(0, 2), (2, 3)]
+    with pytest.raises(ValueError):
+        parallel.Slab(5, 3, 0, 2, 2)
+    assert parallel.min_ranks_for(16384 * 8, 16384 * 8, buffers=2) == 1
+    assert parallel.max_rows_per_gpu(16384 * 8, buffers=2) > 16384 * 50  # a 16384-wide fp64 grid: ~930k rows per GPU
+
+
+def test_fault_injection_raises(monkeypatch):
+    from cuda_mpi_openmp_amd.models.jacobi import FaultInjected
+
+    monkeypatch.setenv("MPX_FAULT_INJECT", "0:3")
+    sol = SlabJacobi(parallel.DistContext(), 8, 8)
+    sol.fill()
+    with pytest.raises(FaultInjected):
+        sol.run(10)
+    assert sol.iteration == 3

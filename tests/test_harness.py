@@ -1,0 +1,148 @@
+"""The run_test.py / tester.py compatible harness, driven with the CPU binaries
+(GPU binaries in the gpu-marked tests)."""
+
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from cuda_mpi_openmp_amd.harness import args as hargs
+from cuda_mpi_openmp_amd.harness import core
+from cuda_mpi_openmp_amd.harness.processors import Lab1Processor
+from cuda_mpi_openmp_amd.utils import imgdata
+
+from .helpers import LAB2_DATA, LAB2_GT, ROOT, hex_bytes
+
+
+def test_passthrough_kwargs_coercion():
+    kw = hargs.passthrough_kwargs(["--a", "true", "--b", "3", "--c", "2.5", "--d", "x", "--flag",
+                                   "--links", '["u1","u2"]', "--e=7"])
+    assert kw == {"a": True, "b": 3, "c": 2.5, "d": "x", "flag": True, "links": ["u1", "u2"], "e": 7}
+
+
+def test_timing_line_and_geometry():
+    assert core.parse_timing("HIP execution time: <0.012345 ms>") == pytest.approx(0.012345)
+    assert core.parse_timing("CPU execution time: <3.000000 ms>") == 3.0
+    assert core.parse_timing("no timing") is None
+    assert core.geometry_prefix([32, 32], [16, 16]) == "32\n32\n16\n16\n"
+    assert core.geometry_prefix(512, 512) == "512\n512\n"
+    assert core.geometry_prefix(None, None) == ""
+    assert core.device_tag("/x/to_plot_hip_exe", [32, 32], [16, 16]) == "to_plot_hip_exe__32_32___16_16_"
+    st = core.time_stats([1.0, 2.0, 3.0, None])
+    assert st["median"] == 2.0 and st["min"] == 1.0 and st["max"] == 3.0
+
+
+def test_imgdata_roundtrip(tmp_path):
+    img = np.random.default_rng(0).integers(0, 256, (7, 9, 4), dtype=np.uint8)
+    raw = imgdata.encode_data(img)
+    assert np.array_equal(imgdata.decode_data(raw), img)
+    p = tmp_path / "x.data"
+    p.write_bytes(raw)
+    d = imgdata.ImgData(str(p))
+    assert d.width == 9 and d.height == 7 and d.data_path == str(p)
+    assert imgdata.parse_hex(d.hex) == raw
+    gt = open(os.path.join(LAB2_GT, "test_01.txt")).read()
+    assert imgdata.hex_groups(hex_bytes(os.path.join(LAB2_GT, "test_01.txt")), row_pixels=3).upper() == gt.strip()
+    # PNG: alpha forced to 255, converted copy written to the cache dir only
+    png = os.path.join(LAB2_DATA, "lenna.png")
+    before = set(os.listdir(LAB2_DATA))
+    d = imgdata.ImgData(png, cache_dir=str(tmp_path / "cache"))
+    assert d.pixels.shape == (512, 512, 4) and (d.pixels[..., 3] == 255).all()
+    assert os.path.exists(d.data_path) and set(os.listdir(LAB2_DATA)) == before
+
+
+def test_lab1_processor_roundtrip():
+    p = Lab1Processor(min_vector_size=1500, max_vector_size=1600)
+    stdin, kw, dbg = p.pre_process(device_info="x")
+    n = dbg["vector_size"]
+    lines = stdin.split("\n")
+    a = np.array(lines[1].split(), dtype=np.float64)
+    assert int(lines[0]) == n and a.size == n and np.array_equal(a, kw["first_vector"])  # exact round trip
+    res = p.get_task_result(" ".join(f"{v:.10e}" for v in kw["first_vector"] - kw["second_vector"]) + " ")
+    assert p.verify_result(res, **kw)
+    assert not p.verify_result(res * 1.001, **kw)
+
+
+def _copy_lab(tmp_path, lab):
+    dst = tmp_path / "labs" / lab
+    shutil.copytree(os.path.join(ROOT, "labs", lab, "src"), dst / "src",
+                    ignore=shutil.ignore_patterns("*.csv", "*.png"))
+    for sub in ("data", "data_out_gt"):
+        if os.path.isdir(os.path.join(ROOT, "labs", lab, sub)):
+            shutil.copytree(os.path.join(ROOT, "labs", lab, sub), dst / sub)
+    return dst
+
+
+def _run_test(args, cwd):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "run_test.py"), *args], cwd=cwd, capture_output=True,
+                          text=True, timeout=600)
+
+
+def test_harness_lab2_cpu_binaries(tmp_path):
+    lab = _copy_lab(tmp_path, "lab2")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "3", "--kernel_sizes", "[[null, null]]",
+                   "--metadata_columns2plot", '["filename"]'], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "SUCCESS" in r.stdout and "FAILED" not in r.stdout
+    df = pd.read_csv(lab / "src" / "stats_cpu_omp_exe.csv")
+    for col in ("idx_run_time", "bin_name", "kernel_size", "test_verification_result", "time_kernel_exe_ms",
+                "status", "err", "precision_array", "atol", "filename", "time_exe_ms_from_start_run_time_bin_name"):
+        assert col in df.columns
+    assert len(df) == 3 and df["test_verification_result"].all()
+    assert os.path.exists(lab / "src" / "median_execution_time.png")
+    # outputs land under data_out/<bin>_<k1>_<k2>/, inputs untouched
+    assert os.path.isdir(lab / "data_out" / "cpu_omp_exe_None_None")
+    assert sorted(os.listdir(lab / "data")) == sorted(os.listdir(os.path.join(ROOT, "labs", "lab2", "data")))
+
+
+def test_harness_lab2_detects_wrong_output(tmp_path):
+    lab = _copy_lab(tmp_path, "lab2")
+    # a "binary" that copies its input: test_01/test_02 must fail verification
+    fake = lab / "src" / "fake_exe"
+    fake.write_text("#!/bin/sh\nread a\nread b\ncp \"$a\" \"$b\"\necho 'CPU execution time: <1.0 ms>'\n")
+    fake.chmod(0o755)
+    r = _run_test(["--binary_path_cuda", str(fake), "--k_times", "5", "--kernel_sizes", "[[null, null]]"], tmp_path)
+    assert "FAILED" in r.stdout
+    assert os.path.exists(lab / "src" / "failed_fake_exe.csv")
+
+
+def test_harness_lab1_cpu(tmp_path):
+    lab = _copy_lab(tmp_path, "lab1")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--k_times", "2", "--kernel_sizes",
+                   "[[null, null]]", "--min_vector_size", "2000", "--max_vector_size", "2100"], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    df = pd.read_csv(lab / "src" / "stats_cpu_omp_exe.csv")
+    assert df["test_verification_result"].all() and (df["vector_size"] >= 2000).all()
+
+
+def test_harness_lab3_cpu_random_classes(tmp_path):
+    lab = _copy_lab(tmp_path, "lab3")
+    shutil.copytree(os.path.join(ROOT, "labs", "lab3", "data"), lab / "data", dirs_exist_ok=True)
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "2", "--kernel_sizes", "[[null, null]]",
+                   "--metadata_columns2plot", '["filename", "stat_init_pts"]'], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--k_times", "1", "--kernel_sizes",
+                   "[[null, null]]", "--count_classes", "5", "--count_pts", "20", "--synthetic", "64x48"], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_harness_lab2_gpu_vs_cpu(tmp_path):
+    lab = _copy_lab(tmp_path, "lab2")
+    shutil.copytree(os.path.join(ROOT, "labs", "lab2", "metric_calc"), lab / "metric_calc")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "to_plot_hip_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "4", "--kernel_sizes",
+                   json.dumps([[[32, 32], [16, 16]], [[16, 16], [32, 32]], [[0, 0], [0, 0]]]),
+                   "--metadata_columns2plot", '["filename"]', "--dir_to_data", str(lab / "metric_calc" / "large")],
+                  tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "[Speedup]" in r.stdout
+    df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
+    assert df["test_verification_result"].all() and (df["gpixel_per_s"] > 0).all()
