@@ -54,6 +54,8 @@ _SIGNATURES = {
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
     "mpx_classify": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp]),
+    "mpx_classify_ex": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp, c_vp]),
+    "mpx_classify_plan": (c_int, [c_int, _dp, _dp, c_int, ctypes.POINTER(ctypes.c_float)]),
     "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_jacobi_f32": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_cpu_threads": (c_int, []),

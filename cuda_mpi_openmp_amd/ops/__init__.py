@@ -2,6 +2,7 @@
 OpenMP C references (CPU tensors) of libmpx."""
 
 from .classify import class_stats, classify_
+from .classify import plan as classify_plan
 from .edge import conv, conv_rows, roberts
 from .filters import Filter, get_filter, list_filters
 from .stencil import jacobi_sweep
@@ -10,6 +11,7 @@ from .vector import vsub
 __all__ = [
     "class_stats",
     "classify_",
+    "classify_plan",
     "conv",
     "conv_rows",
     "roberts",

@@ -4,7 +4,7 @@ maximum-likelihood classification (reference lab3/src/main.cu:40-155)."""
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence, Tuple
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -12,7 +12,8 @@ import torch
 from .. import _native
 from .edge import check_image
 
-PATHS = {"direct": 0, "mfma": 1, "auto": 2}
+PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3}
+PATH_NAMES = {v: k for k, v in PATHS.items()}
 MAX_CLASSES = 32
 
 
@@ -38,25 +39,50 @@ def class_stats(img: torch.Tensor, classes: Sequence[np.ndarray]) -> Tuple[np.nd
 
 
 def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "auto", grid: int = 0,
-              block: int = 0) -> torch.Tensor:
+              block: int = 0, ambiguous: Optional[torch.Tensor] = None) -> torch.Tensor:
     """In place: alpha of every pixel = argmin_c (p - mu_c)^T inv_c (p - mu_c).
 
-    ``path``: ``direct`` (reference FMA chain), ``mfma`` (fp64 MFMA quadratic-form
-    GEMM with an exact fallback for near ties) or ``auto``. Every path returns
-    the same classes; CPU tensors use the OpenMP reference.
+    ``path``:
+      * ``direct`` — the reference fp64 FMA chain;
+      * ``fast``   — fp32 packed-VALU distances;
+      * ``mfma``   — fp32 MFMA distance GEMM (v_mfma_f32_32x32x2f32);
+      * ``auto``   — fast for nc <= 16, mfma above.
+    The fp32 paths classify a pixel only when its best/second margin exceeds a
+    rigorous bound on the fp32-vs-reference error and recompute every other
+    pixel with the fp64 chain, so every path returns identical classes
+    (statistics for which no bound can be proven run ``direct``). With
+    ``ambiguous`` (a 1-element int32 device tensor) the number of pixels that
+    took the exact fallback is added to it. CPU tensors use the OpenMP reference.
     """
     h, w = check_image(img)
+    mu_c, inv_c, nc = _params(mu, inv)
+    L = _native.lib()
+    if img.is_cuda:
+        amb = 0
+        if ambiguous is not None:
+            if not (ambiguous.is_cuda and ambiguous.dtype == torch.int32 and ambiguous.numel() >= 1):
+                raise ValueError("ambiguous must be a 1-element int32 device tensor")
+            amb = ambiguous.data_ptr()
+        _native.check(L.mpx_classify_ex(img.data_ptr(), h * w, nc, mu_c, inv_c, grid, block, PATHS[path], amb,
+                                        _native.stream_of(img)))
+    else:
+        L.mpx_cpu_classify(img.data_ptr(), h * w, nc, mu_c, inv_c)
+    return img
+
+
+def _params(mu: np.ndarray, inv: np.ndarray):
     mu = np.ascontiguousarray(mu, dtype=np.float64).reshape(-1)
     inv = np.ascontiguousarray(inv, dtype=np.float64).reshape(-1)
     nc = mu.size // 3
     if inv.size != 9 * nc or not 1 <= nc <= MAX_CLASSES:
         raise ValueError("mu must be (nc, 3) and inv (nc, 3, 3) with 1 <= nc <= 32")
-    mu_c = _native.f64_array(mu.tolist())
-    inv_c = _native.f64_array(inv.tolist())
-    L = _native.lib()
-    if img.is_cuda:
-        _native.check(L.mpx_classify(img.data_ptr(), h * w, nc, mu_c, inv_c, grid, block, PATHS[path],
-                                     _native.stream_of(img)))
-    else:
-        L.mpx_cpu_classify(img.data_ptr(), h * w, nc, mu_c, inv_c)
-    return img
+    return _native.f64_array(mu.tolist()), _native.f64_array(inv.tolist()), nc
+
+
+def plan(mu: np.ndarray, inv: np.ndarray, path: str = "auto") -> Tuple[str, float]:
+    """(path actually run, fp32 decision margin) for these class statistics."""
+    mu_c, inv_c, nc = _params(mu, inv)
+    margin = ctypes.c_float(0.0)
+    r = _native.lib().mpx_classify_plan(nc, mu_c, inv_c, PATHS[path], ctypes.byref(margin))
+    _native.check(r if r < 0 else 0)
+    return PATH_NAMES[r], float(margin.value)

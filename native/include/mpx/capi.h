@@ -100,6 +100,13 @@ int mpx_class_stats(const uint32_t *img, int w, int h, int nc, const int *np, co
 /* img[i].a = argmin_c (p - mu_c)^T inv_c (p - mu_c), in place (alpha = 255 if all NaN). */
 int mpx_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv,
                  int grid, int block, int path, void *stream);
+/* Same; when `ambiguous` (device uint32) is non-NULL it is incremented once per
+ * pixel whose fp32 margin was too small and that took the exact fp64 chain. */
+int mpx_classify_ex(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv,
+                    int grid, int block, int path, uint32_t *ambiguous, void *stream);
+/* Host-side plan: the path `path` resolves to for these statistics (DIRECT when
+ * the fp32 decision cannot be proven) and the fp32 decision margin. <0 = error. */
+int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin);
 
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*

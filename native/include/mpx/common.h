@@ -35,9 +35,10 @@ enum mpx_conv_mode {
 
 /* Which lab3 classifier implementation to run. */
 enum mpx_classify_path {
-    MPX_CLS_DIRECT = 0, /* fp64 (p-mu)^T A (p-mu), reference-exact                  */
-    MPX_CLS_MFMA = 1,   /* fp64 MFMA quadratic-form GEMM + guarded exact fallback  */
-    MPX_CLS_AUTO = 2
+    MPX_CLS_DIRECT = 0, /* fp64 (p-mu)^T A (p-mu), reference-exact                   */
+    MPX_CLS_MFMA = 1,   /* fp32 MFMA distance GEMM, proven margin + exact fallback  */
+    MPX_CLS_AUTO = 2,   /* FAST for nc <= 16, MFMA above, DIRECT if unprovable      */
+    MPX_CLS_FAST = 3    /* fp32 packed-VALU distances, proven margin + fallback     */
 };
 
 #ifdef __cplusplus

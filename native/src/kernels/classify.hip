@@ -6,19 +6,33 @@
 // class -1 (stored as 255); alpha is written in place.
 //
 // MI355X design
-//   * class parameters travel as a kernel-argument block (3 KiB, < 4 KiB
-//     kernarg limit): the class loop index is wave-uniform, so every mu/A load
-//     is a scalar s_load into SGPRs — the CDNA equivalent of a constant-cache
-//     broadcast, without a hipMemcpyToSymbol in the launch path;
-//   * each lane classifies 4 pixels from one 16-B load and writes them back with
-//     one 16-B store (the reference does a 4-B load and a 1-B store per pixel);
-//   * DIRECT path: the same FMA chain the reference GPU kernel compiles to, so
-//     results are bit-identical to mpx_cpu_classify;
-//   * MFMA path: dist = phi(p) . w_c with phi = [r^2 g^2 b^2 rg rb gb r g b 1],
-//     evaluated as a (16 pixels x 12) x (12 x 16 classes) fp64 GEMM per wave on
-//     v_mfma_f64_16x16x4_f64, then a top-2 argmin; any pixel whose best/second
-//     margin is within a rigorous rounding bound is recomputed with the DIRECT
-//     chain, so the chosen class is identical to the reference's.
+//   * class parameters travel as kernel arguments: the class loop index is
+//     wave-uniform, so every parameter load is a scalar s_load into SGPRs — the
+//     CDNA equivalent of a constant-cache broadcast, with no hipMemcpyToSymbol
+//     in the launch path;
+//   * each lane moves 4 pixels with one 16-B load and one 16-B store (the
+//     reference does a 4-B load and a 1-B store per pixel);
+//   * DIRECT: the fp64 FMA chain the reference GPU kernel compiles to, so the
+//     classes are bit-identical to mpx_cpu_classify. fp64 VALU runs at half the
+//     fp32 rate, so this path is VALU-bound at ~19 fp64 ops per (pixel, class).
+//   * FAST32 and MFMA32 decide in fp32 and prove the decision:
+//       Q_c(p) = sum_k w_ck phi_k(p),  phi = [r^2 g^2 b^2 rg rb gb r g b 1]
+//     (the expanded quadratic form of the symmetrised A_c). The host bounds
+//     |fp32 evaluation - reference fp64 chain| by tol_c for every pixel in
+//     [0,255]^3 (rounding of the weights, of the 10-term fmaf chain and of the
+//     reference chain itself). A pixel is classified in fp32 only if the
+//     second-best value exceeds the best by more than 2 max_c tol_c; every
+//     other pixel (near ties) is recomputed with the DIRECT chain, so all
+//     paths produce identical classes.
+//       - FAST32: VALU, two pixels per v_pk_fma_f32, 9 packed FMAs per class
+//         and pixel pair;
+//       - MFMA32: one v_mfma_f32_32x32x2f32 chain of K = 10 per 32 pixels x
+//         32 classes (the distance GEMM; gfx950 f32 MFMA is a k-ordered fmaf
+//         chain, so the same bound applies), the VALU only ranks the results.
+//     The argmin works on 32-bit keys (value bits with the low 5 mantissa bits
+//     replaced by the class index): best = min(best, key), second =
+//     med3(best, key, second). A bias folded into the constant weight makes
+//     every computed value positive, so unsigned key order is value order.
 #include "internal.hpp"
 
 #include <cmath>
@@ -29,6 +43,13 @@ namespace {
 struct ClassParams {
     double mu[MPX_MAX_CLASSES * 3];
     double A[MPX_MAX_CLASSES * 9];
+};
+
+constexpr int kFeat = 10;
+
+struct FastParams {
+    float w[MPX_MAX_CLASSES][kFeat];  // expanded weights incl. bias; padded classes: 0 ... 0, 3e38
+    float T2;                         // decision margin 2 * max_c tol_c
 };
 
 __device__ __forceinline__ uint32_t classify_direct(uint32_t p, int nc, const ClassParams &cp) {
@@ -80,199 +101,366 @@ __global__ void classify_direct_kernel(uint32_t *__restrict__ img, int64_t npix,
 }
 
 // ---------------------------------------------------------------------------
-// MFMA path. Geometry: 256-thread workgroups, each wave handles 16-pixel
-// groups; D[class][pixel] = sum_k W[k][class] * PHI[k][pixel] so that after
-// the MFMA lane l holds pixel (l & 15) for classes (l >> 4) + 4*reg.
-// v_mfma_f64_16x16x4_f64 operand maps (cdna_hip_programming.md §3):
-//   A[i][k]: lane l holds A[l & 15][k = l >> 4];  B[k][j]: lane l holds B[k = l >> 4][l & 15]
-//   C/D:     lane l, reg r holds D[row = (l >> 4) + 4 r][col = l & 15]
-// Here A = W^T (16 classes x 4 k), B = PHI (4 k x 16 pixels).
+// fp32 decision helpers
 // ---------------------------------------------------------------------------
-typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kPhi = 12;  // 10 features padded to 3 k-steps of 4
+constexpr uint32_t kKeyInit = 0x7f7fffe0u | 31u;  // ~FLT_MAX: "no class yet"
 
-struct QuadParams {
-    double w[kPhi][32];  // w[k][class]: expanded quadratic-form weights (class padded to 32)
-    double tol[32];      // per-class rounding tolerance; +inf for padded classes
-};
-
-// feature k = 4*ks + kq of phi for this lane's pixel, as selects (no divergent
-// switch, no runtime-indexed array that would spill to scratch)
-template <int KS>
-__device__ __forceinline__ double phi_of(int kq, double r, double g, double b) {
-    if constexpr (KS == 0) return kq == 0 ? r * r : (kq == 1 ? g * g : (kq == 2 ? b * b : r * g));
-    else if constexpr (KS == 1) return kq == 0 ? r * b : (kq == 1 ? g * b : (kq == 2 ? r : g));
-    else return kq == 0 ? b : (kq == 1 ? 1.0 : 0.0);
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
-__global__ __launch_bounds__(256) void classify_mfma_kernel(uint32_t *__restrict__ img, int64_t npix, int nc,
-                                                            ClassParams cp, QuadParams qp) {
+__device__ __forceinline__ uint32_t make_key(float d, uint32_t cls) {
+    return (__float_as_uint(d) & ~31u) | cls;
+}
+
+// same, class index wave-uniform: one v_bfi_b32 (inline 31 + one SGPR), where
+// the plain form needs v_and + v_or (gfx9 VOP3 takes no literal next to an SGPR)
+__device__ __forceinline__ uint32_t make_key_s(float d, uint32_t cls) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, 31, %1, %2" : "=v"(r) : "s"(cls), "v"(__float_as_uint(d)));
+    return r;
+}
+
+// running top-2 over keys (B <= S invariant)
+__device__ __forceinline__ void rank_key(uint32_t k, uint32_t &B, uint32_t &S) {
+    S = umed3(B, k, S);
+    B = min(B, k);
+}
+
+// merge another lane's (B2, S2) into (B, S)
+__device__ __forceinline__ void merge_top2(uint32_t &B, uint32_t &S, uint32_t B2, uint32_t S2) {
+    const uint32_t hi = max(B, B2);
+    S = min(hi, min(S, S2));
+    B = min(B, B2);
+}
+
+// true when the fp32 ranking provably equals the reference's: the second
+// value exceeds the best by more than T2 plus the key truncation (2^-18
+// relative) and the rounding of this very test.
+__device__ __forceinline__ bool decided(uint32_t B, uint32_t S, float T2) {
+    const float vb = __uint_as_float(B & ~31u), vs = __uint_as_float(S & ~31u);
+    return (vs - vb) > fmaf(vs, 0x1p-16f, T2);
+}
+
+__device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_t S, float T2, int nc,
+                                                 const ClassParams &cp, uint32_t *amb) {
+    if (__builtin_expect(decided(B, S, T2), 1)) return (p & 0x00ffffffu) | ((B & 31u) << 24);
+    if (amb) atomicAdd(amb, 1u);
+    return classify_direct(p, nc, cp);
+}
+
+// ---------------------------------------------------------------------------
+// FAST32: VALU, 4 pixels per lane as two packed pairs.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
+                                                              ClassParams cp, FastParams fp, uint32_t *amb) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        const uint4 q = v[i];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        f2_t f[2][9];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t a = px[2 * h], b = px[2 * h + 1];
+            const f2_t r = {(float)(a & 0xffu), (float)(b & 0xffu)};
+            const f2_t g = {(float)((a >> 8) & 0xffu), (float)((b >> 8) & 0xffu)};
+            const f2_t bl = {(float)((a >> 16) & 0xffu), (float)((b >> 16) & 0xffu)};
+            f[h][0] = r * r;
+            f[h][1] = g * g;
+            f[h][2] = bl * bl;
+            f[h][3] = r * g;
+            f[h][4] = r * bl;
+            f[h][5] = g * bl;
+            f[h][6] = r;
+            f[h][7] = g;
+            f[h][8] = bl;
+        }
+        uint32_t B[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
+        uint32_t S[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
+        for (int c = 0; c < nc; ++c) {
+            const float *w = fp.w[c];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f2_t d = {w[9], w[9]};
+#pragma unroll
+                for (int k = 0; k < 9; ++k) d = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d);
+                rank_key(make_key_s(d.x, (uint32_t)c), B[2 * h], S[2 * h]);
+                rank_key(make_key_s(d.y, (uint32_t)c), B[2 * h + 1], S[2 * h + 1]);
+            }
+        }
+        uint4 o;
+        o.x = finish_pixel(q.x, B[0], S[0], fp.T2, nc, cp, amb);
+        o.y = finish_pixel(q.y, B[1], S[1], fp.T2, nc, cp, amb);
+        o.z = finish_pixel(q.z, B[2], S[2], fp.T2, nc, cp, amb);
+        o.w = finish_pixel(q.w, B[3], S[3], fp.T2, nc, cp, amb);
+        v[i] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA32: distance GEMM on v_mfma_f32_32x32x2f32.
+//   D[class][pixel] = sum_k W[class][k] * PHI[k][pixel], K = 10 = 5 MFMAs.
+//   A (W):   lane l holds W[class = l & 31][k = 2t + (l >> 5)]  (loaded once)
+//   B (PHI): lane l holds phi_{2t + (l >> 5)}(pixel l & 31)
+//   D:       lane l, reg r holds class (r & 3) + 8 (r >> 2) + 4 (l >> 5), pixel l & 31
+// A wave takes 128-pixel chunks: lane l loads the 16 B at pixel 4 (l & 31)
+// (both half-waves load the same bytes), and group m = 0..3 uses pixel
+// 4 (l & 31) + m as column l & 31, so every result lands in the lane that
+// owns the pixel's uint4. The two half-waves' top-2 keys are merged with
+// v_permlane32_swap. NREG = accumulator registers with real classes (8 for
+// nc <= 16, 16 for nc <= 32).
+// ---------------------------------------------------------------------------
+template <int NREG>
+__global__ __launch_bounds__(256) void classify_mfma32_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
+                                                              ClassParams cp, FastParams fp, uint32_t *amb) {
     const int lane = threadIdx.x & 63;
-    const int wave = (blockIdx.x * (blockDim.x >> 6)) + (threadIdx.x >> 6);
-    const int nwaves = gridDim.x * (blockDim.x >> 6);
-    const int col = lane & 15;  // pixel within the 16-pixel group
-    const int kq = lane >> 4;   // k row this lane feeds, and class row-block of the result
-    const int ncb = (nc + 15) >> 4;  // 16-class blocks (1 or 2)
-    const int64_t ngroups = (npix + 15) >> 4;
-    for (int64_t g = wave; g < ngroups; g += nwaves) {
-        const int64_t pi = g * 16 + col;
-        const bool valid = pi < npix;
-        const uint32_t p = valid ? img[pi] : 0u;
-        const double r = (double)mpx_px_r(p), gg = (double)mpx_px_g(p), b = (double)mpx_px_b(p);
-        double best = 1.7976931348623157e308, second = 1.7976931348623157e308;
-        double best_tol = 0.0, second_tol = 0.0;
-        int cls = -1;
-        for (int cb = 0; cb < ncb; ++cb) {
-            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-            // A operand: class (lane & 15), k (lane >> 4); B operand: k (lane >> 4), pixel (lane & 15)
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(qp.w[0 + kq][cb * 16 + col], phi_of<0>(kq, r, gg, b), acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(qp.w[4 + kq][cb * 16 + col], phi_of<1>(kq, r, gg, b), acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(qp.w[8 + kq][cb * 16 + col], phi_of<2>(kq, r, gg, b), acc, 0, 0, 0);
-            // lane holds classes cb*16 + kq + 4*reg for pixel col
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    float a[5];
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                const int c = cb * 16 + kq + 4 * reg;
-                const double d = acc[reg];
-                const double t = qp.tol[c];
-                if (c < nc) {
-                    if (d < best) {
-                        second = best;
-                        second_tol = best_tol;
-                        best = d;
-                        best_tol = t;
-                        cls = c;
-                    } else if (d < second) {
-                        second = d;
-                        second_tol = t;
-                    }
-                }
-            }
-        }
-        // merge the 4 lanes (kq = 0..3) that share this pixel: xor 16, xor 32
+    for (int t = 0; t < 5; ++t) a[t] = fp.w[col][2 * t + h];
+    // feature byte offsets for k = 2t + h (see the table in the header)
+    const uint32_t sx0 = 8u * h, sy0 = 8u * h;   // rr | gg
+    const uint32_t sx1 = h ? 0u : 16u;            // bb | rg
+    const uint32_t sy1 = h ? 8u : 16u;
+    const uint32_t sx2 = 8u * h, sy2 = 16u;       // rb | gb
+    const uint32_t sx3 = 8u * h;                  // r  | g
+    const uint32_t tag = 4u * h;                  // class offset of this half-wave's rows
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    for (int64_t ch = wave; ch < nchunks; ch += nwaves) {
+        const uint4 q = v[ch * 32 + col];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        f32x16 acc[4];
 #pragma unroll
-        for (int m = 16; m <= 32; m <<= 1) {
-            const double ob = __shfl_xor(best, m), os = __shfl_xor(second, m);
-            const double obt = __shfl_xor(best_tol, m), ost = __shfl_xor(second_tol, m);
-            const int oc = __shfl_xor(cls, m);
-            // keep lowest class index on exact ties (reference strict '<' order)
-            const bool take = (ob < best) || (ob == best && oc < cls && oc >= 0);
-            double nb, nbt, ns, nst;
-            int nc2;
-            if (take) {
-                nb = ob; nbt = obt; nc2 = oc;
-                // new second = min(best, os)
-                if (best < os) { ns = best; nst = best_tol; } else { ns = os; nst = ost; }
-            } else {
-                nb = best; nbt = best_tol; nc2 = cls;
-                if (ob < second) { ns = ob; nst = obt; } else { ns = second; nst = second_tol; }
-            }
-            best = nb; best_tol = nbt; cls = nc2; second = ns; second_tol = nst;
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t p = px[m];
+            const float phi0 = (float)(__builtin_amdgcn_ubfe(p, sx0, 8) * __builtin_amdgcn_ubfe(p, sy0, 8));
+            const float phi1 = (float)(__builtin_amdgcn_ubfe(p, sx1, 8) * __builtin_amdgcn_ubfe(p, sy1, 8));
+            const float phi2 = (float)(__builtin_amdgcn_ubfe(p, sx2, 8) * __builtin_amdgcn_ubfe(p, sy2, 8));
+            const float phi3 = (float)__builtin_amdgcn_ubfe(p, sx3, 8);
+            const float phi4 = h ? 1.0f : (float)((p >> 16) & 0xffu);
+            f32x16 c = {};
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], phi0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], phi1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], phi2, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], phi3, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4], phi4, c, 0, 0, 0);
+            acc[m] = c;
         }
-        if (valid && kq == 0) {
-            // ambiguous (margin within rounding bounds) or non-finite: exact direct chain
-            const bool ambiguous = !(second - best > best_tol + second_tol) || !(best == best);
-            uint32_t res;
-            if (ambiguous || cls < 0)
-                res = classify_direct(p, nc, cp);
-            else
-                res = (p & 0x00ffffffu) | ((uint32_t)cls << 24);
-            img[pi] = res;
+        uint32_t rb[4], rs[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            uint32_t B = make_key(acc[m][0], 0u), S = kKeyInit;
+#pragma unroll
+            for (int r = 1; r < NREG; ++r) rank_key(make_key(acc[m][r], (uint32_t)((r & 3) + 8 * (r >> 2))), B, S);
+            B |= tag;  // row tags (r & 3) + 8 (r >> 2) never set bit 2
+            S |= tag;
+            const auto sb = __builtin_amdgcn_permlane32_swap(B, B, false, false);
+            const auto ss = __builtin_amdgcn_permlane32_swap(S, S, false, false);
+            // (sb[0], sb[1]) = (own, partner) in either order: the merge is symmetric
+            B = sb[0];
+            S = ss[0];
+            merge_top2(B, S, sb[1], ss[1]);
+            rb[m] = B;
+            rs[m] = S;
+        }
+        if (h == 0) {
+            uint4 o;
+            o.x = finish_pixel(q.x, rb[0], rs[0], fp.T2, nc, cp, amb);
+            o.y = finish_pixel(q.y, rb[1], rs[1], fp.T2, nc, cp, amb);
+            o.z = finish_pixel(q.z, rb[2], rs[2], fp.T2, nc, cp, amb);
+            o.w = finish_pixel(q.w, rb[3], rs[3], fp.T2, nc, cp, amb);
+            v[ch * 32 + col] = o;
         }
     }
 }
 
-bool build_quad(int nc, const double *mu, const double *inv, QuadParams &qp) {
-    const double u = 1.1102230246251565e-16;  // 2^-53
-    for (int k = 0; k < kPhi; ++k)
-        for (int c = 0; c < 32; ++c) qp.w[k][c] = 0.0;
-    for (int c = 0; c < 32; ++c) qp.tol[c] = INFINITY;
+// ---------------------------------------------------------------------------
+// Host: expanded fp32 weights and the rigorous decision margin.
+// ---------------------------------------------------------------------------
+typedef long double ld;
+
+// false when the fp32 decision cannot be proven (non-finite statistics, a
+// symmetrised A that is not positive definite, or magnitudes near fp32 range)
+bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
+    const ld u32 = std::ldexp((ld)1, -24), u64 = std::ldexp((ld)1, -53);
+    const ld g10 = 10 * u32 / (1 - 10 * u32);
+    static const ld phimax[kFeat] = {65025, 65025, 65025, 65025, 65025, 65025, 255, 255, 255, 1};
+    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
     for (int c = 0; c < nc; ++c) {
         const double *A = inv + 9 * c;
-        double S[3][3], Sa[3][3];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) {
-                S[i][j] = 0.5 * (A[3 * i + j] + A[3 * j + i]);
-                Sa[i][j] = 0.5 * (std::fabs(A[3 * i + j]) + std::fabs(A[3 * j + i]));
-            }
-        const double m[3] = {mu[3 * c], mu[3 * c + 1], mu[3 * c + 2]};
+        const double *m = mu + 3 * c;
         for (int i = 0; i < 3; ++i)
             if (!std::isfinite(m[i])) return false;
         for (int i = 0; i < 9; ++i)
             if (!std::isfinite(A[i])) return false;
-        double Sm[3], Sam[3];
+        ld S[3][3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) S[i][j] = ((ld)A[3 * i + j] + (ld)A[3 * j + i]) / 2;
+        // positive definiteness (Cholesky pivots): Q_c >= 0 keeps biased values positive
+        const ld p0 = S[0][0];
+        if (!(p0 > 0)) return false;
+        const ld l10 = S[1][0] / p0, l20 = S[2][0] / p0;
+        const ld p1 = S[1][1] - l10 * S[1][0];
+        if (!(p1 > 0)) return false;
+        const ld l21 = (S[2][1] - l20 * S[1][0]) / p1;
+        const ld p2 = S[2][2] - l20 * S[2][0] - l21 * (S[2][1] - l20 * S[1][0]);
+        if (!(p2 > 0)) return false;
+        ld Sm[3], sabs = 0, dmax[3];
         for (int i = 0; i < 3; ++i) {
             Sm[i] = S[i][0] * m[0] + S[i][1] * m[1] + S[i][2] * m[2];
-            Sam[i] = Sa[i][0] * std::fabs(m[0]) + Sa[i][1] * std::fabs(m[1]) + Sa[i][2] * std::fabs(m[2]);
+            dmax[i] = std::fmax(std::fabs((ld)m[i]), std::fabs(255 - (ld)m[i])) * (1 + 4 * u64);
         }
-        const double mSm = m[0] * Sm[0] + m[1] * Sm[1] + m[2] * Sm[2];
-        const double mSam = std::fabs(m[0]) * Sam[0] + std::fabs(m[1]) * Sam[1] + std::fabs(m[2]) * Sam[2];
-        qp.w[0][c] = S[0][0];
-        qp.w[1][c] = S[1][1];
-        qp.w[2][c] = S[2][2];
-        qp.w[3][c] = 2.0 * S[0][1];
-        qp.w[4][c] = 2.0 * S[0][2];
-        qp.w[5][c] = 2.0 * S[1][2];
-        qp.w[6][c] = -2.0 * Sm[0];
-        qp.w[7][c] = -2.0 * Sm[1];
-        qp.w[8][c] = -2.0 * Sm[2];
-        qp.w[9][c] = mSm;
-        // |terms| bound for any pixel with channels in [0, 255]: sum over the
-        // absolute expanded weights times max|phi| = 255^2 (phi_9 = 1 <= 255^2).
-        // Both the expanded MFMA sum and the reference's direct chain stay
-        // within a few ulps of this bound; 64 u is a wide safety factor, and an
-        // asymmetric A (adjugate rounding) is covered by the |A - A^T| term.
-        double asym = 0.0;
+        w[c][0] = S[0][0];
+        w[c][1] = S[1][1];
+        w[c][2] = S[2][2];
+        w[c][3] = 2 * S[0][1];
+        w[c][4] = 2 * S[0][2];
+        w[c][5] = 2 * S[1][2];
+        w[c][6] = -2 * Sm[0];
+        w[c][7] = -2 * Sm[1];
+        w[c][8] = -2 * Sm[2];
+        w[c][9] = m[0] * Sm[0] + m[1] * Sm[1] + m[2] * Sm[2];
+        // reference fp64 chain: |computed - exact| <= ~8 u sum |A_ij| |d_i| |d_j|; 16 u for margin
+        ld aq = 0;
         for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) asym += std::fabs(A[3 * i + j] - A[3 * j + i]);
-        const double wsum = Sa[0][0] + Sa[1][1] + Sa[2][2] + 2.0 * (Sa[0][1] + Sa[0][2] + Sa[1][2]) +
-                            2.0 * (Sam[0] + Sam[1] + Sam[2]) + mSam;
-        const double pmax = 255.0 + std::fabs(m[0]) + std::fabs(m[1]) + std::fabs(m[2]);
-        qp.tol[c] = 64.0 * u * wsum * 65025.0 + 64.0 * u * asym * pmax * pmax + 1e-300;
+            for (int j = 0; j < 3; ++j) {
+                aq += std::fabs((ld)A[3 * i + j]) * dmax[i] * dmax[j];
+                sabs += std::fabs(S[i][j]);
+            }
+        refb[c] = 16 * u64 * aq;
+        // a slightly indefinite S hidden by long-double rounding: Q >= -1e-15 |S| |d|^2
+        psd[c] = 1e-15L * sabs * (dmax[0] * dmax[0] + dmax[1] * dmax[1] + dmax[2] * dmax[2]);
     }
+    auto tol = [&](int c, ld bias, float *out) -> ld {
+        ld mag = 0, rep = 0, ev = 0;
+        for (int k = 0; k < kFeat; ++k) {
+            const ld wk = w[c][k] + (k == 9 ? bias : 0);
+            const float f = (float)wk;
+            if (out) out[k] = f;
+            rep += std::fabs((ld)f - wk) * phimax[k];
+            ev += std::fabs((ld)f) * phimax[k];
+            mag += std::fabs(wk) * phimax[k];
+        }
+        // fp32 chain + weight rounding + long-double arithmetic slack + reference chain
+        return (g10 * ev + rep + 1e-15L * mag + refb[c] + psd[c]) * 1.001L + 1e-30L;
+    };
+    ld tmax0 = 0, mag = 0;
+    for (int c = 0; c < nc; ++c) {
+        tmax0 = std::fmax(tmax0, tol(c, 0, nullptr));
+        for (int k = 0; k < kFeat; ++k) mag = std::fmax(mag, std::fabs(w[c][k]) * phimax[k]);
+    }
+    if (!(mag < 1e30L)) return false;
+    const ld bias = 4 * tmax0;
+    ld tmax = 0;
+    for (int c = 0; c < nc; ++c) tmax = std::fmax(tmax, tol(c, bias, fp.w[c]));
+    if (!(bias > 2 * tmax)) return false;
+    for (int c = nc; c < MPX_MAX_CLASSES; ++c)
+        for (int k = 0; k < kFeat; ++k) fp.w[c][k] = (k == 9) ? 3.0e38f : 0.0f;
+    float t2 = (float)(2 * tmax);
+    if ((ld)t2 < 2 * tmax) t2 = std::nextafter(t2, INFINITY);
+    fp.T2 = t2;
     return true;
 }
 
 }  // namespace
 
+// AUTO: fp32 VALU up to 16 classes, the MFMA distance GEMM above (measured
+// crossover on MI355X, profiles/round1_kernels.md), DIRECT when the fp32
+// decision cannot be proven for these statistics.
+int classify_choose(int nc, int path, bool fast_ok) {
+    if (path == MPX_CLS_DIRECT || !fast_ok) return MPX_CLS_DIRECT;
+    if (path == MPX_CLS_AUTO) return nc <= 16 ? MPX_CLS_FAST : MPX_CLS_MFMA;
+    return path;
+}
+
 int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid, int block,
-                  int path, void *stream) {
+                  int path, uint32_t *amb, void *stream) {
     MPX_CHECK_ARG(npix >= 0, "npix must be >= 0");
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
     MPX_CHECK_ARG(grid >= 0 && block >= 0 && block <= 1024, "bad launch geometry");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_AUTO, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_FAST, "bad path");
     if (npix == 0) return MPX_OK;
     MPX_CHECK_ARG(img, "null image");
     ClassParams cp{};
     for (int i = 0; i < 3 * nc; ++i) cp.mu[i] = mu[i];
     for (int i = 0; i < 9 * nc; ++i) cp.A[i] = inv[i];
     hipStream_t s = as_stream(stream);
-    bool use_mfma = (path == MPX_CLS_MFMA) || (path == MPX_CLS_AUTO && nc >= 4);
-    QuadParams qp;
-    if (use_mfma && !build_quad(nc, mu, inv, qp)) use_mfma = false;  // non-finite stats: exact path only
-    if (use_mfma) {
-        int blk = 256;
-        int64_t waves_needed = (npix + 15) / 16;
-        int g = grid > 0 ? grid : (int)std::min<int64_t>((waves_needed + 3) / 4, (int64_t)kNumCUs * 8);
-        if (g < 1) g = 1;
-        hipLaunchKernelGGL(classify_mfma_kernel, dim3(g), dim3(blk), 0, s, img, npix, nc, cp, qp);
-    } else {
-        const int vec = aligned16(img) ? 1 : 0;
-        if (block == 0) block = 256;
-        if (grid == 0) {
-            int64_t g = (npix / 4 + block - 1) / block;
-            grid = (int)std::max<int64_t>(1, std::min<int64_t>(g, (int64_t)kNumCUs * 8));
+    FastParams fp;
+    const bool fast_ok = path != MPX_CLS_DIRECT && aligned16(img) && build_fast(nc, mu, inv, fp);
+    const int chosen = classify_choose(nc, path, fast_ok);
+    int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
+    if (chosen == MPX_CLS_MFMA) {
+        const int64_t nchunks = npix / 128;
+        if (nchunks > 0) {
+            const int64_t blocks = (nchunks + 3) / 4;
+            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            if (nc <= 16)
+                hipLaunchKernelGGL(classify_mfma32_kernel<8>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, fp, amb);
+            else
+                hipLaunchKernelGGL(classify_mfma32_kernel<16>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, fp,
+                                   amb);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nchunks * 128;
         }
-        hipLaunchKernelGGL(classify_direct_kernel, dim3(grid), dim3(block), 0, s, img, npix, nc, cp, vec);
+    } else if (chosen == MPX_CLS_FAST) {
+        const int64_t nvec = npix / 4;
+        if (nvec > 0) {
+            const int blk = block > 0 ? block : 256;
+            const int64_t blocks = (nvec + blk - 1) / blk;
+            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            hipLaunchKernelGGL(classify_fast32_kernel, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nvec * 4;
+        }
     }
-    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    if (done < npix) {
+        uint32_t *rest = img + done;
+        const int64_t n = npix - done;
+        const int vec = aligned16(rest) ? 1 : 0;
+        int blk = block > 0 ? block : 256;
+        int g = grid;
+        if (g == 0 || chosen != MPX_CLS_DIRECT) {
+            int64_t want = (n / 4 + blk - 1) / blk;
+            g = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)kNumCUs * 8));
+        }
+        hipLaunchKernelGGL(classify_direct_kernel, dim3(g), dim3(blk), 0, s, rest, n, nc, cp, vec);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    }
     return MPX_OK;
+}
+
+int classify_plan_impl(int nc, const double *mu, const double *inv, int path, float *margin) {
+    MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
+    MPX_CHECK_ARG(mu && inv, "null class parameters");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_FAST, "bad path");
+    FastParams fp;
+    const bool ok = path != MPX_CLS_DIRECT && build_fast(nc, mu, inv, fp);
+    if (margin) *margin = ok ? fp.T2 : 0.0f;
+    return classify_choose(nc, path, ok);
 }
 
 }  // namespace mpx
 
 extern "C" int mpx_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid,
                             int block, int path, void *stream) {
-    return mpx::classify_impl(img, npix, nc, mu, inv, grid, block, path, stream);
+    return mpx::classify_impl(img, npix, nc, mu, inv, grid, block, path, nullptr, stream);
+}
+
+extern "C" int mpx_classify_ex(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid,
+                               int block, int path, uint32_t *ambiguous, void *stream) {
+    return mpx::classify_impl(img, npix, nc, mu, inv, grid, block, path, ambiguous, stream);
+}
+
+extern "C" int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin) {
+    return mpx::classify_plan_impl(nc, mu, inv, path, margin);
 }

@@ -98,3 +98,27 @@ def test_jacobi_cpu_matches_torch():
     expect = ref.jacobi(u, 1, 33)
     assert torch.equal(un[1:33, 1:-1], expect[1:33, 1:-1])
     assert r == float((expect[1:33, 1:-1] - u[1:33, 1:-1]).abs().max())
+
+
+def test_classify_plan_routes():
+    """Host-side path selection of the fp32 classifiers (no GPU needed)."""
+    img = rand_img(64, 64, seed=1)
+    rng = np.random.default_rng(0)
+
+    def stats(nc):
+        return ops.class_stats(img, [rng.integers(0, 64, (30, 2)) for _ in range(nc)])
+
+    mu, inv = stats(4)
+    path, margin = ops.classify_plan(mu, inv, "auto")
+    assert path == "fast" and 0 < margin < 1e-2
+    assert ops.classify_plan(mu, inv, "mfma")[0] == "mfma"
+    assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
+    mu20, inv20 = stats(20)
+    assert ops.classify_plan(mu20, inv20, "auto")[0] == "mfma"
+    # single-point class -> non-finite statistics -> only the exact chain
+    mu_n, inv_n = ops.class_stats(img, [np.array([[0, 0]]), rng.integers(0, 64, (30, 2))])
+    assert ops.classify_plan(mu_n, inv_n, "fast")[0] == "direct"
+    # an indefinite form has no positive lower bound -> direct
+    bad = inv.copy()
+    bad[0] = np.diag([1e-3, -1e-3, 1e-3])
+    assert ops.classify_plan(mu, bad, "auto")[0] == "direct"

@@ -113,10 +113,13 @@ def test_classify_ground_truth(gpu):
     img = bytes_to_img(hex_bytes(os.path.join(LAB3_DATA, "test_01_lab3.txt")))
     mu, inv = ops.class_stats(img, LAB3_CLASSES)
     gt = hex_bytes(os.path.join(LAB3_GT, "test_01_lab3.txt"))
-    for path in ("direct", "mfma", "auto"):
+    for path in CLS_PATHS:
         d = img.to(gpu)
         ops.classify_(d, mu, inv, path=path)
         assert img_to_bytes(d) == gt, path
+
+
+CLS_PATHS = ("direct", "fast", "mfma", "auto")
 
 
 def _random_classes(img, nc, npts, seed):
@@ -126,9 +129,9 @@ def _random_classes(img, nc, npts, seed):
 
 
 @pytest.mark.parametrize("nc", [1, 2, 5, 16, 17, 32])
-@pytest.mark.parametrize("path", ["direct", "mfma"])
+@pytest.mark.parametrize("path", CLS_PATHS)
 def test_classify_matches_cpu(gpu, nc, path):
-    img = smooth_img(193, 211, seed=nc)
+    img = smooth_img(193, 211, seed=nc)  # 40723 pixels: not a multiple of 4 or 128 (tail path)
     mu, inv = ops.class_stats(img, _random_classes(img, nc, 40, nc))
     cpu = img.clone()
     ops.classify_(cpu, mu, inv)
@@ -139,16 +142,66 @@ def test_classify_matches_cpu(gpu, nc, path):
     assert (t[..., 3] != cpu[..., 3]).float().mean() < 1e-3  # torch's summation order differs on near-ties
 
 
+@pytest.mark.parametrize("path", CLS_PATHS)
+def test_classify_random_pixels_and_fallback_rate(gpu, path):
+    """Uniform random pixels (the bench's input): identical classes; the exact
+    fallback stays rare."""
+    img = rand_img(512, 640, seed=11)
+    nc = 24
+    mu, inv = ops.class_stats(img, _random_classes(img, nc, 64, 3))
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    d = img.to(gpu)
+    amb = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.classify_(d, mu, inv, path=path, ambiguous=amb)
+    assert torch.equal(d.cpu(), cpu)
+    if path != "direct":
+        assert amb.item() < 0.01 * img.shape[0] * img.shape[1]
+    else:
+        assert amb.item() == 0
+
+
+@pytest.mark.parametrize("path", ["fast", "mfma"])
+def test_classify_exact_ties_all_fall_back(gpu, path):
+    """Duplicated classes tie exactly on every pixel: every pixel must take the
+    fp64 chain and keep the lowest class index (reference strict '<')."""
+    img = smooth_img(64, 96, seed=4)
+    pts = _random_classes(img, 2, 30, 5)
+    mu, inv = ops.class_stats(img, [pts[0], pts[1], pts[0]])
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    d = img.to(gpu)
+    amb = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.classify_(d, mu, inv, path=path, ambiguous=amb)
+    assert torch.equal(d.cpu(), cpu)
+    assert (cpu[..., 3] != 2).all()
+    assert amb.item() >= int((cpu[..., 3] == 0).sum())  # every class-0 pixel tied with class 2
+
+
+def test_classify_unaligned_view(gpu):
+    img = smooth_img(33, 65, seed=6)
+    mu, inv = ops.class_stats(img, _random_classes(img, 3, 20, 6))
+    flat = img.reshape(-1, 4)
+    cpu = flat[1:].clone()
+    ops.classify_(cpu.reshape(1, -1, 4), mu, inv)
+    dev = flat.to(gpu)
+    view = dev[1:].reshape(1, -1, 4)  # 4-byte offset: not 16-B aligned -> direct kernel
+    for path in CLS_PATHS:  # classification ignores alpha, so re-running in place is idempotent
+        ops.classify_(view, mu, inv, path=path)
+        assert torch.equal(view.reshape(-1, 4).cpu(), cpu), path
+
+
 def test_classify_near_ties_fall_back_exactly(gpu):
-    """Two nearly identical classes: the MFMA path must reproduce the direct chain."""
+    """Two nearly identical classes: the fp32 paths must reproduce the direct chain."""
     img = smooth_img(128, 128, seed=1)
     pts = _random_classes(img, 1, 50, 0)[0]
     mu, inv = ops.class_stats(img, [pts, pts, pts[:-1]])
     cpu = img.clone()
     ops.classify_(cpu, mu, inv)
-    d = img.to(gpu)
-    ops.classify_(d, mu, inv, path="mfma")
-    assert torch.equal(d.cpu(), cpu)
+    for path in ("fast", "mfma"):
+        d = img.to(gpu)
+        ops.classify_(d, mu, inv, path=path)
+        assert torch.equal(d.cpu(), cpu), path
 
 
 def test_classify_single_point_class_nan(gpu):
@@ -157,7 +210,7 @@ def test_classify_single_point_class_nan(gpu):
     mu, inv = ops.class_stats(img, [np.array([[0, 0]]), np.array([[1, 1], [2, 2], [5, 7]])])
     cpu = img.clone()
     ops.classify_(cpu, mu, inv)
-    for path in ("direct", "mfma"):
+    for path in CLS_PATHS:
         d = img.to(gpu)
         ops.classify_(d, mu, inv, path=path)
         assert torch.equal(d.cpu(), cpu)

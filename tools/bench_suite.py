@@ -95,13 +95,16 @@ def bench_lab3(dev, size=8192):
         mu, inv = ops.class_stats(host, pts)
         ref = host.clone()
         cpu = cpu_time_ms(lambda: ops.classify_(ref, mu, inv))
-        for path in ("direct", "mfma"):
+        for path in ("direct", "fast", "mfma", "auto"):
             work = img.clone()
-            us = gpu_time_us(lambda: ops.classify_(work, mu, inv, path=path), iters=5, warmup=1)
+            amb = torch.zeros(1, dtype=torch.int32, device=dev)
+            ops.classify_(work, mu, inv, path=path, ambiguous=amb)
             ok = torch.equal(work.cpu(), ref)
-            emit(workload="lab3_classify", path=path, nc=nc, hw=[size, size], us=round(us, 1),
-                 gpix_s=round(size * size / us / 1e3, 2), cpu_omp_ms=round(cpu, 2),
-                 speedup_vs_cpu=round(cpu * 1e3 / us, 1), verified=ok)
+            us = gpu_time_us(lambda: ops.classify_(work, mu, inv, path=path), iters=5, warmup=1)
+            emit(workload="lab3_classify", path=path, ran=ops.classify_plan(mu, inv, path)[0], nc=nc,
+                 hw=[size, size], us=round(us, 1), gpix_s=round(size * size / us / 1e3, 2),
+                 cpu_omp_ms=round(cpu, 2), speedup_vs_cpu=round(cpu * 1e3 / us, 1), verified=ok,
+                 fallback_pixels=int(amb.item()))
             del work
 
 
