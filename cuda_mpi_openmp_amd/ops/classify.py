@@ -46,7 +46,8 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``direct`` — the reference fp64 FMA chain;
       * ``fast``   — fp32 packed-VALU distances;
       * ``mfma``   — fp32 MFMA distance GEMM (v_mfma_f32_32x32x2f32);
-      * ``auto``   — fast for nc <= 16, mfma above.
+      * ``auto``   — ``fast`` (measured fastest at every nc on MI355X: the f32
+        MFMA shares the VALU's fp32 datapath on gfx950).
     The fp32 paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes

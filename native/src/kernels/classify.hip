@@ -16,8 +16,10 @@
 //     classes are bit-identical to mpx_cpu_classify. fp64 VALU runs at half the
 //     fp32 rate, so this path is VALU-bound at ~19 fp64 ops per (pixel, class).
 //   * FAST32 and MFMA32 decide in fp32 and prove the decision:
-//       Q_c(p) = sum_k w_ck phi_k(p),  phi = [r^2 g^2 b^2 rg rb gb r g b 1]
-//     (the expanded quadratic form of the symmetrised A_c). The host bounds
+//       Q_c(p) = sum_k w_ck phi_k(q),  phi = [r^2 g^2 b^2 rg rb gb r g b 1](q)
+//     with q = p - 128 per channel (the expanded quadratic form of the
+//     symmetrised A_c around the cube centre: |q| <= 128 keeps every term,
+//     and so the rounding bound, ~4x smaller than around 0). The host bounds
 //     |fp32 evaluation - reference fp64 chain| by tol_c for every pixel in
 //     [0,255]^3 (rounding of the weights, of the 10-term fmaf chain and of the
 //     reference chain itself). A pixel is classified in fp32 only if the
@@ -139,12 +141,14 @@ __device__ __forceinline__ void merge_top2(uint32_t &B, uint32_t &S, uint32_t B2
     B = min(B, B2);
 }
 
-// true when the fp32 ranking provably equals the reference's: the second
-// value exceeds the best by more than T2 plus the key truncation (2^-18
-// relative) and the rounding of this very test.
+// true when the fp32 ranking provably equals the reference's. Keys lose at
+// most 2^-18 of their value to the class tag, so it suffices that
+// vs - vb > T2 + vb 2^-17 exactly; evaluating the test in fp32 costs at most
+// 2^-23 relative on each side, covered by the 1.125 factor on vs >= vb and
+// the host's (1 + 2^-20) inflation of T2.
 __device__ __forceinline__ bool decided(uint32_t B, uint32_t S, float T2) {
     const float vb = __uint_as_float(B & ~31u), vs = __uint_as_float(S & ~31u);
-    return (vs - vb) > fmaf(vs, 0x1p-16f, T2);
+    return (vs - vb) > fmaf(vs, 0x1.2p-17f, T2);
 }
 
 __device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_t S, float T2, int nc,
@@ -167,10 +171,15 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         f2_t f[2][9];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+            // channel - 128, exact in fp32 (v_cvt_f32_ubyteN + one packed add).
+            // NB: (float)__builtin_amdgcn_sbfe(x, o, 8) is miscompiled by hipcc
+            // 7.2 into v_cvt_f32_u32_sdwa sext(x) (negative values convert as
+            // unsigned), so signed bytes are never converted directly.
             const uint32_t a = px[2 * h], b = px[2 * h + 1];
-            const f2_t r = {(float)(a & 0xffu), (float)(b & 0xffu)};
-            const f2_t g = {(float)((a >> 8) & 0xffu), (float)((b >> 8) & 0xffu)};
-            const f2_t bl = {(float)((a >> 16) & 0xffu), (float)((b >> 16) & 0xffu)};
+            const f2_t c128 = {-128.0f, -128.0f};
+            const f2_t r = f2_t{(float)(a & 0xffu), (float)(b & 0xffu)} + c128;
+            const f2_t g = f2_t{(float)((a >> 8) & 0xffu), (float)((b >> 8) & 0xffu)} + c128;
+            const f2_t bl = f2_t{(float)((a >> 16) & 0xffu), (float)((b >> 16) & 0xffu)} + c128;
             f[h][0] = r * r;
             f[h][1] = g * g;
             f[h][2] = bl * bl;
@@ -241,12 +250,15 @@ __global__ __launch_bounds__(256) void classify_mfma32_kernel(uint32_t *__restri
         f32x16 acc[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            const uint32_t p = px[m];
-            const float phi0 = (float)(__builtin_amdgcn_ubfe(p, sx0, 8) * __builtin_amdgcn_ubfe(p, sy0, 8));
-            const float phi1 = (float)(__builtin_amdgcn_ubfe(p, sx1, 8) * __builtin_amdgcn_ubfe(p, sy1, 8));
-            const float phi2 = (float)(__builtin_amdgcn_ubfe(p, sx2, 8) * __builtin_amdgcn_ubfe(p, sy2, 8));
-            const float phi3 = (float)__builtin_amdgcn_ubfe(p, sx3, 8);
-            const float phi4 = h ? 1.0f : (float)((p >> 16) & 0xffu);
+            // signed bytes (channel - 128) feed the exact integer products; the
+            // single-channel features convert the unsigned byte and subtract 128
+            // (see the sbfe miscompile note in the FAST32 kernel)
+            const int p = (int)(px[m] ^ 0x80808080u);
+            const float phi0 = (float)(__mul24(__builtin_amdgcn_sbfe(p, sx0, 8), __builtin_amdgcn_sbfe(p, sy0, 8)));
+            const float phi1 = (float)(__mul24(__builtin_amdgcn_sbfe(p, sx1, 8), __builtin_amdgcn_sbfe(p, sy1, 8)));
+            const float phi2 = (float)(__mul24(__builtin_amdgcn_sbfe(p, sx2, 8), __builtin_amdgcn_sbfe(p, sy2, 8)));
+            const float phi3 = (float)__builtin_amdgcn_ubfe(px[m], sx3, 8) - 128.0f;
+            const float phi4 = h ? 1.0f : (float)((px[m] >> 16) & 0xffu) - 128.0f;
             f32x16 c = {};
             c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], phi0, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], phi1, c, 0, 0, 0);
@@ -293,13 +305,15 @@ typedef long double ld;
 bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
     const ld u32 = std::ldexp((ld)1, -24), u64 = std::ldexp((ld)1, -53);
     const ld g10 = 10 * u32 / (1 - 10 * u32);
-    static const ld phimax[kFeat] = {65025, 65025, 65025, 65025, 65025, 65025, 255, 255, 255, 1};
+    // |q_i q_j| <= 128^2, |q_i| <= 128 for q = p - 128, p in [0, 255]^3
+    static const ld phimax[kFeat] = {16384, 16384, 16384, 16384, 16384, 16384, 128, 128, 128, 1};
     ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
     for (int c = 0; c < nc; ++c) {
         const double *A = inv + 9 * c;
-        const double *m = mu + 3 * c;
+        const double *mraw = mu + 3 * c;
         for (int i = 0; i < 3; ++i)
-            if (!std::isfinite(m[i])) return false;
+            if (!std::isfinite(mraw[i])) return false;
+        const ld m[3] = {(ld)mraw[0] - 128, (ld)mraw[1] - 128, (ld)mraw[2] - 128};  // centred mean (exact)
         for (int i = 0; i < 9; ++i)
             if (!std::isfinite(A[i])) return false;
         ld S[3][3];
@@ -317,7 +331,7 @@ bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
         ld Sm[3], sabs = 0, dmax[3];
         for (int i = 0; i < 3; ++i) {
             Sm[i] = S[i][0] * m[0] + S[i][1] * m[1] + S[i][2] * m[2];
-            dmax[i] = std::fmax(std::fabs((ld)m[i]), std::fabs(255 - (ld)m[i])) * (1 + 4 * u64);
+            dmax[i] = std::fmax(std::fabs((ld)mraw[i]), std::fabs(255 - (ld)mraw[i])) * (1 + 4 * u64);
         }
         w[c][0] = S[0][0];
         w[c][1] = S[1][1];
@@ -365,20 +379,25 @@ bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
     if (!(bias > 2 * tmax)) return false;
     for (int c = nc; c < MPX_MAX_CLASSES; ++c)
         for (int k = 0; k < kFeat; ++k) fp.w[c][k] = (k == 9) ? 3.0e38f : 0.0f;
-    float t2 = (float)(2 * tmax);
-    if ((ld)t2 < 2 * tmax) t2 = std::nextafter(t2, INFINITY);
+    const ld t2x = 2 * tmax * (1 + std::ldexp((ld)1, -20));  // see decided()
+    float t2 = (float)t2x;
+    if ((ld)t2 < t2x) t2 = std::nextafter(t2, INFINITY);
     fp.T2 = t2;
     return true;
 }
 
 }  // namespace
 
-// AUTO: fp32 VALU up to 16 classes, the MFMA distance GEMM above (measured
-// crossover on MI355X, profiles/round1_kernels.md), DIRECT when the fp32
-// decision cannot be proven for these statistics.
+// AUTO: FAST32, DIRECT when the fp32 decision cannot be proven for these
+// statistics. Measured on MI355X (profiles/lab3_classify.md): the f32 MFMA and
+// the f32 VALU share one datapath on gfx950 — SQ_VALU_MFMA_BUSY_CYCLES and the
+// VALU issue cycles ADD UP to the kernel time — so the distance GEMM cannot hide
+// the ranking work behind the matrix core, and FAST32 is as fast or faster at
+// every class count (nc = 4: 132 vs 546 us, nc = 32: 677 vs 689 us at 8192^2).
 int classify_choose(int nc, int path, bool fast_ok) {
+    (void)nc;
     if (path == MPX_CLS_DIRECT || !fast_ok) return MPX_CLS_DIRECT;
-    if (path == MPX_CLS_AUTO) return nc <= 16 ? MPX_CLS_FAST : MPX_CLS_MFMA;
+    if (path == MPX_CLS_AUTO) return MPX_CLS_FAST;
     return path;
 }
 

@@ -2,14 +2,26 @@
 // BASELINE.json, re-expressed over RCCL): slab rows with one halo row above
 // and below, Dirichlet columns 0 and cols-1, fused L-infinity residual.
 //
-// MI355X design: HBM-bound 5-point stencil. Each lane owns a 16-B column
-// vector (double2 / float4) and slides down kRows rows keeping the up/centre
-// rows in registers, so each input row is fetched from HBM once per sweep; the
-// left/right neighbours at the vector edges come from the L1 (the adjacent
-// lanes just loaded them). The residual is reduced wave -> lane 0 -> one
-// device-scope atomic max per wave on the bit pattern (non-negative IEEE
-// values order like unsigned integers), so no second kernel is needed.
+// MI355X design: HBM-bound 5-point stencil (2 x 8 B per fp64 point).
+//   * wave strips: a wave owns a strip of 62 16-B column vectors (lanes 1..62
+//     compute, lanes 0 and 63 only load the strip's halo vectors) and walks
+//     R rows down it, so every input row is fetched once per sweep and the
+//     left/right neighbours of a vector come from the adjacent lanes through
+//     DPP wave shifts (v_mov_dpp wave_shr:1 / wave_shl:1) — one 16-B load per
+//     lane and row, nothing re-read through L1;
+//   * a 5-slot row ring of unconditional (clamped) loads, unrolled by 5 so the
+//     slots are compile-time registers, keeps three rows of HBM requests in
+//     flight per wave; stores are raw buffer stores whose
+//     masked-off lanes get an out-of-range offset, so there is no divergent
+//     store branch to break the compiler's vmcnt accounting;
+//   * the residual is reduced wave -> lane 0 -> one device-scope atomic max per
+//     wave on the bit pattern (non-negative IEEE values order like unsigned
+//     integers), so no second kernel is needed.
+// Pitches or widths that are not a multiple of the vector width use the
+// generic per-lane kernel below.
 #include "internal.hpp"
+
+#include <type_traits>
 
 namespace mpx {
 namespace {
@@ -113,12 +125,141 @@ __global__ __launch_bounds__(256) void jacobi_kernel(const T *__restrict__ u, T 
     }
 }
 
+// ---------------------------------------------------------------------------
+// wave-strip kernel (16-B vectors, cols % NV == 0, pitch % NV == 0)
+// ---------------------------------------------------------------------------
+constexpr int kStripVec = 62;             // output vectors per wave
+constexpr uint32_t kDrop = 0x7ffffff0u;   // buffer offset past any range: store dropped
+
+template <typename T> struct JWide;
+template <> struct JWide<double> { typedef double type __attribute__((ext_vector_type(2))); };
+template <> struct JWide<float> { typedef float type __attribute__((ext_vector_type(4))); };
+
+template <typename T>
+__device__ __forceinline__ T dpp_shift(T v, int ctrl) {
+    if constexpr (sizeof(T) == 8) {
+        const uint2 b = __builtin_bit_cast(uint2, v);
+        uint2 r;
+        if (ctrl == 0x138) {
+            r.x = __builtin_amdgcn_mov_dpp((int)b.x, 0x138, 0xf, 0xf, true);
+            r.y = __builtin_amdgcn_mov_dpp((int)b.y, 0x138, 0xf, 0xf, true);
+        } else {
+            r.x = __builtin_amdgcn_mov_dpp((int)b.x, 0x130, 0xf, 0xf, true);
+            r.y = __builtin_amdgcn_mov_dpp((int)b.y, 0x130, 0xf, 0xf, true);
+        }
+        return __builtin_bit_cast(T, r);
+    } else {
+        const int b = __builtin_bit_cast(int, v);
+        return __builtin_bit_cast(T, ctrl == 0x138 ? __builtin_amdgcn_mov_dpp(b, 0x138, 0xf, 0xf, true)
+                                                   : __builtin_amdgcn_mov_dpp(b, 0x130, 0xf, 0xf, true));
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
+                                                          int pitch, int r0, int r1, int strips, int rows_per_wave,
+                                                          int nwaves, T *__restrict__ resid) {
+    using V = typename JWide<T>::type;
+    constexpr int NV = JVec<T>::n;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    T rmax = (T)0;
+    if (wave < nwaves) {
+        const int strip = wave % strips;  // consecutive waves: adjacent strips of the same rows
+        const int rb = wave / strips;
+        const int nvec = cols / NV;
+        const int cv = strip * kStripVec - 1 + lane;  // this lane's column vector
+        const bool out_lane = lane >= 1 && lane <= kStripVec && cv < nvec;
+        const int cvc = min(max(cv, 0), nvec - 1);
+        const int i0 = r0 + rb * rows_per_wave;
+        const int i1 = min(i0 + rows_per_wave, r1);
+        const T *base = u + (int64_t)cvc * NV;
+        auto ld = [&](int i) { return *reinterpret_cast<const V *>(base + (int64_t)i * pitch); };
+        // ring: row x_{i0-1+t} lives in slot t % 5; the loop advances 5 rows so
+        // every slot index is a compile-time constant (no register rotation,
+        // whose moves would force a wait on the in-flight prefetch)
+        V S[5];
+        S[0] = ld(i0 - 1);
+        S[1] = ld(i0);
+        S[2] = ld(min(i0 + 1, i1));
+        S[3] = ld(min(i0 + 2, i1));
+        S[4] = V{};  // first written by step 0; a copy of S[3] would wait on its load
+        const uint32_t soff = out_lane ? (uint32_t)(cv * NV * sizeof(T)) : kDrop;
+        const int j0 = cv * NV;
+        __builtin_amdgcn_sched_barrier(0);
+        auto step = [&](auto kc, int i) {
+            constexpr int k = decltype(kc)::value;
+            const int r = i + k;                   // row computed in this step
+            S[(k + 4) % 5] = ld(min(r + 3, i1));   // x_{r+3} replaces x_{r-2}
+            const V up = S[k % 5], cen = S[(k + 1) % 5], dn = S[(k + 2) % 5];
+            const T left = dpp_shift<T>(cen[NV - 1], 0x138);  // lane - 1's last element
+            const T right = dpp_shift<T>(cen[0], 0x130);      // lane + 1's first element
+            V res;
+#pragma unroll
+            for (int e = 0; e < NV; ++e) {
+                const int j = j0 + e;
+                const T l = e == 0 ? left : cen[e - 1];
+                const T rr = e == NV - 1 ? right : cen[e + 1];
+                const T sm = ((up[e] + dn[e]) + (l + rr)) * (T)0.25;
+                const bool interior = j > 0 && j < cols - 1;
+                res[e] = interior ? sm : cen[e];
+                const T d = sm > cen[e] ? sm - cen[e] : cen[e] - sm;
+                rmax = fmax(rmax, (interior && out_lane) ? d : (T)0);  // select + v_max: no exec branch
+            }
+            // rows past i1 (tail group) store nowhere: offset out of range
+            const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
+                un + (int64_t)min(r, i1 - 1) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, 0);
+            // keep each step's prefetch at its start: the scheduler otherwise sinks
+            // loads past the next step's use and the wait counts collapse to 0
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        using I4 = std::integral_constant<int, 4>;
+        // straight-line groups of 5 rows; the last group's surplus rows are
+        // computed on clamped data and dropped by the buffer store
+        for (int i = i0; i < i1; i += 5) {
+            step(I0{}, i);
+            step(I1{}, i);
+            step(I2{}, i);
+            step(I3{}, i);
+            step(I4{}, i);
+        }
+    }
+    if (resid) {
+        using B = typename JVec<T>::bits;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const T o = __shfl_xor(rmax, m);
+            rmax = o > rmax ? o : rmax;
+        }
+        if ((threadIdx.x & 63) == 0 && rmax > (T)0) atomicMax(reinterpret_cast<B *>(resid), __builtin_bit_cast(B, rmax));
+    }
+}
+
 template <typename T>
 int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *resid, void *stream) {
     MPX_CHECK_ARG(u && un, "null pointer");
     MPX_CHECK_ARG(cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0, "bad slab geometry");
     if (r1 == r0) return MPX_OK;
     constexpr int NV = JVec<T>::n;
+    if ((pitch % NV == 0) && (cols % NV == 0) && aligned16(u) && aligned16(un)) {
+        const int strips = (cols / NV + kStripVec - 1) / kStripVec;
+        const int rows = r1 - r0;
+        // long row runs amortise the two halo rows; shorten them until the
+        // launch has >= 16384 waves (16 per SIMD)
+        int R = 64;
+        while (R > 4 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
+        const int nwaves = strips * ((rows + R - 1) / R);
+        hipLaunchKernelGGL((jacobi_wave_kernel<T>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
+                           cols, pitch, r0, r1, strips, R, nwaves, resid);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        return MPX_OK;
+    }
     const bool vec = (pitch % NV == 0) && aligned16(u) && aligned16(un);
     const int lanes = vec ? (cols + NV - 1) / NV : cols;
     const dim3 blk(256);

@@ -6,7 +6,7 @@
 // 16-B loads per operand in flight per grid-stride step, and writes with
 // non-temporal stores because the result is never re-read by this kernel.
 // Launch geometry is honoured exactly when the caller passes one (the harness
-// sweeps [grid, block] pairs); 0/0 picks a grid that fills the 256 CUs.
+// sweeps [grid, block] pairs); 0/0 picks one vector per thread (see below).
 #include "internal.hpp"
 
 namespace mpx {
@@ -64,14 +64,20 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
     if (n == 0) return MPX_OK;
     MPX_CHECK_ARG(a && b && c, "null pointer");
     const bool vec = aligned16(a) && aligned16(b) && aligned16(c);
-    if (block == 0) block = 256;
     if (grid == 0) {
-        // fill every CU with 8 resident 256-thread blocks, grid-stride the rest
-        const int64_t per_block = (int64_t)block * Vec16<T>::n * 4;
+        // one 16-B vector per thread in 1024-thread blocks: measured on MI355X
+        // at 2^26 fp32 / 2^25 fp64 (tools/vsub_sweep.py, profiles/lab1_vsub.md)
+        // 5.95 / 6.06 TB/s, = torch's own elementwise kernel, against 4.3-5.8
+        // TB/s for persistent grid-stride geometries (2048x256 .. 256x256):
+        // with one access per wave in flight per address range, the DRAM
+        // pages are consumed in order instead of by 4 strided streams per wave
+        if (block == 0) block = 1024;
+        const int64_t per_block = (int64_t)block * (vec ? Vec16<T>::n : 1);
         int64_t g = (n + per_block - 1) / per_block;
-        const int64_t cap = (int64_t)kNumCUs * 8;
+        const int64_t cap = (int64_t)1 << 30;
         grid = (int)(g < 1 ? 1 : (g > cap ? cap : g));
     }
+    if (block == 0) block = 256;
     if (vec)
         hipLaunchKernelGGL(vsub_vec_kernel<T>, dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     else

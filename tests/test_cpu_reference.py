@@ -114,7 +114,8 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu, inv, "mfma")[0] == "mfma"
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
     mu20, inv20 = stats(20)
-    assert ops.classify_plan(mu20, inv20, "auto")[0] == "mfma"
+    assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
+    assert ops.classify_plan(mu20, inv20, "mfma")[0] == "mfma"
     # single-point class -> non-finite statistics -> only the exact chain
     mu_n, inv_n = ops.class_stats(img, [np.array([[0, 0]]), rng.integers(0, 64, (30, 2))])
     assert ops.classify_plan(mu_n, inv_n, "fast")[0] == "direct"
