@@ -18,7 +18,6 @@ HIPFLAGS  := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC
              -ffp-contract=off -Wall -Wno-unused-function $(INC)
 COPT      := -O3 -fopenmp -ffp-contract=off -fPIC -Wall -std=gnu11 -Inative/include
 CSER      := -O0 -ffp-contract=off -Wall -Wno-unknown-pragmas -std=gnu11 -Inative/include
-RCCL_LIBS := -L$(ROCM)/lib -lrccl
 
 B         := build
 PYLIB     := cuda_mpi_openmp_amd/_lib/libmpx.so
@@ -26,7 +25,7 @@ ALIB      := $(B)/libmpx.a
 
 HIP_SRCS  := $(wildcard native/src/kernels/*.hip)
 HIP_OBJS  := $(patsubst native/src/kernels/%.hip,$(B)/k_%.o,$(HIP_SRCS))
-CORE_OBJS := $(B)/capi.o
+CORE_OBJS := $(B)/capi.o $(B)/comm.o
 CPU_OBJ   := $(B)/cpu_kernels.o
 LIB_OBJS  := $(HIP_OBJS) $(CORE_OBJS) $(CPU_OBJ)
 HDRS      := $(wildcard native/include/mpx/*.h native/include/mpx/*.hpp native/src/kernels/*.hpp native/src/cpu/*.h)
@@ -56,21 +55,25 @@ $(B)/k_classify.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 $(B)/capi.o: native/src/core/capi.cpp $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# RCCL is not linked: comm.cpp binds the librccl torch already loaded (dlsym)
+$(B)/comm.o: native/src/core/comm.cpp $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(B)/cpu_kernels.o: native/src/cpu/cpu_kernels.c $(HDRS) | $(B)
 	$(CC) $(COPT) -c $< -o $@
 
 $(PYLIB): $(LIB_OBJS) | $(B)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(LIB_OBJS) -lgomp -lm
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(LIB_OBJS) -lgomp -lm -ldl
 
 $(ALIB): $(LIB_OBJS) | $(B)
 	rm -f $@ && ar rcs $@ $(LIB_OBJS)
 
 # ---- GPU programs: two personalities from one source ----
 labs/lab%/src/to_plot_hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -o $@
+	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
 
 labs/lab%/src/hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -DMPX_SUBMISSION $< -x none $(ALIB) -lgomp -lm -o $@
+	$(HIPCC) $(HIPFLAGS) -DMPX_SUBMISSION $< -x none $(ALIB) -lgomp -lm -ldl -o $@
 
 # ---- CPU references: serial -O0 (published methodology) and OpenMP -O3 ----
 labs/lab%/src/cpu_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS)
@@ -83,7 +86,7 @@ labs/lab3/src/read_input_exe: native/apps/lab3_read_input.c
 	$(CC) $(CSER) $< -o $@
 
 bin/gpu_info: native/apps/gpu_info.cpp $(ALIB) $(HDRS) | $(B)
-	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -o $@
+	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
 
 bin/hw1: native/apps/hw1_quadratic.c | $(B)
 	$(CC) $(CSER) $< -lm -o $@

@@ -54,6 +54,20 @@ _SIGNATURES = {
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
     "mpx_classify": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp]),
+    "mpx_comm_load": (c_int, [ctypes.c_char_p]),
+    "mpx_comm_version": (c_int, []),
+    "mpx_comm_unique_id": (c_int, [c_vp, c_int]),
+    "mpx_comm_init": (c_int, [ctypes.POINTER(c_vp), c_int, c_int, c_vp, c_int, c_int]),
+    "mpx_comm_destroy": (c_int, [c_vp]),
+    "mpx_comm_rank": (c_int, [c_vp]),
+    "mpx_comm_size": (c_int, [c_vp]),
+    "mpx_comm_p2p_start": (c_int, [c_vp, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_vp),
+                                   ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp]),
+    "mpx_comm_p2p_wait": (c_int, [c_vp, c_vp]),
+    "mpx_comm_p2p": (c_int, [c_vp, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_vp),
+                             ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp]),
+    "mpx_comm_allreduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "mpx_comm_check": (c_int, [c_vp]),
     "mpx_classify_ex": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_classify_plan": (c_int, [c_int, _dp, _dp, c_int, ctypes.POINTER(ctypes.c_float)]),
     "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),

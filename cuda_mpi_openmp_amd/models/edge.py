@@ -41,16 +41,30 @@ class SlabEdgeDetector:
     """One rank's share of a row-decomposed image convolution."""
 
     def __init__(self, ctx: DistContext, global_h: int, w: int, filt: str | Filter = "sobel5",
-                 overlap: bool = True):
+                 overlap: bool | str = "auto"):
         self.ctx = ctx
         self.filter = get_filter(filt) if isinstance(filt, str) else filt
         self.w = w
         self.slab = Slab(global_h, ctx.world, ctx.rank, self.filter.halo_up, self.filter.halo_down)
         self.halo = HaloExchange(self.slab, ctx)
-        self.overlap = overlap
+        # "auto": with the native RCCL tier the exchange runs in order on the
+        # compute stream and one launch convolves every row — measured faster
+        # than forking the transfer onto a second queue (the RCCL kernel then
+        # shares the CUs with the convolution and each cross-queue join costs
+        # 7-16 us; profiles/comm_step.md); torch.distributed keeps the overlap.
+        if overlap == "auto":
+            overlap = ctx.native is None
+        self.overlap = bool(overlap)
         dev = ctx.device
         self.buf = torch.empty((self.slab.buffer_rows, w, 4), dtype=torch.uint8, device=dev)
         self.out = torch.empty((self.slab.rows, w, 4), dtype=torch.uint8, device=dev)
+        # pre-validated launches for the three row ranges of a step
+        s = self.slab
+        mk = lambda a, b: ops.ConvLauncher(self.buf, self.out, self.filter, src_row0=s.own_offset,  # noqa: E731
+                                          out_row0=0, oy0=a, oy1=b, y_lo=s.y_lo, y_hi=s.y_hi)
+        self._all = mk(0, s.rows)
+        self._interior = mk(*s.interior())
+        self._boundary = [mk(a, b) for a, b in s.boundary()]
 
     @property
     def own(self) -> torch.Tensor:
@@ -72,18 +86,17 @@ class SlabEdgeDetector:
 
     def step(self) -> torch.Tensor:
         """Exchange halos and convolve every owned row; returns the output slab."""
-        s = self.slab
+        st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
         if not self.ctx.is_distributed:
-            self._rows(0, s.rows)
+            self._all(st)
             return self.out
         if self.overlap:
             self.halo.start(self.buf)       # RCCL waits only for work queued so far
-            a, b = s.interior()
-            self._rows(a, b)                # overlaps the halo transfer
+            self._interior(st)              # overlaps the halo transfer
             self.halo.wait()                # current stream waits for the halo rows
-            for a2, b2 in s.boundary():
-                self._rows(a2, b2)
+            for launch in self._boundary:
+                launch(st)
         else:
             self.halo.exchange(self.buf)
-            self._rows(0, s.rows)
+            self._all(st)
         return self.out

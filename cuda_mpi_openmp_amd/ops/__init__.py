@@ -3,7 +3,7 @@ OpenMP C references (CPU tensors) of libmpx."""
 
 from .classify import class_stats, classify_
 from .classify import plan as classify_plan
-from .edge import conv, conv_rows, roberts
+from .edge import ConvLauncher, conv, conv_rows, roberts
 from .filters import Filter, get_filter, list_filters
 from .stencil import jacobi_sweep
 from .vector import vsub
@@ -13,6 +13,7 @@ __all__ = [
     "classify_",
     "classify_plan",
     "conv",
+    "ConvLauncher",
     "conv_rows",
     "roberts",
     "Filter",

@@ -43,25 +43,17 @@ def roberts(img: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
-def conv_rows(src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
-              oy0: int, oy1: int, y_lo: int, y_hi: int, direct: bool = False) -> None:
-    """Low-level KxK conv over logical rows [oy0, oy1).
-
-    ``src`` / ``out`` are (rows, W, 4) buffers whose logical row 0 is at
-    ``src_row0`` / ``out_row0``; reads are clamped into logical rows
-    [y_lo, y_hi] (negative / past-the-end rows are resident halo rows).
-    """
+def _conv_args(src: torch.Tensor, out: torch.Tensor, filt: Filter, src_row0: int, out_row0: int, oy0: int,
+               oy1: int, y_lo: int, y_hi: int) -> tuple:
     hs, w = check_image(src, "src")
     ho, wo = check_image(out, "out")
     if wo != w or src.device != out.device:
         raise ValueError("src/out width or device mismatch")
-    if oy1 <= oy0:
-        return
     if not (0 <= src_row0 + y_lo and src_row0 + y_hi < hs):
         raise ValueError("clamp rows fall outside the source buffer")
-    if not (0 <= out_row0 + oy0 and out_row0 + oy1 <= ho):
+    if oy1 > oy0 and not (0 <= out_row0 + oy0 and out_row0 + oy1 <= ho):
         raise ValueError("output rows fall outside the output buffer")
-    if not (y_lo <= oy0 and oy1 - 1 <= y_hi):
+    if oy1 > oy0 and not (y_lo <= oy0 and oy1 - 1 <= y_hi):
         raise ValueError("output rows must lie inside the clamp range")
     # the C ABI indexes src and out by the same logical row, so each base pointer
     # is shifted to its own logical row 0
@@ -70,13 +62,54 @@ def conv_rows(src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: i
     sp = src.data_ptr() + src_row0 * row_bytes
     op = out.data_ptr() + out_row0 * row_bytes
     wx, wy = filt.c_taps()
+    return (sp, op, w, pitch, oy0, oy1, y_lo, y_hi, filt.k, filt.anchor, filt.mode, wx, wy)
+
+
+def conv_rows(src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
+              oy0: int, oy1: int, y_lo: int, y_hi: int, direct: bool = False) -> None:
+    """Low-level KxK conv over logical rows [oy0, oy1).
+
+    ``src`` / ``out`` are (rows, W, 4) buffers whose logical row 0 is at
+    ``src_row0`` / ``out_row0``; reads are clamped into logical rows
+    [y_lo, y_hi] (negative / past-the-end rows are resident halo rows).
+    """
+    args = _conv_args(src, out, filt, src_row0, out_row0, oy0, oy1, y_lo, y_hi)
+    if oy1 <= oy0:
+        return
     L = _native.lib()
     if src.is_cuda:
         fn = L.mpx_conv_direct if direct else L.mpx_conv
-        _native.check(fn(sp, op, w, pitch, oy0, oy1, y_lo, y_hi, filt.k, filt.anchor, filt.mode, wx, wy,
-                         _native.stream_of(src)))
+        _native.check(fn(*args, _native.stream_of(src)))
     else:
-        L.mpx_cpu_conv(sp, op, w, pitch, oy0, oy1, y_lo, y_hi, filt.k, filt.anchor, filt.mode, wx, wy)
+        L.mpx_cpu_conv(*args)
+
+
+class ConvLauncher:
+    """A validated ``conv_rows`` launch bound to fixed buffers and rows.
+
+    Hot loops (model steps, the benchmark) call it with the stream handle they
+    already hold: one ctypes call, no argument checks, no tap re-marshalling.
+    The launcher keeps ``src``/``out`` alive; it must not outlive a resize.
+    """
+
+    def __init__(self, src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
+                 oy0: int, oy1: int, y_lo: int, y_hi: int):
+        self.args = _conv_args(src, out, filt, src_row0, out_row0, oy0, oy1, y_lo, y_hi)
+        self.empty = oy1 <= oy0
+        self.cuda = src.is_cuda
+        L = _native.lib()
+        self.fn = L.mpx_conv if self.cuda else L.mpx_cpu_conv
+        self._keep = (src, out)
+
+    def __call__(self, stream: Optional[int] = None) -> None:
+        if self.empty:
+            return
+        if self.cuda:
+            rc = self.fn(*self.args, stream)
+            if rc:
+                _native.check(rc)
+        else:
+            self.fn(*self.args)
 
 
 def conv(img: torch.Tensor, filt="sobel5", out: Optional[torch.Tensor] = None, direct: bool = False) -> torch.Tensor:

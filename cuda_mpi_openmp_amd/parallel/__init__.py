@@ -3,6 +3,7 @@
 from .collectives import all_reduce_max, all_reduce_sum, broadcast_object, gather_slabs, max_over_ranks, scatter_rows
 from .dist import DistContext, context, init, shutdown
 from .halo import HaloExchange
+from .native_comm import NativeComm, P2PPlan
 from .slab import Slab, max_rows_per_gpu, min_ranks_for
 
 __all__ = [
@@ -17,6 +18,8 @@ __all__ = [
     "init",
     "shutdown",
     "HaloExchange",
+    "NativeComm",
+    "P2PPlan",
     "Slab",
     "max_rows_per_gpu",
     "min_ranks_for",

@@ -17,15 +17,28 @@ from .dist import DistContext
 from .slab import Slab
 
 
+def _native_ok(x: torch.Tensor, ctx: DistContext) -> bool:
+    return ctx.native is not None and x.is_cuda and x.is_contiguous() and x.dtype in (
+        torch.float64, torch.float32, torch.int32)
+
+
 def all_reduce_max(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    """In-place MAX over ranks, ordered on the current stream (native RCCL tier
+    when available, torch.distributed otherwise)."""
     if ctx.is_distributed:
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        if _native_ok(x, ctx):
+            ctx.native.all_reduce_(x, "max")
+        else:
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
     return x
 
 
 def all_reduce_sum(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     if ctx.is_distributed:
-        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        if _native_ok(x, ctx):
+            ctx.native.all_reduce_(x, "sum")
+        else:
+            dist.all_reduce(x, op=dist.ReduceOp.SUM)
     return x
 
 

@@ -13,7 +13,7 @@ from __future__ import annotations
 import datetime
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Any, Optional
 
 import torch
 import torch.distributed as dist
@@ -26,6 +26,7 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
+    native: Optional[Any] = None  # NativeComm (libmpx RCCL tier) when every rank could create it
 
     @property
     def is_distributed(self) -> bool:
@@ -83,12 +84,21 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
         if use_cuda:
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+    if world > 1 and use_cuda and backend == "nccl":
+        from .native_comm import NativeComm  # collective: every rank runs init()
+
+        ctx.native = NativeComm.create(ctx)
     _CTX = ctx
     return ctx
 
 
 def shutdown() -> None:
     global _CTX
+    if _CTX is not None and _CTX.native is not None:
+        if _CTX.device.type == "cuda":
+            torch.cuda.synchronize(_CTX.device)
+        _CTX.native.close()
+        _CTX.native = None
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

@@ -11,7 +11,7 @@ then orders the current stream after the transfer.
 
 from __future__ import annotations
 
-from typing import List
+from typing import Dict, List, Tuple
 
 import torch
 import torch.distributed as dist
@@ -21,10 +21,16 @@ from .slab import Slab
 
 
 class HaloExchange:
+    """``start``/``wait`` pair; with ``ctx.native`` (the libmpx RCCL tier) the
+    same op list runs as one grouped send/recv from C on a comm stream forked
+    from the current stream, otherwise through ``batch_isend_irecv``."""
+
     def __init__(self, slab: Slab, ctx: DistContext):
         self.slab = slab
         self.ctx = ctx
         self._works: List = []
+        self._plans: Dict[Tuple[int, Tuple[int, ...]], object] = {}
+        self._native_pending = False
 
     def _ops(self, buf: torch.Tensor):
         s = self.slab
@@ -50,14 +56,37 @@ class HaloExchange:
         if not self.ctx.is_distributed:
             self._works = []
             return
+        nc = self.ctx.native
+        if nc is not None and buf.is_cuda:
+            nc.p2p_start(self._plan(buf))
+            self._native_pending = True
+            return
         ops = self._ops(buf)
         self._works = dist.batch_isend_irecv(ops) if ops else []
 
     def wait(self) -> None:
+        if self._native_pending:
+            self.ctx.native.p2p_wait()
+            self._native_pending = False
         for w in self._works:
             w.wait()
         self._works = []
 
     def exchange(self, buf: torch.Tensor) -> None:
+        """Blocking-in-stream exchange: later work on the current stream sees the
+        halos. Natively this is one grouped send/recv on the current stream."""
+        nc = self.ctx.native
+        if nc is not None and buf.is_cuda:
+            nc.p2p(self._plan(buf))
+            return
         self.start(buf)
         self.wait()
+
+    def _plan(self, buf: torch.Tensor):
+        key = (buf.data_ptr(), tuple(buf.shape))
+        plan = self._plans.get(key)
+        if plan is None:
+            from .native_comm import plan_from_p2p_ops
+
+            plan = self._plans[key] = plan_from_p2p_ops(self._ops(buf))
+        return plan

@@ -108,6 +108,32 @@ int mpx_classify_ex(uint32_t *img, int64_t npix, int nc, const double *mu, const
  * the fp32 decision cannot be proven) and the fp32 decision margin. <0 = error. */
 int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin);
 
+/* ---------------- native RCCL tier (inter-GPU transport) ---------------- */
+/*
+ * The ncclXxx entry points are bound with dlsym from `path` (the librccl torch
+ * loaded; RTLD_NOLOAD first so one RCCL serves the whole process).
+ * A communicator owns a non-blocking comm stream and two events:
+ * p2p_start orders a grouped send/recv list after the work queued on `stream`
+ * and runs it on the comm stream; p2p_wait makes `stream` wait for it.
+ */
+int mpx_comm_load(const char *path);
+int mpx_comm_version(void);
+int mpx_comm_unique_id(void *out, int nbytes); /* returns the id size */
+int mpx_comm_init(void **comm, int nranks, int rank, const void *id, int nbytes, int device);
+int mpx_comm_destroy(void *comm);
+int mpx_comm_rank(void *comm);
+int mpx_comm_size(void *comm);
+int mpx_comm_p2p_start(void *comm, int n, const int *kind, void *const *ptr, const int64_t *bytes,
+                       const int *peer, void *stream); /* kind 0 send, 1 recv */
+int mpx_comm_p2p_wait(void *comm, void *stream);
+/* the same op list in order on `stream` itself (no comm stream, no events) */
+int mpx_comm_p2p(void *comm, int n, const int *kind, void *const *ptr, const int64_t *bytes, const int *peer,
+                 void *stream);
+/* dtype 0 f64, 1 f32, 2 i32, 3 u64; op 0 sum, 1 max, 2 min; on `stream` */
+int mpx_comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
+                       void *stream);
+int mpx_comm_check(void *comm);
+
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*
  * One sweep over rows [r0, r1) of a slab stored with one halo row above and
