@@ -94,5 +94,33 @@ bin/hw1: native/apps/hw1_quadratic.c | $(B)
 bin/hw2: native/apps/hw2_bubble_sort.c | $(B)
 	$(CC) $(CSER) $< -o $@
 
+# ---- host-only sanitizer builds of the CPU references ----
+# GPU ASan / xnack+ code objects are not available on the MI355X pool, so the
+# sanitizers cover the host code paths: the CPU references, the .data / text
+# I/O and the stdin parsers shared with the GPU programs.
+SAN       := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
+SAN_APPS  := $(foreach L,1 2 3,build/san/lab$(L)_cpu_exe build/san/lab$(L)_cpu_omp_exe) build/san/lab3_read_input_exe \
+             build/san/hw1 build/san/hw2
+.PHONY: sanitize
+sanitize: $(SAN_APPS)
+
+build/san:
+	@mkdir -p build/san
+
+build/san/lab%_cpu_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS) | build/san
+	$(CC) $(SAN) -ffp-contract=off -Wall -Wno-unknown-pragmas -std=gnu11 -Inative/include $< native/src/cpu/cpu_kernels.c -lm -o $@
+
+build/san/lab%_cpu_omp_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS) | build/san
+	$(CC) $(SAN) -fopenmp -ffp-contract=off -Wall -std=gnu11 -Inative/include $< native/src/cpu/cpu_kernels.c -lm -o $@
+
+build/san/lab3_read_input_exe: native/apps/lab3_read_input.c | build/san
+	$(CC) $(SAN) -Wall -std=gnu11 $< -o $@
+
+build/san/hw1: native/apps/hw1_quadratic.c | build/san
+	$(CC) $(SAN) -Wall -std=gnu11 $< -lm -o $@
+
+build/san/hw2: native/apps/hw2_bubble_sort.c | build/san
+	$(CC) $(SAN) -Wall -std=gnu11 $< -o $@
+
 clean:
 	rm -rf $(B) bin $(PYLIB) $(GPU_APPS) $(CPU_APPS) labs/lab3/src/read_input_exe

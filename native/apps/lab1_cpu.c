@@ -37,21 +37,24 @@ int main(void) {
         fprintf(stderr, "[ERROR CPU] expected vector size\n");
         return 1;
     }
+    int rc = 1;
     double *a = (double *)malloc(sizeof(double) * (n ? n : 1));
     double *b = (double *)malloc(sizeof(double) * (n ? n : 1));
     double *c = (double *)malloc(sizeof(double) * (n ? n : 1));
     if (!a || !b || !c) {
         fprintf(stderr, "[ERROR CPU] allocation failed\n");
-        return 1;
+        goto done;
     }
-    if (read_vec(a, n, "first vector") || read_vec(b, n, "second vector")) return 1;
+    if (read_vec(a, n, "first vector") || read_vec(b, n, "second vector")) goto done;
     const double t0 = now_ms();
     mpx_cpu_vsub_f64(a, b, c, n);
     const double t1 = now_ms();
     printf("CPU execution time: <%f ms>\n", t1 - t0);
     for (int i = 0; i < n; ++i) printf("%.10e ", c[i]);
+    rc = 0;
+done:  /* one exit path: the host sanitizer build checks for leaks */
     free(a);
     free(b);
     free(c);
-    return 0;
+    return rc;
 }

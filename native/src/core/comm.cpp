@@ -150,7 +150,7 @@ extern "C" int mpx_comm_init(void **out, int nranks, int rank, const void *id, i
     // convolution become runnable together, the dispatcher places RCCL's few
     // workgroups first instead of queueing them behind thousands of conv waves
     int prio_lo = 0, prio_hi = 0;
-    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
@@ -166,12 +166,12 @@ extern "C" int mpx_comm_init(void **out, int nranks, int rank, const void *id, i
 extern "C" int mpx_comm_destroy(void *h) {
     if (!h) return MPX_OK;
     Comm *c = static_cast<Comm *>(h);
-    hipSetDevice(c->device);
-    if (c->cstream) hipStreamSynchronize(c->cstream);
+    (void)hipSetDevice(c->device);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) g_api.CommDestroy(c->comm);
-    if (c->ready) hipEventDestroy(c->ready);
-    if (c->done) hipEventDestroy(c->done);
-    if (c->cstream) hipStreamDestroy(c->cstream);
+    if (c->ready) (void)hipEventDestroy(c->ready);
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     delete c;
     return MPX_OK;
 }
