@@ -33,7 +33,7 @@ HDRS      := $(wildcard native/include/mpx/*.h native/include/mpx/*.hpp native/s
 LABS      := labs/lab1/src labs/lab2/src labs/lab3/src
 GPU_APPS  := $(foreach L,1 2 3,labs/lab$(L)/src/to_plot_hip_exe labs/lab$(L)/src/hip_exe)
 CPU_APPS  := $(foreach L,1 2 3,labs/lab$(L)/src/cpu_exe labs/lab$(L)/src/cpu_omp_exe)
-MISC_APPS := labs/lab3/src/read_input_exe bin/gpu_info bin/hw1 bin/hw2
+MISC_APPS := labs/lab3/src/read_input_exe bin/gpu_info bin/hw1 bin/hw2 bin/mpx_mgpu
 
 .PHONY: all lib apps clean
 all: lib apps
@@ -87,6 +87,10 @@ labs/lab3/src/read_input_exe: native/apps/lab3_read_input.c
 
 bin/gpu_info: native/apps/gpu_info.cpp $(ALIB) $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
+
+# native multi-GPU runtime: links /opt/rocm's RCCL directly (no torch in this process)
+bin/mpx_mgpu: native/apps/mpx_mgpu.cpp $(ALIB) $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -L$(ROCM)/lib -lrccl -lgomp -lm -ldl -lpthread -Wl,-rpath,$(ROCM)/lib -o $@
 
 bin/hw1: native/apps/hw1_quadratic.c | $(B)
 	$(CC) $(CSER) $< -lm -o $@

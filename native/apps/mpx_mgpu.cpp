@@ -1,0 +1,478 @@
+// mpx_mgpu — the native multi-GPU runtime: one process drives N MI355X GPUs,
+// one host thread per device, RCCL over xGMI between them. No Python, no MPI.
+//
+//   mpx_mgpu conv   [--gpus N] [--size S] [--filter sobel5] [--steps K] [--warmup W]
+//   mpx_mgpu jacobi [--gpus N] [--size S] [--iters K] [--warmup W] [--check-every C] [--fp32]
+//   mpx_mgpu vsub   [--gpus N] [--n ELEMS_PER_GPU] [--steps K] [--warmup W] [--fp64]
+//
+// Each prints one JSON line (whole-job throughput, ms per step, verification).
+//
+// Reference: the reference has no multi-process or multi-GPU code (SURVEY §0,
+// §2.6: "MPI" in the name only); this is the MPI tier of the BASELINE north
+// star rebuilt MI355X-first:
+//   * bootstrap without MPI: ncclGetUniqueId once, ncclCommInitRank from each
+//     device thread (ncclGroupStart/End around the inits, one process);
+//   * row-slab domain decomposition, each slab sized for one GPU's HBM;
+//   * halo exchange = one grouped ncclSend/ncclRecv per neighbour pair, in
+//     order on the device's compute stream (for halos of a few rows this beats
+//     overlapping on a second queue on MI355X — profiles/comm_step.md);
+//   * global residual = ncclAllReduce(max) every --check-every iterations (the
+//     small-message latency over xGMI is paid once per check, not per sweep);
+//   * weak scaling: the per-GPU slab is fixed, the global problem grows with N.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mpx/capi.h"
+#include "mpx/common.h"
+#include "mpx/filters.h"
+
+#define NCCL_CHECK(cmd)                                                                                  \
+    do {                                                                                                 \
+        ncclResult_t r_ = (cmd);                                                                         \
+        if (r_ != ncclSuccess) {                                                                         \
+            fprintf(stderr, "[ERROR RCCL] File: '%s'; Line: %i; Message: %s.\n", __FILE__, __LINE__,     \
+                    ncclGetErrorString(r_));                                                             \
+            exit(1);                                                                                     \
+        }                                                                                                \
+    } while (0)
+#define HIP_OK(cmd)                                                                                      \
+    do {                                                                                                 \
+        hipError_t e_ = (cmd);                                                                           \
+        if (e_ != hipSuccess) {                                                                          \
+            fprintf(stderr, "[ERROR HIP] File: '%s'; Line: %i; Message: %s.\n", __FILE__, __LINE__,      \
+                    hipGetErrorString(e_));                                                              \
+            exit(1);                                                                                     \
+        }                                                                                                \
+    } while (0)
+#define MPX_OK_OR_DIE(cmd)                                                                               \
+    do {                                                                                                 \
+        if ((cmd) != 0) {                                                                                \
+            fprintf(stderr, "[ERROR MPX] File: '%s'; Line: %i; Message: %s.\n", __FILE__, __LINE__,      \
+                    mpx_last_error());                                                                   \
+            exit(1);                                                                                     \
+        }                                                                                                \
+    } while (0)
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Args {
+    std::string mode;
+    int gpus = 0;  // 0: every visible device
+    int size = 0;
+    int steps = 0;
+    int warmup = 5;
+    int check_every = 10;
+    long long n = 0;
+    bool fp32 = false, fp64 = false;
+    std::string filter = "sobel5";
+};
+
+Args parse(int argc, char **argv) {
+    Args a;
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s conv|jacobi|vsub [--gpus N] [--size S] [--steps K] [--iters K] [--warmup W] "
+                        "[--filter F] [--check-every C] [--n N] [--fp32|--fp64]\n", argv[0]);
+        exit(2);
+    }
+    a.mode = argv[1];
+    for (int i = 2; i < argc; ++i) {
+        std::string k = argv[i];
+        auto val = [&]() -> const char * {
+            if (i + 1 >= argc) {
+                fprintf(stderr, "missing value for %s\n", k.c_str());
+                exit(2);
+            }
+            return argv[++i];
+        };
+        if (k == "--gpus") a.gpus = atoi(val());
+        else if (k == "--size") a.size = atoi(val());
+        else if (k == "--steps" || k == "--iters") a.steps = atoi(val());
+        else if (k == "--warmup") a.warmup = atoi(val());
+        else if (k == "--check-every") a.check_every = std::max(1, atoi(val()));
+        else if (k == "--n") a.n = atoll(val());
+        else if (k == "--filter") a.filter = val();
+        else if (k == "--fp32") a.fp32 = true;
+        else if (k == "--fp64") a.fp64 = true;
+        else {
+            fprintf(stderr, "unknown option %s\n", k.c_str());
+            exit(2);
+        }
+    }
+    return a;
+}
+
+// reusable thread barrier (C++17 has no std::barrier)
+class Barrier {
+  public:
+    explicit Barrier(int n) : n_(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(m_);
+        const long gen = gen_;
+        if (++count_ == n_) {
+            count_ = 0;
+            ++gen_;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk, [&] { return gen_ != gen; });
+        }
+    }
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int n_, count_ = 0;
+    long gen_ = 0;
+};
+
+// Row slab of `rows` global rows owned by `rank` of `world` (remainder rows go
+// to the first ranks, like cuda_mpi_openmp_amd.parallel.Slab).
+struct Slab {
+    long long row0, rows;
+    Slab(long long global, int world, int rank) {
+        const long long base = global / world, extra = global % world;
+        rows = base + (rank < extra ? 1 : 0);
+        row0 = rank * base + std::min<long long>(rank, extra);
+    }
+};
+
+__global__ void fill_bytes(uint8_t *p, size_t n, uint64_t seed) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = seed + 0x9e3779b97f4a7c15ull * (i + 1);  // splitmix64
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        p[i] = (uint8_t)(z ^ (z >> 31));
+    }
+}
+
+template <typename T>
+__global__ void fill_unit(T *p, size_t n, uint64_t seed) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = seed + 0x9e3779b97f4a7c15ull * (i + 1);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        p[i] = (T)((double)((z ^ (z >> 31)) >> 11) * 0x1.0p-53);
+    }
+}
+
+// fp32 host reference of one sweep, same operation order as the kernel and as
+// mpx_cpu_jacobi_f64: ((up + down) + (left + right)) * 0.25, columns 1..cols-2
+void cpu_sweep_f32(const float *u, float *un, int cols, int r0, int r1) {
+    for (int i = r0; i < r1; ++i)
+        for (int j = 1; j < cols - 1; ++j) {
+            const float *c = u + (size_t)i * cols;
+            un[(size_t)i * cols + j] = ((c[j - cols] + c[j + cols]) + (c[j - 1] + c[j + 1])) * 0.25f;
+        }
+}
+
+struct Shared {
+    int world = 1;
+    ncclUniqueId id;
+    Barrier *bar = nullptr;
+    std::vector<double> elapsed;  // seconds per rank
+    std::vector<int> verified;    // 1 ok, 0 mismatch, -1 not checked
+    std::vector<double> extra;    // residual etc.
+};
+
+ncclComm_t init_comm(Shared &sh, int rank) {
+    ncclComm_t c;
+    NCCL_CHECK(ncclCommInitRank(&c, sh.world, sh.id, rank));
+    return c;
+}
+
+// grouped halo exchange of row blocks between vertically adjacent slabs
+void halo_exchange(ncclComm_t comm, hipStream_t s, int rank, int world, uint8_t *buf, size_t row_bytes,
+                   long long own_off, long long rows, int halo_up, int halo_down) {
+    NCCL_CHECK(ncclGroupStart());
+    if (rank > 0) {  // rank above: it needs my first halo_down rows, I need its last halo_up rows
+        if (halo_down) NCCL_CHECK(ncclSend(buf + own_off * row_bytes, halo_down * row_bytes, ncclUint8, rank - 1, comm, s));
+        if (halo_up) NCCL_CHECK(ncclRecv(buf, halo_up * row_bytes, ncclUint8, rank - 1, comm, s));
+    }
+    if (rank + 1 < world) {
+        if (halo_up) NCCL_CHECK(ncclSend(buf + (own_off + rows - halo_up) * row_bytes, halo_up * row_bytes, ncclUint8,
+                                         rank + 1, comm, s));
+        if (halo_down) NCCL_CHECK(ncclRecv(buf + (own_off + rows) * row_bytes, halo_down * row_bytes, ncclUint8,
+                                           rank + 1, comm, s));
+    }
+    NCCL_CHECK(ncclGroupEnd());
+}
+
+// ---------------------------------------------------------------- conv
+void conv_worker(const Args &a, Shared &sh, int rank) {
+    HIP_OK(hipSetDevice(rank));
+    ncclComm_t comm = init_comm(sh, rank);
+    hipStream_t s;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int k, anchor, mode;
+    float wx[MPX_MAX_K * MPX_MAX_K], wy[MPX_MAX_K * MPX_MAX_K];
+    MPX_OK_OR_DIE(mpx_filter_lookup(a.filter.c_str(), &k, &anchor, &mode, wx, wy));
+    const int hu = anchor, hd = k - 1 - anchor;  // rows needed above / below
+    const int w = a.size;
+    const long long rows = a.size;  // weak scaling: one size x size slab per GPU
+    const bool up = rank > 0, down = rank + 1 < sh.world;
+    const long long buf_rows = rows + hu + hd;
+    const size_t row_bytes = (size_t)w * 4;
+    uint8_t *buf, *out;
+    HIP_OK(hipMalloc(&buf, buf_rows * row_bytes));
+    HIP_OK(hipMalloc(&out, rows * row_bytes));
+    fill_bytes<<<1024, 256, 0, s>>>(buf, buf_rows * row_bytes, 1234 + rank);
+    // logical rows of the slab: [0, rows); reads clamp into [y_lo, y_hi]
+    const int y_lo = up ? -hu : 0, y_hi = (int)rows - 1 + (down ? hd : 0);
+    const uint32_t *in = reinterpret_cast<const uint32_t *>(buf + hu * row_bytes);
+    auto step = [&]() {
+        if (sh.world > 1) halo_exchange(comm, s, rank, sh.world, buf, row_bytes, hu, rows, hu, hd);
+        MPX_OK_OR_DIE(mpx_conv(in, reinterpret_cast<uint32_t *>(out), w, w, 0, (int)rows, y_lo, y_hi, k, anchor, mode,
+                               wx, wy, s));
+    };
+    for (int i = 0; i < a.warmup; ++i) step();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    const auto t0 = Clock::now();
+    for (int i = 0; i < a.steps; ++i) step();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
+    // verify the halo-dependent edge rows (and a band around them) on the CPU
+    const int band = std::min<long long>(32, rows);
+    std::vector<uint32_t> hbuf(buf_rows * w), hout(rows * w), ref(rows * w);
+    HIP_OK(hipMemcpy(hbuf.data(), buf, buf_rows * row_bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(hout.data(), out, rows * row_bytes, hipMemcpyDeviceToHost));
+    const uint32_t *hin = hbuf.data() + (size_t)hu * w;
+    bool ok = true;
+    for (int part = 0; part < 2; ++part) {
+        const int oy0 = part == 0 ? 0 : (int)rows - band, oy1 = part == 0 ? band : (int)rows;
+        mpx_cpu_conv(hin, ref.data(), w, w, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy);
+        ok &= std::memcmp(ref.data() + (size_t)oy0 * w, hout.data() + (size_t)oy0 * w,
+                          (size_t)(oy1 - oy0) * row_bytes) == 0;
+    }
+    sh.verified[rank] = ok ? 1 : 0;
+    HIP_OK(hipFree(buf));
+    HIP_OK(hipFree(out));
+    HIP_OK(hipStreamDestroy(s));
+    NCCL_CHECK(ncclCommDestroy(comm));
+}
+
+// ---------------------------------------------------------------- jacobi
+template <typename T>
+void jacobi_worker(const Args &a, Shared &sh, int rank) {
+    HIP_OK(hipSetDevice(rank));
+    ncclComm_t comm = init_comm(sh, rank);
+    hipStream_t s;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const int cols = a.size;
+    const Slab sl(a.size, sh.world, rank);  // strong scaling of one size x size grid
+    const long long rows = sl.rows;
+    const size_t row_bytes = (size_t)cols * sizeof(T);
+    const size_t bytes = (rows + 2) * row_bytes;
+    T *u, *un, *res;
+    HIP_OK(hipMalloc(&u, bytes));
+    HIP_OK(hipMalloc(&un, bytes));
+    HIP_OK(hipMalloc(&res, sizeof(T)));
+    fill_unit<T><<<1024, 256, 0, s>>>(u, (rows + 2) * cols, 77 + rank);
+    HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
+    const ncclDataType_t dt = sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
+    const bool up = rank > 0, down = rank + 1 < sh.world;
+    int it = 0;
+    double last_res = -1;
+    auto iterate = [&]() {
+        // halos of u (1 row each way), in order before the sweep that reads them
+        if (sh.world > 1) {
+            NCCL_CHECK(ncclGroupStart());
+            if (up) {
+                NCCL_CHECK(ncclSend(u + cols, cols, dt, rank - 1, comm, s));
+                NCCL_CHECK(ncclRecv(u, cols, dt, rank - 1, comm, s));
+            }
+            if (down) {
+                NCCL_CHECK(ncclSend(u + rows * cols, cols, dt, rank + 1, comm, s));
+                NCCL_CHECK(ncclRecv(u + (rows + 1) * cols, cols, dt, rank + 1, comm, s));
+            }
+            NCCL_CHECK(ncclGroupEnd());
+        }
+        const bool check = (it + 1) % a.check_every == 0;
+        // owned rows 1..rows; buffer row 0 of the first rank and row rows+1 of
+        // the last are the global Dirichlet boundary (never received into)
+        if constexpr (sizeof(T) == 8)
+            MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, 1, (int)rows + 1, check ? res : nullptr, s));
+        else
+            MPX_OK_OR_DIE(mpx_jacobi_f32(u, un, cols, cols, 1, (int)rows + 1, check ? res : nullptr, s));
+        std::swap(u, un);
+        if (check) {
+            NCCL_CHECK(ncclAllReduce(res, res, 1, dt, ncclMax, comm, s));
+            T h;
+            HIP_OK(hipMemcpyAsync(&h, res, sizeof(T), hipMemcpyDeviceToHost, s));
+            HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
+            HIP_OK(hipStreamSynchronize(s));
+            last_res = (double)h;
+        }
+        ++it;
+    };
+    for (int i = 0; i < a.warmup; ++i) iterate();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    const auto t0 = Clock::now();
+    for (int i = 0; i < a.steps; ++i) iterate();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
+    sh.extra[rank] = last_res;
+    // verify one more sweep of the first owned rows against the CPU reference
+    const long long vr = std::min<long long>(rows, 8);
+    if (sh.world > 1) {  // refresh halos exactly as an iteration does
+        NCCL_CHECK(ncclGroupStart());
+        if (up) {
+            NCCL_CHECK(ncclSend(u + cols, cols, dt, rank - 1, comm, s));
+            NCCL_CHECK(ncclRecv(u, cols, dt, rank - 1, comm, s));
+        }
+        if (down) {
+            NCCL_CHECK(ncclSend(u + rows * cols, cols, dt, rank + 1, comm, s));
+            NCCL_CHECK(ncclRecv(u + (rows + 1) * cols, cols, dt, rank + 1, comm, s));
+        }
+        NCCL_CHECK(ncclGroupEnd());
+    }
+    std::vector<T> hu_((vr + 2) * cols), hun((vr + 2) * cols), gun((vr + 2) * cols);
+    HIP_OK(hipMemcpyAsync(hu_.data(), u, (vr + 2) * row_bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    hun = hu_;
+    const int r0 = 1;
+    if constexpr (sizeof(T) == 8) {
+        MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, r0, (int)vr + 1, nullptr, s));
+        mpx_cpu_jacobi_f64(hu_.data(), hun.data(), cols, cols, r0, (int)vr + 1);
+    } else {
+        MPX_OK_OR_DIE(mpx_jacobi_f32(u, un, cols, cols, r0, (int)vr + 1, nullptr, s));
+        cpu_sweep_f32(hu_.data(), hun.data(), cols, r0, (int)vr + 1);
+    }
+    HIP_OK(hipMemcpyAsync(gun.data(), un, (vr + 2) * row_bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    sh.verified[rank] = std::memcmp(gun.data() + r0 * cols, hun.data() + r0 * cols,
+                                    (size_t)(vr + 1 - r0) * row_bytes) == 0;
+    HIP_OK(hipFree(u));
+    HIP_OK(hipFree(un));
+    HIP_OK(hipFree(res));
+    HIP_OK(hipStreamDestroy(s));
+    NCCL_CHECK(ncclCommDestroy(comm));
+}
+
+// ---------------------------------------------------------------- vsub
+template <typename T>
+void vsub_worker(const Args &a, Shared &sh, int rank) {
+    HIP_OK(hipSetDevice(rank));
+    hipStream_t s;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const long long n = a.n;
+    T *x, *y, *z;
+    HIP_OK(hipMalloc(&x, n * sizeof(T)));
+    HIP_OK(hipMalloc(&y, n * sizeof(T)));
+    HIP_OK(hipMalloc(&z, n * sizeof(T)));
+    fill_unit<T><<<1024, 256, 0, s>>>(x, n, 5 + 2 * rank);
+    fill_unit<T><<<1024, 256, 0, s>>>(y, n, 6 + 2 * rank);
+    auto step = [&]() {
+        if constexpr (sizeof(T) == 8) MPX_OK_OR_DIE(mpx_vsub_f64(x, y, z, n, 0, 0, s));
+        else MPX_OK_OR_DIE(mpx_vsub_f32(x, y, z, n, 0, 0, s));
+    };
+    for (int i = 0; i < a.warmup; ++i) step();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    const auto t0 = Clock::now();
+    for (int i = 0; i < a.steps; ++i) step();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
+    const long long m = std::min<long long>(n, 1 << 16);
+    std::vector<T> hx(m), hy(m), hz(m);
+    HIP_OK(hipMemcpy(hx.data(), x, m * sizeof(T), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(hy.data(), y, m * sizeof(T), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(hz.data(), z, m * sizeof(T), hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (long long i = 0; i < m; ++i) ok &= hz[i] == hx[i] - hy[i];
+    sh.verified[rank] = ok;
+    HIP_OK(hipFree(x));
+    HIP_OK(hipFree(y));
+    HIP_OK(hipFree(z));
+    HIP_OK(hipStreamDestroy(s));
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    Args a = parse(argc, argv);
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (ndev < 1) {
+        fprintf(stderr, "[ERROR HIP] no GPU visible\n");
+        return 1;
+    }
+    const int N = a.gpus > 0 ? a.gpus : ndev;
+    if (N > ndev) {
+        fprintf(stderr, "[ERROR] --gpus %d but only %d device(s) visible\n", N, ndev);
+        return 1;
+    }
+    Shared sh;
+    sh.world = N;
+    Barrier bar(N);
+    sh.bar = &bar;
+    sh.elapsed.assign(N, 0.0);
+    sh.verified.assign(N, -1);
+    sh.extra.assign(N, 0.0);
+    if (a.mode != "vsub") NCCL_CHECK(ncclGetUniqueId(&sh.id));
+
+    std::vector<std::thread> th;
+    if (a.mode == "conv") {
+        if (a.size <= 0) a.size = 4096;
+        if (a.steps <= 0) a.steps = 50;
+        for (int r = 0; r < N; ++r) th.emplace_back([&, r] { conv_worker(a, sh, r); });
+    } else if (a.mode == "jacobi") {
+        if (a.size <= 0) a.size = 16384;
+        if (a.steps <= 0) a.steps = 50;
+        for (int r = 0; r < N; ++r)
+            th.emplace_back([&, r] { a.fp32 ? jacobi_worker<float>(a, sh, r) : jacobi_worker<double>(a, sh, r); });
+    } else if (a.mode == "vsub") {
+        if (a.n <= 0) a.n = 1LL << 26;
+        if (a.steps <= 0) a.steps = 50;
+        for (int r = 0; r < N; ++r)
+            th.emplace_back([&, r] { a.fp64 ? vsub_worker<double>(a, sh, r) : vsub_worker<float>(a, sh, r); });
+    } else {
+        fprintf(stderr, "unknown mode '%s' (conv | jacobi | vsub)\n", a.mode.c_str());
+        return 2;
+    }
+    for (auto &t : th) t.join();
+
+    const double el = *std::max_element(sh.elapsed.begin(), sh.elapsed.end());
+    const double ms = el * 1e3 / a.steps;
+    const bool ok = std::all_of(sh.verified.begin(), sh.verified.end(), [](int v) { return v == 1; });
+    if (a.mode == "conv") {
+        const double gpix = (double)N * a.size * a.size * a.steps / el / 1e9;
+        printf("{\"workload\": \"conv\", \"filter\": \"%s\", \"n_gpus\": %d, \"slab\": [%d, %d], \"steps\": %d, "
+               "\"ms_per_step\": %.5f, \"value\": %.3f, \"unit\": \"Gpixel/s\", \"scaling\": \"weak\", "
+               "\"verified_bit_exact\": %s}\n",
+               a.filter.c_str(), N, a.size, a.size, a.steps, ms, gpix, ok ? "true" : "false");
+    } else if (a.mode == "jacobi") {
+        const double pts = (double)a.size * a.size * a.steps / el / 1e9;
+        const double tbs = (double)a.size * a.size * (a.fp32 ? 4 : 8) * 2 * a.steps / el / 1e12;
+        printf("{\"workload\": \"jacobi\", \"dtype\": \"%s\", \"n_gpus\": %d, \"grid\": [%d, %d], \"iters\": %d, "
+               "\"check_every\": %d, \"ms_per_iter\": %.5f, \"value\": %.3f, \"unit\": \"Gpoint/s\", "
+               "\"TBps_aggregate\": %.3f, \"scaling\": \"strong\", \"residual\": %.6e, \"verified\": %s}\n",
+               a.fp32 ? "fp32" : "fp64", N, a.size, a.size, a.steps, a.check_every, ms, pts, tbs, sh.extra[0],
+               ok ? "true" : "false");
+    } else {
+        const int es = a.fp64 ? 8 : 4;
+        const double tbs = (double)N * a.n * es * 3 * a.steps / el / 1e12;
+        printf("{\"workload\": \"vsub\", \"dtype\": \"%s\", \"n_gpus\": %d, \"n_per_gpu\": %lld, \"steps\": %d, "
+               "\"ms_per_step\": %.5f, \"value\": %.3f, \"unit\": \"TB/s\", \"scaling\": \"weak\", \"verified\": %s}\n",
+               a.fp64 ? "fp64" : "fp32", N, a.n, a.steps, ms, tbs, ok ? "true" : "false");
+    }
+    return ok ? 0 : 3;
+}

@@ -151,3 +151,29 @@ def test_lab2_gpu_timing_policies(tmp_path):
     for pol in ("cold", "warm", "median:5"):
         r = run("labs/lab2/src/to_plot_hip_exe", f"32\n32\n16\n16\n{src}\n{tmp_path}/o.data", env={"MPX_TIMING": pol})
         assert r.returncode == 0 and r.stdout.startswith("HIP execution time: <")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ["conv", "--size", "1024", "--steps", "5", "--warmup", "1"],
+    ["conv", "--size", "1000", "--steps", "3", "--warmup", "1", "--filter", "roberts"],
+    ["jacobi", "--size", "2048", "--iters", "20", "--warmup", "2", "--check-every", "5"],
+    ["jacobi", "--size", "1024", "--iters", "10", "--warmup", "1", "--fp32"],
+    ["vsub", "--n", "1000003", "--steps", "5", "--warmup", "1"],
+    ["vsub", "--n", "65536", "--steps", "5", "--warmup", "1", "--fp64"],
+])
+def test_mpx_mgpu_single_gpu(args):
+    """Native multi-GPU runtime (one process, one thread + RCCL communicator per
+    device) on the one GPU of the test box; every workload self-verifies."""
+    import json
+
+    r = run("bin/mpx_mgpu", "", args=[*args, "--gpus", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+    assert rec.get("verified_bit_exact", rec.get("verified")) is True
+
+
+def test_mpx_mgpu_usage_errors():
+    assert run("bin/mpx_mgpu", "").returncode == 2
+    assert run("bin/mpx_mgpu", "", args=["conv", "--bogus"]).returncode == 2
