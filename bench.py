@@ -80,6 +80,8 @@ def main() -> int:
     p.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                    help="halo transfer overlapped with the interior rows (on), in order before one full launch "
                         "(off), or the measured-faster choice for the transport in use (auto)")
+    p.add_argument("--watchdog", type=float, default=None,
+                   help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
@@ -95,8 +97,11 @@ def main() -> int:
     sync(ctx)
     ctx.barrier()
 
+    wd_s = args.watchdog if args.watchdog is not None else (300.0 if n > 1 else 0.0)
+    watchdog = parallel.Watchdog(ctx, wd_s, what="benchmark step")
     for _ in range(args.warmup):
         det.step()
+        watchdog.beat()
     sync(ctx)
     ctx.barrier()
 
@@ -109,6 +114,7 @@ def main() -> int:
     sync(ctx)
     ctx.barrier()
     t1 = time.perf_counter()
+    watchdog.beat()
     elapsed = parallel.max_over_ranks(t1 - t0, ctx)
 
     ms_per_step = elapsed * 1e3 / max(1, args.steps)
@@ -120,6 +126,7 @@ def main() -> int:
         ok = verify_band(det)
         ok = parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
 
+    watchdog.stop()
     cpu_ms = None
     if ctx.rank == 0 and not args.no_cpu_baseline:
         cpu_ms = cpu_baseline_ms(det, args.size)

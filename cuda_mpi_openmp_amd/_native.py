@@ -68,6 +68,7 @@ _SIGNATURES = {
                              ctypes.POINTER(c_i64), ctypes.POINTER(c_int), c_vp]),
     "mpx_comm_allreduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "mpx_comm_check": (c_int, [c_vp]),
+    "mpx_comm_abort": (c_int, [c_vp]),
     "mpx_classify_ex": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_classify_plan": (c_int, [c_int, _dp, _dp, c_int, ctypes.POINTER(ctypes.c_float)]),
     "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),

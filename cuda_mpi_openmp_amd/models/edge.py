@@ -19,6 +19,7 @@ from ..ops.filters import Filter, get_filter
 from ..parallel.dist import DistContext
 from ..parallel.halo import HaloExchange
 from ..parallel.slab import Slab
+from ..utils import trace
 
 
 class EdgeDetector:
@@ -65,6 +66,7 @@ class SlabEdgeDetector:
         self._all = mk(0, s.rows)
         self._interior = mk(*s.interior())
         self._boundary = [mk(a, b) for a, b in s.boundary()]
+        self._traced = trace.enabled()  # roctx ranges only when MPX_ROCTX=1
 
     @property
     def own(self) -> torch.Tensor:
@@ -86,6 +88,12 @@ class SlabEdgeDetector:
 
     def step(self) -> torch.Tensor:
         """Exchange halos and convolve every owned row; returns the output slab."""
+        if self._traced:
+            with trace.range("edge.step"):
+                return self._step()
+        return self._step()
+
+    def _step(self) -> torch.Tensor:
         st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
         if not self.ctx.is_distributed:
             self._all(st)

@@ -21,7 +21,6 @@ fixed. A decomposed run is bit-identical to a one-rank run.
 
 from __future__ import annotations
 
-import os
 from typing import Callable, Optional
 
 import torch
@@ -29,21 +28,9 @@ import torch
 from .. import ops
 from ..parallel.collectives import all_reduce_max, gather_slabs
 from ..parallel.dist import DistContext
+from ..parallel.fault import FaultInjected, fault_hook as _fault_hook  # noqa: F401 (re-export)
 from ..parallel.halo import HaloExchange
 from ..parallel.slab import Slab
-
-
-class FaultInjected(RuntimeError):
-    """Raised by the MPX_FAULT_INJECT hook (tests of failure detection)."""
-
-
-def _fault_hook(rank: int, it: int) -> None:
-    spec = os.environ.get("MPX_FAULT_INJECT")  # "rank:iteration"
-    if not spec:
-        return
-    r, i = (int(v) for v in spec.split(":"))
-    if r == rank and i == it:
-        raise FaultInjected(f"injected fault on rank {rank} at iteration {it}")
 
 
 class SlabJacobi:

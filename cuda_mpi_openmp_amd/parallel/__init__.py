@@ -2,6 +2,7 @@
 
 from .collectives import all_reduce_max, all_reduce_sum, broadcast_object, gather_slabs, max_over_ranks, scatter_rows
 from .dist import DistContext, context, init, shutdown
+from .fault import EXIT_HUNG, FaultInjected, Watchdog, fault_hook
 from .halo import HaloExchange
 from .native_comm import NativeComm, P2PPlan
 from .slab import Slab, max_rows_per_gpu, min_ranks_for
@@ -14,6 +15,10 @@ __all__ = [
     "max_over_ranks",
     "scatter_rows",
     "DistContext",
+    "EXIT_HUNG",
+    "FaultInjected",
+    "Watchdog",
+    "fault_hook",
     "context",
     "init",
     "shutdown",

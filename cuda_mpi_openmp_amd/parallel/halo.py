@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from .dist import DistContext
+from ..utils import trace
 from .slab import Slab
 
 
@@ -75,12 +76,13 @@ class HaloExchange:
     def exchange(self, buf: torch.Tensor) -> None:
         """Blocking-in-stream exchange: later work on the current stream sees the
         halos. Natively this is one grouped send/recv on the current stream."""
-        nc = self.ctx.native
-        if nc is not None and buf.is_cuda:
-            nc.p2p(self._plan(buf))
-            return
-        self.start(buf)
-        self.wait()
+        with trace.range("halo.exchange"):
+            nc = self.ctx.native
+            if nc is not None and buf.is_cuda:
+                nc.p2p(self._plan(buf))
+                return
+            self.start(buf)
+            self.wait()
 
     def _plan(self, buf: torch.Tensor):
         key = (buf.data_ptr(), tuple(buf.shape))

@@ -149,6 +149,11 @@ class NativeComm:
     def check(self) -> None:
         _native.check(self._L.mpx_comm_check(self.handle))
 
+    def abort(self) -> None:
+        """ncclCommAbort: unblock and free a communicator whose peers are gone."""
+        if self.handle:
+            self._L.mpx_comm_abort(self.handle)
+
     def close(self) -> None:
         if self.handle:
             self._L.mpx_comm_destroy(self.handle)

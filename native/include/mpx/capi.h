@@ -133,6 +133,8 @@ int mpx_comm_p2p(void *comm, int n, const int *kind, void *const *ptr, const int
 int mpx_comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
                        void *stream);
 int mpx_comm_check(void *comm);
+/* ncclCommAbort: release a communicator whose peers hung or died (watchdog) */
+int mpx_comm_abort(void *comm);
 
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*

@@ -43,6 +43,7 @@ struct RcclApi {
     decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
     decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -100,7 +101,7 @@ extern "C" int mpx_comm_load(const char *path) {
     RcclApi a;
     a.handle = h;
     bool ok = bind(h, "ncclGetUniqueId", a.GetUniqueId) && bind(h, "ncclCommInitRank", a.CommInitRank) &&
-              bind(h, "ncclCommDestroy", a.CommDestroy) &&
+              bind(h, "ncclCommDestroy", a.CommDestroy) && bind(h, "ncclCommAbort", a.CommAbort) &&
               bind(h, "ncclCommGetAsyncError", a.CommGetAsyncError) &&
               bind(h, "ncclGetErrorString", a.GetErrorString) && bind(h, "ncclGroupStart", a.GroupStart) &&
               bind(h, "ncclGroupEnd", a.GroupEnd) && bind(h, "ncclSend", a.Send) && bind(h, "ncclRecv", a.Recv) &&
@@ -265,5 +266,18 @@ extern "C" int mpx_comm_check(void *h) {
         set_error("RCCL asynchronous error: %s", g_api.GetErrorString(ar));
         return MPX_ERR_HIP;
     }
+    return MPX_OK;
+}
+
+// Failure recovery: abort a communicator whose peers stopped responding (a
+// hung or dead rank). Outstanding RCCL kernels are released; the handle is
+// freed. Safe to call from a watchdog thread while another thread is blocked
+// on the stream.
+extern "C" int mpx_comm_abort(void *h) {
+    if (!h) return MPX_OK;
+    Comm *c = static_cast<Comm *>(h);
+    (void)hipSetDevice(c->device);
+    if (c->comm) g_api.CommAbort(c->comm);
+    c->comm = nullptr;
     return MPX_OK;
 }
