@@ -39,6 +39,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help='JSON list of CSV columns listed in the plot legend, e.g. ["filename"]')
     p.add_argument("--timeout", type=float, default=None, help="Per-run timeout in seconds.")
     p.add_argument("--timing", type=str, default=None, help="GPU timing policy: cold | warm | median:N")
+    p.add_argument("--warmup", type=int, default=None,
+                   help="untimed launches before the timed one(s) in the GPU binary (MPX_WARMUP)")
+    p.add_argument("--n_gpus", type=int, default=1,
+                   help="split each run over N GPUs inside the GPU binary (MPX_NGPUS); reported time is the "
+                        "slowest device's kernel time")
     return p
 
 
@@ -65,9 +70,17 @@ def main(argv: Optional[List[str]] = None) -> int:
     print(f"kernel_sizes=<{kernel_sizes}>")
     print(f"kwargs=<{json.dumps(kwargs, indent=2)}>")
     print(f"metadata_columns2plot=<{json.dumps(meta, indent=2)}>")
+    print(f"n_gpus=<{args.n_gpus}>")
     if lab_name in ("lab2", "lab3") and "dir_to_data" not in kwargs:
         kwargs["lab_dir"] = lab_dir
-    env = {"MPX_TIMING": args.timing} if args.timing else None
+    env = {}
+    if args.timing:
+        env["MPX_TIMING"] = args.timing
+    if args.warmup is not None:
+        env["MPX_WARMUP"] = str(max(0, args.warmup))
+    if args.n_gpus and args.n_gpus > 1:
+        env["MPX_NGPUS"] = str(args.n_gpus)
+    env = env or None
     tester = Tester(binary_path_gpu=args.binary_path_cuda, k_times=args.k_times, kernel_sizes=kernel_sizes,
                     metadata_columns2plot=meta, binary_path_cpu=args.binary_path_cpu, return_inp=args.return_inp,
                     return_task_res=args.return_task_res, timeout=args.timeout, gpu_env=env)

@@ -75,6 +75,7 @@ class Tester:
                 row["time_exe_ms_from_start_run_time_bin_name"] = (time.time() - t_start) * 1e3
                 row["wall_ms"] = rec.wall_ms
                 row["device"] = device
+                row["n_gpus"] = int((env or {}).get("MPX_NGPUS", 1)) if device == self.gpu_label else 0
                 self._throughput(row)
                 rows.append(row)
                 print(f"[Experiment bin_name=<{bin_name}> task={i} kernel_size=<{[k1, k2]}>] finished with "

@@ -6,8 +6,10 @@
 //     stdout "HIP execution time: <X ms>\n" (reference lab3/src/to_plot.cu:76-117,174)
 //   submission personality (-DMPX_SUBMISSION, "hip_exe"): no geometry, no output line.
 // Output: the input image with alpha = class index (255 when every distance is NaN).
-// MPX_LAB3_PATH = direct (default, geometry honoured) | mfma | auto.
+// MPX_LAB3_PATH = direct (default, geometry honoured) | fast | mfma | auto.
+// MPX_NGPUS=N shards the pixels over N devices (harness --n_gpus N).
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -29,6 +31,7 @@ int main() {
     if (const char *e = std::getenv("MPX_LAB3_PATH")) {
         if (!std::strcmp(e, "mfma")) path = MPX_CLS_MFMA;
         else if (!std::strcmp(e, "auto")) path = MPX_CLS_AUTO;
+        else if (!std::strcmp(e, "fast")) path = MPX_CLS_FAST;
     }
     std::string in_path, out_path;
     if (!in.next_token(in_path) || !in.next_token(out_path)) {
@@ -63,11 +66,37 @@ int main() {
     std::vector<double> mu(3 * nc), inv(9 * nc);
     MPX_CHECK(mpx_class_stats(img, w, h, nc, np.data(), coords.data(), mu.data(), inv.data()));
 
-    DeviceBuffer<uint32_t> dimg(npix);
-    HIP_CHECK(hipMemcpy(dimg.get(), img, npix * 4, hipMemcpyHostToDevice));
-    const float ms = time_kernel(
-        [&] { MPX_CHECK(mpx_classify(dimg.get(), npix, nc, mu.data(), inv.data(), blocks, threads, path, nullptr)); });
-    HIP_CHECK(hipMemcpy(img, dimg.get(), npix * 4, hipMemcpyDeviceToHost));
+    const int nparts = parts_from_env();
+    float ms = 0.0f;
+    if (nparts == 1) {
+        DeviceBuffer<uint32_t> dimg(npix);
+        HIP_CHECK(hipMemcpy(dimg.get(), img, npix * 4, hipMemcpyHostToDevice));
+        ms = time_kernel([&] {
+            MPX_CHECK(mpx_classify(dimg.get(), npix, nc, mu.data(), inv.data(), blocks, threads, path, nullptr));
+        });
+        HIP_CHECK(hipMemcpy(img, dimg.get(), npix * 4, hipMemcpyDeviceToHost));
+    } else {
+        // MPX_NGPUS = N: pixel shards (128-pixel aligned), class statistics
+        // computed once on the host and passed to every device's launch
+        Parts parts(nparts);
+        std::vector<std::unique_ptr<DeviceBuffer<uint32_t>>> d(nparts);
+        std::vector<int64_t> lo(nparts), hi(nparts);
+        for (int i = 0; i < nparts; ++i) {
+            part_range(npix, nparts, i, 128, lo[i], hi[i]);
+            parts.use(i);
+            d[i].reset(new DeviceBuffer<uint32_t>(hi[i] - lo[i]));
+            if (hi[i] > lo[i])
+                HIP_CHECK(hipMemcpy(d[i]->get(), img + lo[i], (hi[i] - lo[i]) * 4, hipMemcpyHostToDevice));
+        }
+        ms = parts.time([&](int i, hipStream_t st) {
+            MPX_CHECK(mpx_classify(d[i]->get(), hi[i] - lo[i], nc, mu.data(), inv.data(), blocks, threads, path, st));
+        });
+        for (int i = 0; i < nparts; ++i) {
+            parts.use(i);
+            if (hi[i] > lo[i])
+                HIP_CHECK(hipMemcpy(img + lo[i], d[i]->get(), (hi[i] - lo[i]) * 4, hipMemcpyDeviceToHost));
+        }
+    }
     const int rc = mpx_write_data_image(out_path.c_str(), img, w, h);
     std::free(img);
     if (rc) return 1;

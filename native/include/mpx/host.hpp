@@ -70,22 +70,27 @@ class DeviceBuffer {
 //               which includes first-launch code-object loading);
 //   warm      : one untimed warm-up launch, then time one launch (default);
 //   median:N  : warm-up, then the median of N timed launches.
+// MPX_WARMUP=W overrides the number of untimed launches (harness --warmup W).
 struct TimingPolicy {
     bool warmup = true;
+    int warmups = 1;
     int reps = 1;
     static TimingPolicy from_env() {
         TimingPolicy p;
         const char *s = std::getenv("MPX_TIMING");
-        if (!s || !*s || std::strcmp(s, "warm") == 0) return p;
-        if (std::strcmp(s, "cold") == 0) {
+        if (!s || !*s || std::strcmp(s, "warm") == 0) {
+        } else if (std::strcmp(s, "cold") == 0) {
             p.warmup = false;
-            return p;
-        }
-        if (std::strncmp(s, "median:", 7) == 0) {
+            p.warmups = 0;
+        } else if (std::strncmp(s, "median:", 7) == 0) {
             p.reps = std::max(1, std::atoi(s + 7));
-            return p;
+        } else {
+            std::fprintf(stderr, "[WARN] unknown MPX_TIMING='%s', using warm\n", s);
         }
-        std::fprintf(stderr, "[WARN] unknown MPX_TIMING='%s', using warm\n", s);
+        if (const char *w = std::getenv("MPX_WARMUP")) {
+            p.warmups = std::max(0, std::atoi(w));
+            p.warmup = p.warmups > 0;
+        }
         return p;
     }
 };
@@ -97,7 +102,7 @@ float time_kernel(F &&launch, hipStream_t stream = nullptr) {
     hipEvent_t a, b;
     HIP_CHECK(hipEventCreate(&a));
     HIP_CHECK(hipEventCreate(&b));
-    if (pol.warmup) {
+    for (int i = 0; i < pol.warmups; ++i) {
         launch();
         HIP_CHECK(hipStreamSynchronize(stream));
     }
@@ -116,6 +121,100 @@ float time_kernel(F &&launch, hipStream_t stream = nullptr) {
     HIP_CHECK(hipEventDestroy(b));
     std::sort(ts.begin(), ts.end());
     return ts[ts.size() / 2];
+}
+
+// ---- multi-device parts (MPX_NGPUS=N, harness --n_gpus N) ----
+// The lab programs split their work into N parts; part p runs on device
+// p % (visible devices) with its own stream and events, so the split logic is
+// exercised even on a box with fewer GPUs. The reported time is the max over
+// parts of each part's kernel time — the parallel time when the parts own
+// distinct GPUs.
+inline int parts_from_env() {
+    const char *s = std::getenv("MPX_NGPUS");
+    const int n = s ? std::atoi(s) : 1;
+    return n < 1 ? 1 : n;
+}
+
+class Parts {
+  public:
+    struct Part {
+        int dev = 0;
+        hipStream_t stream = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+    };
+    explicit Parts(int n) : p_(n) {
+        int ndev = 0;
+        HIP_CHECK(hipGetDeviceCount(&ndev));
+        for (int i = 0; i < n; ++i) {
+            p_[i].dev = i % ndev;
+            HIP_CHECK(hipSetDevice(p_[i].dev));
+            HIP_CHECK(hipStreamCreateWithFlags(&p_[i].stream, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreate(&p_[i].a));
+            HIP_CHECK(hipEventCreate(&p_[i].b));
+        }
+    }
+    ~Parts() {
+        for (auto &q : p_) {
+            (void)hipSetDevice(q.dev);
+            (void)hipEventDestroy(q.a);
+            (void)hipEventDestroy(q.b);
+            (void)hipStreamDestroy(q.stream);
+        }
+    }
+    Parts(const Parts &) = delete;
+    Parts &operator=(const Parts &) = delete;
+    int size() const { return (int)p_.size(); }
+    const Part &operator[](int i) const { return p_[i]; }
+    void use(int i) const { HIP_CHECK(hipSetDevice(p_[i].dev)); }
+    void sync_all() const {
+        for (int i = 0; i < size(); ++i) {
+            use(i);
+            HIP_CHECK(hipStreamSynchronize(p_[i].stream));
+        }
+    }
+    // launch(i, stream) queues part i; returns kernel ms under MPX_TIMING
+    template <typename F>
+    float time(F &&launch) const {
+        const TimingPolicy pol = TimingPolicy::from_env();
+        for (int w = 0; w < pol.warmups; ++w) {
+            for (int i = 0; i < size(); ++i) {
+                use(i);
+                launch(i, p_[i].stream);
+            }
+            sync_all();
+        }
+        std::vector<float> ts;
+        for (int r = 0; r < pol.reps; ++r) {
+            for (int i = 0; i < size(); ++i) {
+                use(i);
+                HIP_CHECK(hipEventRecord(p_[i].a, p_[i].stream));
+                launch(i, p_[i].stream);
+                HIP_CHECK(hipEventRecord(p_[i].b, p_[i].stream));
+            }
+            float worst = 0.0f;
+            for (int i = 0; i < size(); ++i) {
+                use(i);
+                HIP_CHECK(hipEventSynchronize(p_[i].b));
+                HIP_CHECK(hipGetLastError());
+                float t = 0.0f;
+                HIP_CHECK(hipEventElapsedTime(&t, p_[i].a, p_[i].b));
+                worst = std::max(worst, t);
+            }
+            ts.push_back(worst);
+        }
+        std::sort(ts.begin(), ts.end());
+        return ts[ts.size() / 2];
+    }
+
+  private:
+    std::vector<Part> p_;
+};
+
+// [begin, end) of part i of n over `total` items, boundaries multiples of `align`
+inline void part_range(int64_t total, int n, int i, int64_t align, int64_t &begin, int64_t &end) {
+    const int64_t per = ((total + n - 1) / n + align - 1) / align * align;
+    begin = std::min<int64_t>(total, per * i);
+    end = std::min<int64_t>(total, begin + per);
 }
 
 // ---- stdin ----

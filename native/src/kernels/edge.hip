@@ -132,7 +132,6 @@ Taps make_taps(int k, const float *wx, const float *wy, bool two) {
 }
 
 // Production tile: RPT = 8 rows per wave -> 128 x 32 output tiles.
-constexpr int kRPT = 8;
 // resident workgroups per CU the chunking targets (VGPR-limited to 4 at ~100 VGPRs)
 constexpr int kBlocksPerCU = 4;
 

@@ -177,3 +177,46 @@ def test_mpx_mgpu_single_gpu(args):
 def test_mpx_mgpu_usage_errors():
     assert run("bin/mpx_mgpu", "").returncode == 2
     assert run("bin/mpx_mgpu", "", args=["conv", "--bogus"]).returncode == 2
+
+
+def _png_to_data(png, dst):
+    from cuda_mpi_openmp_amd.utils import ImgData
+
+    dst.write_bytes(open(ImgData(str(png), cache_dir=str(dst.parent)).data_path, "rb").read())
+    return dst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["roberts", "sobel5", "gauss5"])
+def test_lab2_gpu_multi_part_matches_cpu(op, tmp_path):
+    """MPX_NGPUS=3: three row slabs (on the box's one GPU) with halo rows from
+    the host image must reproduce the CPU program byte for byte."""
+    src = _png_to_data(os.path.join(ROOT, "labs", "lab2", "metric_calc", "large", "doom.png"), tmp_path / "in.data")
+    ref, got = tmp_path / "ref.data", tmp_path / "got.data"
+    assert run("labs/lab2/src/cpu_omp_exe", f"{src}\n{ref}", env={"MPX_LAB2_OP": op}).returncode == 0
+    r = run("labs/lab2/src/to_plot_hip_exe", f"0\n0\n0\n0\n{src}\n{got}", env={"MPX_LAB2_OP": op, "MPX_NGPUS": "3",
+                                                                           "MPX_WARMUP": "2"})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("HIP execution time: <")
+    assert got.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+def test_lab1_gpu_multi_part():
+    r = run("labs/lab1/src/to_plot_hip_exe", "0\n0\n5\n1 2 3 4 5\n5 4 3 2 1", env={"MPX_NGPUS": "3"})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split("\n", 1)[1] == ("-4.0000000000e+00 -2.0000000000e+00 0.0000000000e+00 "
+                                          "2.0000000000e+00 4.0000000000e+00 ")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["direct", "fast"])
+def test_lab3_gpu_multi_part_matches_cpu(path, tmp_path):
+    src = _png_to_data(os.path.join(ROOT, "labs", "lab2", "metric_calc", "medium", "lenna.png"), tmp_path / "in.data")
+    classes = "3\n4 10 10 20 20 30 30 40 40\n4 100 200 110 210 120 220 130 230\n5 400 50 410 60 420 70 430 80 500 500"
+    ref, got = tmp_path / "ref.data", tmp_path / "got.data"
+    assert run("labs/lab3/src/cpu_omp_exe", f"{src}\n{ref}\n{classes}").returncode == 0
+    r = run("labs/lab3/src/to_plot_hip_exe", f"0\n0\n{src}\n{got}\n{classes}",
+            env={"MPX_NGPUS": "5", "MPX_LAB3_PATH": path})
+    assert r.returncode == 0, r.stderr
+    assert got.read_bytes() == ref.read_bytes()

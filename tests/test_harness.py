@@ -146,3 +146,16 @@ def test_harness_lab2_gpu_vs_cpu(tmp_path):
     assert "[Speedup]" in r.stdout
     df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
     assert df["test_verification_result"].all() and (df["gpixel_per_s"] > 0).all()
+
+
+@pytest.mark.gpu
+def test_harness_lab2_gpu_n_gpus_warmup(tmp_path):
+    """--n_gpus / --warmup reach the GPU binary (MPX_NGPUS / MPX_WARMUP) and the
+    CSV records n_gpus."""
+    lab = _copy_lab(tmp_path, "lab2")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "to_plot_hip_exe"), "--k_times", "2", "--kernel_sizes",
+                   json.dumps([[[0, 0], [0, 0]]]), "--n_gpus", "2", "--warmup", "2", "--synthetic", "640x480"],
+                  tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
+    assert df["test_verification_result"].all() and (df["n_gpus"] == 2).all()
