@@ -49,7 +49,7 @@ _SIGNATURES = {
         [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
     ),
     "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
-    "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_vp]),
+    "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_int, c_vp]),
     "mpx_filter_lookup": (c_int, [c_char_p, _ip, _ip, _ip, _fp, _fp]),
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
@@ -69,6 +69,7 @@ _SIGNATURES = {
     "mpx_comm_allreduce": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "mpx_comm_check": (c_int, [c_vp]),
     "mpx_comm_abort": (c_int, [c_vp]),
+    "mpx_comm_stream": (c_vp, [c_vp]),
     "mpx_classify_ex": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_classify_plan": (c_int, [c_int, _dp, _dp, c_int, ctypes.POINTER(ctypes.c_float)]),
     "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),

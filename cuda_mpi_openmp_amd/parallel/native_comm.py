@@ -149,6 +149,12 @@ class NativeComm:
     def check(self) -> None:
         _native.check(self._L.mpx_comm_check(self.handle))
 
+    def comm_stream(self) -> torch.cuda.Stream:
+        """The communicator's own (highest-priority) stream as a torch stream."""
+        if getattr(self, "_cs", None) is None:
+            self._cs = torch.cuda.ExternalStream(self._L.mpx_comm_stream(self.handle), device=self.device)
+        return self._cs
+
     def abort(self) -> None:
         """ncclCommAbort: unblock and free a communicator whose peers are gone."""
         if self.handle:

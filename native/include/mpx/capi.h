@@ -81,7 +81,7 @@ int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h, int k, int
                      const float *wx, const float *wy, void *stream);
 /* Exhaustive check of the fast magnitude path over every float in [0, 65025];
  * adds the number of disagreements with correctly rounded sqrtf to *bad_device. */
-int mpx_selftest_fast_sqrt(unsigned long long *bad_device, void *stream);
+int mpx_selftest_fast_sqrt(unsigned long long *bad_device, int raw, void *stream);
 
 /* Named filter table (native/include/mpx/filters.h). Returns MPX_ERR_ARG for an
  * unknown name; wx/wy receive k*k taps (wy zero-filled for one-filter modes).
@@ -135,6 +135,8 @@ int mpx_comm_allreduce(void *comm, const void *send, void *recv, int64_t count, 
 int mpx_comm_check(void *comm);
 /* ncclCommAbort: release a communicator whose peers hung or died (watchdog) */
 int mpx_comm_abort(void *comm);
+/* the communicator's comm stream (for caller-managed cross-step pipelining) */
+void *mpx_comm_stream(void *comm);
 
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*

@@ -281,3 +281,8 @@ extern "C" int mpx_comm_abort(void *h) {
     c->comm = nullptr;
     return MPX_OK;
 }
+
+// The communicator's comm stream (highest priority, non-blocking): callers that
+// software-pipeline exchanges across steps order work on it with their own
+// events (e.g. torch.cuda.ExternalStream + Event).
+extern "C" void *mpx_comm_stream(void *h) { return h ? static_cast<Comm *>(h)->cstream : nullptr; }

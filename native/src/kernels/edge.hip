@@ -206,12 +206,16 @@ int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // Exhaustive self-test of the fast magnitude path: every float s in
 // [0, 65025] (bit patterns 0 .. 0x477E0100) must map to the same gray level as
 // the correctly rounded sqrtf. Counts mismatches into *bad.
-__global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigned long long *bad) {
+// raw = 0: the production fast path (v_sqrt + fract margin + exact fallback);
+// raw = 1: bare truncation of v_sqrt_f32 with no margin test at all.
+__global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigned long long *bad, int raw) {
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long nbad = 0;
     for (uint32_t u = first + blockIdx.x * blockDim.x + threadIdx.x; u <= last && u >= first; u += stride) {
         const float s = __builtin_bit_cast(float, u);
-        nbad += edge::mag_to_gray<true>(s) != edge::mag_to_gray<false>(s);
+        const uint32_t exact = edge::mag_to_gray<false>(s);
+        const uint32_t fast = raw ? (uint32_t)__builtin_amdgcn_sqrtf(fminf(s, 65025.0f)) : edge::mag_to_gray<true>(s);
+        nbad += fast != exact;
     }
     if (nbad) atomicAdd(bad, nbad);
 }
@@ -354,11 +358,11 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
     return MPX_ERR_ARG;
 }
 
-extern "C" int mpx_selftest_fast_sqrt(unsigned long long *bad_device, void *stream) {
+extern "C" int mpx_selftest_fast_sqrt(unsigned long long *bad_device, int raw, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(bad_device, "null counter");
     hipLaunchKernelGGL(fast_sqrt_selftest_kernel, dim3(kNumCUs * 16), dim3(256), 0, as_stream(stream), 0u,
-                       0x477E0100u, bad_device);
+                       0x477E0100u, bad_device, raw);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }

@@ -41,7 +41,9 @@ __device__ __forceinline__ void mag2_to_gray(float s0, float s1, uint32_t &g0, u
     const float r0 = __builtin_amdgcn_sqrtf(c0), r1 = __builtin_amdgcn_sqrtf(c1);
     const float f0 = __builtin_amdgcn_fractf(r0), f1 = __builtin_amdgcn_fractf(r1);
     constexpr float kHalfOpen = 0.5f - kSqrtMargin;
-    const bool ok = (fabsf(f0 - 0.5f) < kHalfOpen) && (fabsf(f1 - 0.5f) < kHalfOpen);
+    // '&', not '&&': both pixels' tests run unconditionally; a short-circuit
+    // puts the second pixel's sqrt under an exec-mask branch every row
+    const bool ok = (fabsf(f0 - 0.5f) < kHalfOpen) & (fabsf(f1 - 0.5f) < kHalfOpen);
     g0 = (uint32_t)r0;
     g1 = (uint32_t)r1;
     if (!ok) {

@@ -237,3 +237,22 @@ def test_jacobi_sweep(gpu, dtype, shape):
         assert float(res.item()) == r_cpu
     else:
         assert torch.allclose(got.double(), un_ref[1:rows + 1], rtol=1e-6, atol=1e-6)
+
+
+def test_fast_sqrt_exhaustive(gpu, capsys):
+    """Every fp32 magnitude^2 in [0, 65025]: the production fast magnitude
+    (v_sqrt_f32 + fract margin + exact fallback) equals the correctly rounded
+    sqrtf + truncation of the reference. Also reports how many inputs the bare
+    v_sqrt_f32 truncation would get wrong (the reason the margin exists)."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    counts = []
+    for raw in (0, 1):
+        bad = torch.zeros(1, dtype=torch.int64, device=gpu)
+        _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), raw, 0))
+        torch.cuda.synchronize()
+        counts.append(int(bad.item()))
+    with capsys.disabled():
+        print(f"\nfast sqrt mismatches over all fp32 in [0, 65025]: production {counts[0]}, bare v_sqrt {counts[1]}")
+    assert counts[0] == 0

@@ -45,7 +45,7 @@ def main():
 
     # exhaustive fast-sqrt equivalence check
     bad = torch.zeros(1, dtype=torch.int64, device=dev)
-    _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), 0))
+    _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), 0, 0))
     torch.cuda.synchronize()
     print(json.dumps({"fast_sqrt_selftest_mismatches": int(bad.item())}), flush=True)
 

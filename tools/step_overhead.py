@@ -84,6 +84,12 @@ def main():
             step_native()
         for _ in range(15):
             step_inline()
+        ev_conv[0].record()
+        ev_conv[1].record()
+        comm.p2p(plans[0])
+        ev_recv[0].record()
+        for _ in range(15):
+            step_pipelined()
         torch.cuda.synchronize()
         comm.close()
         dist.destroy_process_group()
@@ -92,6 +98,33 @@ def main():
         s = st()
         comm.p2p(plan)
         full(s)
+
+    # software-pipelined: two input buffers; during step k the comm stream
+    # refreshes the halos of buffer (k+1)%2 while the compute stream convolves
+    # buffer k%2 (its halos arrived during step k-1)
+    buf2 = buf.clone()
+    plans = [plan, P2PPlan([(0, buf2[hu:hu + hd], 0), (1, buf2[hu + size:hu + size + hd], 0),
+                            (0, buf2[size:size + hu], 0), (1, buf2[0:hu], 0)])]
+    convs = [full, ops.ConvLauncher(buf2, out, f, src_row0=hu, out_row0=0, oy0=0, oy1=size, y_lo=0,
+                                    y_hi=size - 1)]
+    ev_recv = [torch.cuda.Event(), torch.cuda.Event()]
+    ev_conv = [torch.cuda.Event(), torch.cuda.Event()]
+    cs = comm.comm_stream() if comm is not None else None
+    pstate = {"k": 0}
+
+    def step_pipelined():
+        k = pstate["k"]
+        cur, nxt = k % 2, (k + 1) % 2
+        compute = torch.cuda.current_stream(dev)
+        # comm: halos of the next buffer, after the conv that last read it
+        cs.wait_event(ev_conv[nxt])
+        comm.p2p(plans[nxt], cs)
+        ev_recv[nxt].record(cs)
+        # compute: this step's buffer (its exchange completed a step ago)
+        compute.wait_event(ev_recv[cur])
+        convs[cur](compute.cuda_stream)
+        ev_conv[cur].record(compute)
+        pstate["k"] = k + 1
 
     if comm is not None:
         h, g = host_and_gpu_us(step_native)
@@ -102,6 +135,13 @@ def main():
                           "host_us": round(h, 2), "gpu_us": round(g, 2)}))
         h, g = host_and_gpu_us(lambda: comm.p2p(plan))
         print(json.dumps({"what": "native p2p in-order only", "host_us": round(h, 2), "gpu_us": round(g, 2)}))
+        ev_conv[0].record()
+        ev_conv[1].record()
+        comm.p2p(plans[0])
+        ev_recv[0].record()
+        h, g = host_and_gpu_us(step_pipelined)
+        print(json.dumps({"what": "step N>1 shape, native RCCL software-pipelined (exchange k+1 during conv k)",
+                          "host_us": round(h, 2), "gpu_us": round(g, 2)}))
         h, g = host_and_gpu_us(lambda: (comm.p2p_start(plan), comm.p2p_wait()))
         print(json.dumps({"what": "native p2p start+wait only", "host_us": round(h, 2), "gpu_us": round(g, 2)}))
     else:
