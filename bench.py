@@ -77,9 +77,10 @@ def main() -> int:
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--size", type=int, default=4096, help="image side per GPU slab")
     p.add_argument("--filter", default="sobel5")
-    p.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+    p.add_argument("--overlap", choices=["auto", "on", "off", "pipeline"], default="auto",
                    help="halo transfer overlapped with the interior rows (on), in order before one full launch "
-                        "(off), or the measured-faster choice for the transport in use (auto)")
+                        "(off), exchanged one step ahead on the comm stream with double-buffered input (pipeline; "
+                        "native RCCL tier), or the measured-faster choice for the transport in use (auto)")
     p.add_argument("--watchdog", type=float, default=None,
                    help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -92,7 +93,7 @@ def main() -> int:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
     n = ctx.world
     det = SlabEdgeDetector(ctx, args.size * n, args.size, args.filter,
-                           overlap={"auto": "auto", "on": True, "off": False}[args.overlap])
+                           overlap={"auto": "auto", "on": True, "off": False, "pipeline": "pipeline"}[args.overlap])
     det.fill_random(seed=1234 + ctx.rank)
     sync(ctx)
     ctx.barrier()
@@ -111,6 +112,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         det.step()
+    det.finish()
     sync(ctx)
     ctx.barrier()
     t1 = time.perf_counter()
@@ -150,7 +152,8 @@ def main() -> int:
                          f"{det.filter.k}x{det.filter.k} filter ({det.filter.name}, wave-streaming HIP kernel)",
                 "global_batch": n,
                 "seq_len": args.size,
-                "parallelism": f"slab{n}" + (("+halo-overlap" if det.overlap else "+halo-inorder") if n > 1 else ""),
+                "parallelism": f"slab{n}" + (("+halo-pipelined" if det.pipeline else "+halo-overlap" if det.overlap
+                                              else "+halo-inorder") if n > 1 else ""),
                 "transport": ("native-rccl" if ctx.native is not None else "torch.distributed") if n > 1 else None,
                 "image_hw": [args.size * n, args.size],
                 "halo_rows": [det.filter.halo_up, det.filter.halo_down],

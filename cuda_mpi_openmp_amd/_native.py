@@ -54,6 +54,7 @@ _SIGNATURES = {
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
     "mpx_classify": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp]),
+    "mpx_jacobi_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp]),
     "mpx_comm_load": (c_int, [ctypes.c_char_p]),
     "mpx_comm_version": (c_int, []),
     "mpx_comm_unique_id": (c_int, [c_vp, c_int]),

@@ -39,7 +39,24 @@ class EdgeDetector:
 
 
 class SlabEdgeDetector:
-    """One rank's share of a row-decomposed image convolution."""
+    """One rank's share of a row-decomposed image convolution.
+
+    ``overlap`` selects how a step's halo exchange meets its convolution:
+
+    * ``False`` ("inorder"): exchange, then one launch for every row, both in
+      order on the compute stream;
+    * ``True`` ("overlap"): exchange on a second queue while the interior rows
+      are convolved, then the boundary rows;
+    * ``"pipeline"`` (native RCCL tier only): software-pipelined over steps —
+      two input buffers; during step k the comm stream refreshes the halos of
+      the buffer step k+1 will read while the compute stream convolves the
+      buffer whose halos arrived during step k-1. Every step still performs a
+      full exchange and a full convolution; the exchange simply runs one step
+      ahead (a frame of latency, no loss of throughput), and the compute
+      stream only ever waits on an exchange that finished a step earlier.
+    * ``"auto"``: ``False`` with the native tier, ``True`` without (measured,
+      profiles/comm_step.md).
+    """
 
     def __init__(self, ctx: DistContext, global_h: int, w: int, filt: str | Filter = "sobel5",
                  overlap: bool | str = "auto"):
@@ -55,31 +72,56 @@ class SlabEdgeDetector:
         # 7-16 us; profiles/comm_step.md); torch.distributed keeps the overlap.
         if overlap == "auto":
             overlap = ctx.native is None
-        self.overlap = bool(overlap)
+        self.pipeline = overlap == "pipeline" and ctx.native is not None and ctx.device.type == "cuda"
+        self.overlap = bool(overlap) and not self.pipeline and overlap != "pipeline"
         dev = ctx.device
-        self.buf = torch.empty((self.slab.buffer_rows, w, 4), dtype=torch.uint8, device=dev)
+        nbuf = 2 if self.pipeline else 1
+        self.bufs = [torch.empty((self.slab.buffer_rows, w, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
         self.out = torch.empty((self.slab.rows, w, 4), dtype=torch.uint8, device=dev)
         # pre-validated launches for the three row ranges of a step
         s = self.slab
-        mk = lambda a, b: ops.ConvLauncher(self.buf, self.out, self.filter, src_row0=s.own_offset,  # noqa: E731
-                                          out_row0=0, oy0=a, oy1=b, y_lo=s.y_lo, y_hi=s.y_hi)
-        self._all = mk(0, s.rows)
-        self._interior = mk(*s.interior())
-        self._boundary = [mk(a, b) for a, b in s.boundary()]
+        mk = lambda b, lo, hi: ops.ConvLauncher(b, self.out, self.filter, src_row0=s.own_offset,  # noqa: E731
+                                               out_row0=0, oy0=lo, oy1=hi, y_lo=s.y_lo, y_hi=s.y_hi)
+        self._all_b = [mk(b, 0, s.rows) for b in self.bufs]
+        self._all = self._all_b[0]
+        self._interior = mk(self.bufs[0], *s.interior())
+        self._boundary = [mk(self.bufs[0], a, b) for a, b in s.boundary()]
         self._traced = trace.enabled()  # roctx ranges only when MPX_ROCTX=1
+        self._k = 0          # steps issued (pipeline mode)
+        self._primed = False
+        if self.pipeline:
+            self._ev_recv = [torch.cuda.Event(), torch.cuda.Event()]
+            self._ev_conv = [torch.cuda.Event(), torch.cuda.Event()]
+
+    @property
+    def buf(self) -> torch.Tensor:
+        """The input buffer the most recent (or next, before any step) step reads."""
+        return self.bufs[(self._k - 1) % len(self.bufs)] if self._k else self.bufs[0]
 
     @property
     def own(self) -> torch.Tensor:
         s = self.slab
         return self.buf[s.own_offset: s.own_offset + s.rows]
 
+    def _drain_comm(self) -> None:
+        if self.pipeline:
+            self.ctx.native.comm_stream().synchronize()
+            self._primed = False
+
     def load(self, slab_rows: torch.Tensor) -> None:
-        self.own.copy_(slab_rows)
+        self._drain_comm()
+        s = self.slab
+        for b in self.bufs:
+            b[s.own_offset: s.own_offset + s.rows].copy_(slab_rows)
 
     def fill_random(self, seed: int) -> None:
-        g = torch.Generator(device=self.buf.device)
+        self._drain_comm()
+        g = torch.Generator(device=self.bufs[0].device)
         g.manual_seed(seed)
-        self.own.copy_(torch.randint(0, 256, self.own.shape, dtype=torch.uint8, device=self.buf.device, generator=g))
+        s = self.slab
+        rows = torch.randint(0, 256, (s.rows, self.w, 4), dtype=torch.uint8, device=self.bufs[0].device, generator=g)
+        for b in self.bufs:
+            b[s.own_offset: s.own_offset + s.rows].copy_(rows)
 
     def _rows(self, a: int, b: int) -> None:
         s = self.slab
@@ -94,6 +136,8 @@ class SlabEdgeDetector:
         return self._step()
 
     def _step(self) -> torch.Tensor:
+        if self.pipeline:
+            return self._step_pipelined()
         st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
         if not self.ctx.is_distributed:
             self._all(st)
@@ -108,3 +152,33 @@ class SlabEdgeDetector:
             self.halo.exchange(self.buf)
             self._all(st)
         return self.out
+
+    def _step_pipelined(self) -> torch.Tensor:
+        nc = self.ctx.native
+        cs = nc.comm_stream()
+        compute = torch.cuda.current_stream(self.out.device)
+        if not self._primed:
+            # halos of the first buffer, in order; both buffers free to overwrite
+            for ev in self._ev_conv:
+                ev.record(compute)
+            cs.wait_stream(compute)
+            nc.p2p(self.halo._plan(self.bufs[self._k % 2]), cs)
+            self._ev_recv[self._k % 2].record(cs)
+            self._primed = True
+        cur, nxt = self._k % 2, (self._k + 1) % 2
+        # comm stream: refresh the next buffer's halos once the conv that last
+        # read that buffer has finished (write-after-read on its halo rows)
+        cs.wait_event(self._ev_conv[nxt])
+        nc.p2p(self.halo._plan(self.bufs[nxt]), cs)
+        self._ev_recv[nxt].record(cs)
+        # compute stream: this step's buffer; its exchange was issued a step ago
+        compute.wait_event(self._ev_recv[cur])
+        self._all_b[cur](compute.cuda_stream)
+        self._ev_conv[cur].record(compute)
+        self._k += 1
+        return self.out
+
+    def finish(self) -> None:
+        """Join the comm stream into the current stream (end of a timed run)."""
+        if self.pipeline and self._primed:
+            torch.cuda.current_stream(self.out.device).wait_stream(self.ctx.native.comm_stream())

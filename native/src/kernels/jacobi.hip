@@ -155,7 +155,7 @@ __device__ __forceinline__ T dpp_shift(T v, int ctrl) {
     }
 }
 
-template <typename T>
+template <typename T, int AUX = 0>
 __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
                                                           int nwaves, T *__restrict__ resid) {
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
             const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
                 un + (int64_t)min(r, i1 - 1) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, AUX);
             // keep each step's prefetch at its start: the scheduler otherwise sinks
             // loads past the next step's use and the wait counts collapse to 0
             __builtin_amdgcn_sched_barrier(0);
@@ -255,7 +255,7 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
         int R = 64;
         while (R > 4 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
-        hipLaunchKernelGGL((jacobi_wave_kernel<T>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
+        hipLaunchKernelGGL((jacobi_wave_kernel<T, 0>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
                            cols, pitch, r0, r1, strips, R, nwaves, resid);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;
@@ -284,4 +284,30 @@ extern "C" int mpx_jacobi_f64(const double *u, double *un, int cols, int pitch, 
 extern "C" int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r1, float *resid,
                               void *stream) {
     return mpx::launch_jacobi<float>(u, un, cols, pitch, r0, r1, resid, stream);
+}
+
+// Tuning entry point (tools/jbench.py): wave kernel with an explicit rows-per-
+// wave R and buffer-store cache policy aux (0 default, 2 = nontemporal).
+extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0, int r1, void *resid, int fp64,
+                                  int R, int aux, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(u && un && cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0 && R >= 1, "bad arguments");
+    MPX_CHECK_ARG(aux == 0 || aux == 2, "aux must be 0 or 2");
+    const int NV = fp64 ? 2 : 4;
+    MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un), "needs the vector layout");
+    const int strips = (cols / NV + kStripVec - 1) / kStripVec;
+    const int nwaves = strips * ((r1 - r0 + R - 1) / R);
+    const dim3 g((nwaves + 3) / 4), b(256);
+    hipStream_t s = as_stream(stream);
+#define MPX_JV(T, A)                                                                                          \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, A>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, \
+                       R, nwaves, (T *)resid)
+    if (fp64) {
+        if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
+    } else {
+        if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
+    }
+#undef MPX_JV
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
 }

@@ -144,8 +144,9 @@ def test_slab_conv_equals_single(world, filt, tmp_path):
     run_world(world, "conv_worker", 37, 29, filt, True, str(tmp_path))
 
 
-def test_slab_conv_no_overlap(tmp_path):
-    run_world(2, "conv_worker", 20, 16, "sobel5", False, str(tmp_path))
+@pytest.mark.parametrize("mode", [False, "pipeline"])
+def test_slab_conv_no_overlap(mode, tmp_path):
+    run_world(2, "conv_worker", 20, 16, "sobel5", mode, str(tmp_path))
 
 
 def test_slab_jacobi_equals_single(tmp_path):

@@ -138,3 +138,29 @@ def test_p2p_host_overhead(world1, gpu):
     torch.cuda.synchronize(gpu)
     print(f"native p2p start+wait host cost: {host_us:.1f} us")
     assert host_us < 500
+
+
+@pytest.mark.gpu
+def test_slab_edge_pipelined_world1(world1, gpu):
+    """Pipelined SlabEdgeDetector on a world-of-one native communicator: the
+    double-buffer / event protocol must give the same image every step."""
+    from cuda_mpi_openmp_amd import ops
+    from cuda_mpi_openmp_amd.models import SlabEdgeDetector
+
+    ctx, comm = world1
+    ctx = parallel.DistContext(rank=0, world=1, local_rank=0, device=gpu, backend="nccl", native=comm)
+    det = SlabEdgeDetector(ctx, 512, 384, "sobel5", overlap="pipeline")
+    assert det.pipeline and len(det.bufs) == 2
+    det.fill_random(seed=3)
+    ref = ops.conv(det.own.contiguous(), "sobel5")
+    for _ in range(5):
+        out = det.step()
+        det.finish()
+        torch.cuda.synchronize(gpu)
+        assert torch.equal(out, ref)
+    img = torch.randint(0, 256, (512, 384, 4), dtype=torch.uint8, device=gpu)
+    det.load(img)  # drains the comm stream first
+    out = det.step()
+    det.finish()
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(out, ops.conv(img, "sobel5"))
