@@ -1,0 +1,49 @@
+"""bench.py driver contract (task spec): one JSON line from rank 0 with the
+required keys, run here under torchrun with two gloo ranks on CPU."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+from .helpers import ROOT
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(args, nproc=None):
+    cmd = [sys.executable]
+    if nproc:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
+                "127.0.0.1", "--master-port", str(_port())]
+    cmd += [os.path.join(ROOT, "bench.py"), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_contract_two_ranks_cpu():
+    rec = _run(["--gpus", "2", "--device", "cpu", "--size", "96", "--steps", "3", "--warmup", "1"], nproc=2)
+    assert REQUIRED <= set(rec)
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1 and rec["scaling"] == "weak"
+    assert rec["higher_is_better"] is True and rec["value"] > 0 and rec["verified_bit_exact"] is True
+    assert rec["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert rec["config"]["parallelism"].startswith("slab2")
+    # value is the whole-job aggregate: N * size^2 * steps / time
+    assert abs(rec["value"] - 2 * 96 * 96 / (rec["ms_per_step"] * 1e-3) / 1e9) < 1e-3 * max(1.0, rec["value"])
+
+
+def test_bench_contract_single_process_cpu():
+    rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--overlap", "pipeline"])
+    assert REQUIRED <= set(rec) and rec["n_gpus"] == 1
