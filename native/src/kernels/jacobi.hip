@@ -250,12 +250,16 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
     if ((pitch % NV == 0) && (cols % NV == 0) && aligned16(u) && aligned16(un)) {
         const int strips = (cols / NV + kStripVec - 1) / kStripVec;
         const int rows = r1 - r0;
-        // long row runs amortise the two halo rows; shorten them until the
-        // launch has >= 16384 waves (16 per SIMD)
-        int R = 64;
-        while (R > 4 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
+        // 4 rows per wave (tools/jbench.py, profiles/jacobi.md: 16384^2 fp64
+        // R4 781 us / R16 818 / R64 913 — many short waves hide HBM latency
+        // better than amortising the two halo rows, which neighbouring waves
+        // re-read from L2); stores nontemporal (aux NT): the next sweep reads
+        // u_new from HBM anyway, and keeping it out of L2 leaves L2 to those
+        // shared halo rows
+        int R = 4;
+        while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
-        hipLaunchKernelGGL((jacobi_wave_kernel<T, 0>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
+        hipLaunchKernelGGL((jacobi_wave_kernel<T, 2>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
                            cols, pitch, r0, r1, strips, R, nwaves, resid);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;

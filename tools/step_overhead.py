@@ -79,21 +79,6 @@ def main():
         b_top(s)
         b_bot(s)
 
-    if comm is not None and only_native:
-        for _ in range(15):
-            step_native()
-        for _ in range(15):
-            step_inline()
-        ev_conv[0].record()
-        ev_conv[1].record()
-        comm.p2p(plans[0])
-        ev_recv[0].record()
-        for _ in range(15):
-            step_pipelined()
-        torch.cuda.synchronize()
-        comm.close()
-        dist.destroy_process_group()
-        return
     def step_inline():
         s = st()
         comm.p2p(plan)
@@ -126,6 +111,21 @@ def main():
         ev_conv[cur].record(compute)
         pstate["k"] = k + 1
 
+    if comm is not None and only_native:
+        for _ in range(15):
+            step_native()
+        for _ in range(15):
+            step_inline()
+        ev_conv[0].record()
+        ev_conv[1].record()
+        comm.p2p(plans[0])
+        ev_recv[0].record()
+        for _ in range(15):
+            step_pipelined()
+        torch.cuda.synchronize()
+        comm.close()
+        dist.destroy_process_group()
+        return
     if comm is not None:
         h, g = host_and_gpu_us(step_native)
         print(json.dumps({"what": "step N>1 shape, native RCCL fork/join overlap (self exchange)",
