@@ -22,7 +22,9 @@ def main():
         un = torch.empty_like(u)
         ref = torch.empty_like(u)
         ops.jacobi_sweep(u, ref, 1, n + 1)
-        var = {"production": lambda: ops.jacobi_sweep(u, un, 1, n + 1)}
+        res_t = torch.zeros(1, dtype=dt, device=dev)
+        var = {"production": lambda: ops.jacobi_sweep(u, un, 1, n + 1),
+               "production+residual": lambda: (res_t.zero_(), ops.jacobi_sweep(u, un, 1, n + 1, res_t))}
         for R in (4, 8, 16, 32, 64):
             for aux in (0, 2):
                 var[f"R{R}/aux{aux}"] = (lambda R=R, aux=aux: _native.check(L.mpx_jacobi_variant(
