@@ -35,14 +35,17 @@ from ..parallel.slab import Slab
 
 class SlabJacobi:
     def __init__(self, ctx: DistContext, global_rows: int, cols: int, dtype=torch.float64, check_every: int = 10,
-                 overlap: bool = True):
+                 overlap: bool | str = "auto"):
         if cols < 3:
             raise ValueError("need at least 3 columns")
         self.ctx = ctx
         self.cols = cols
         self.dtype = dtype
         self.check_every = max(1, int(check_every))
-        self.overlap = overlap
+        # "auto": in order with the native RCCL tier (a cross-queue join costs
+        # ~10 us on MI355X, more than the 1-row halo transfer it would hide;
+        # profiles/comm_step.md), overlapped on torch.distributed
+        self.overlap = (ctx.native is None) if overlap == "auto" else bool(overlap)
         self.slab = Slab(global_rows, ctx.world, ctx.rank, halo_up=1, halo_down=1)
         self.halo = HaloExchange(self.slab, ctx)
         shape = (self.slab.buffer_rows, cols)

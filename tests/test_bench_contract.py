@@ -47,3 +47,13 @@ def test_bench_contract_two_ranks_cpu():
 def test_bench_contract_single_process_cpu():
     rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--overlap", "pipeline"])
     assert REQUIRED <= set(rec) and rec["n_gpus"] == 1
+
+
+def test_bench_jacobi_two_ranks_cpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tools", "bench_jacobi.py"), "--device", "cpu",
+           "--size", "64", "--iters", "12", "--warmup", "2", "--check-every", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong" and rec["residual"] is not None and rec["value"] > 0
