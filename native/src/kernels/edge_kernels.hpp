@@ -455,15 +455,15 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     uint2 pre[D];         // prefetch ring: raw pixels of input rows i .. i+D-1
     f2_t we[K][NE];       // window ring, even pairs (register-pair aligned for v_pk_fma_f32)
     f2_t wo[K][NO > 0 ? NO : 1];  // window ring, odd pairs
-    uint32_t alp0[K], alp1[K];  // alpha ring, kept in place (bits 24-31)
+    uint32_t alp0[K], alp1[K];  // raw source pixels of the centre row (alpha = byte 3)
 
     // consume the input row in window slot u: luminance (packed), alpha, and the
     // horizontal window w[0 .. NV-1] = columns cin-A .. cin+1+R from the
     // neighbouring lanes by DPP wave shifts
     auto consume = [&](int u, uint2 px) {
         const f2_t l = luma2(px.x, px.y);
-        alp0[u] = px.x & 0xff000000u;
-        alp1[u] = px.y & 0xff000000u;
+        alp0[u] = px.x;  // raw pixel: v_perm takes its alpha byte at compose time
+        alp1[u] = px.y;
         float wv[NV];
         wv[A] = l.x;
         wv[A + 1] = l.y;
@@ -533,9 +533,11 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
                 g0 = finish_gray<MODE, FAST>(gx.x, 0.0f);
                 g1 = finish_gray<MODE, FAST>(gx.y, 0.0f);
             }
-            // gray = g * 0x010101 + alpha: one v_mad_u32_u24 per pixel
-            const uint32_t v0 = __umul24(g0, 0x010101u) + alp0[(u + 1 + A) % K];
-            const uint32_t v1 = __umul24(g1, 0x010101u) + alp1[(u + 1 + A) % K];
+            // (g, g, g, alpha): one v_perm_b32 per pixel — selector bytes 0-2
+            // take g's low byte (g <= 255), byte 3 takes the source pixel's
+            // alpha (selector 7 = byte 3 of the first operand); no alpha mask
+            const uint32_t v0 = __builtin_amdgcn_perm(alp0[(u + 1 + A) % K], g0, 0x07000000u);
+            const uint32_t v1 = __builtin_amdgcn_perm(alp1[(u + 1 + A) % K], g1, 0x07000000u);
             // Branch-free stores: a buffer descriptor spanning exactly this
             // output row; lanes (or padded rows) with nothing to store get an
             // out-of-range offset and the hardware bounds check drops them.
