@@ -77,7 +77,10 @@ class Lab1Processor(LabProcessor):
         return {"min_vector_size": self.min_vector_size, "max_vector_size": self.max_vector_size, "atol": self.atol}
 
     def pre_process(self, **kwargs):
-        n = int(self.rng.randint(self.min_vector_size, self.max_vector_size))
+        # reference draw: randint(min, max) (upper bound exclusive); a fixed
+        # size (min == max) is that size instead of numpy's ValueError
+        lo, hi = self.min_vector_size, self.max_vector_size
+        n = int(self.rng.randint(lo, hi)) if hi > lo else int(lo)
         a = self.rng.uniform(self.lo, self.hi, n)
         b = self.rng.uniform(self.lo, self.hi, n)
         return f"{n}\n{fmt_vector(a)}\n{fmt_vector(b)}", {"first_vector": a, "second_vector": b}, {"vector_size": n}

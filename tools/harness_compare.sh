@@ -16,6 +16,7 @@ for bucket in small medium large; do
       --k_times 12 --kernel_sizes "$GEOMS2" --timing $timing --dir_to_data labs/lab2/metric_calc/$bucket --dir_to_data_out $W/data_out \
       --metadata_columns2plot '["filename"]' > $W/run.log 2>&1 || { tail -20 $W/run.log; exit 1; }
     grep -E "SUCCESS|FAILED|Speedup" $W/run.log | head -5
+    rm -rf $W/data_out $W/src/*.png
   done
 done
 GEOMS1='[[1,32],[4,64],[32,128],[512,512],[1024,1024],[0,0]]'
