@@ -16,6 +16,7 @@
 
 int main() {
     using namespace mpx::host;
+    eager_code_objects();
     Scanner in;
     int grid = 512, block = 512;  // reference submission launch <<<512, 512>>>
 #ifndef MPX_SUBMISSION
@@ -23,6 +24,7 @@ int main() {
         std::fprintf(stderr, "[ERROR CPU] expected launch geometry <grid> <block> on stdin\n");
         return 1;
     }
+    tuned_if_nonpositive(grid, block);
 #endif
     int n = 0;
     if (!in.next_int(n) || n < 0) {

@@ -43,7 +43,7 @@ __device__ __forceinline__ void mag2_to_gray(float s0, float s1, uint32_t &g0, u
     constexpr float kHalfOpen = 0.5f - kSqrtMargin;
     // '&', not '&&': both pixels' tests run unconditionally; a short-circuit
     // puts the second pixel's sqrt under an exec-mask branch every row
-    const bool ok = (fabsf(f0 - 0.5f) < kHalfOpen) & (fabsf(f1 - 0.5f) < kHalfOpen);
+    const bool ok = (int)(fabsf(f0 - 0.5f) < kHalfOpen) & (int)(fabsf(f1 - 0.5f) < kHalfOpen);
     g0 = (uint32_t)r0;
     g1 = (uint32_t)r1;
     if (!ok) {

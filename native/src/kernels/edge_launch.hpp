@@ -1,0 +1,99 @@
+// Launch helpers of the lab2 wave-streaming / LDS-streaming kernels, shared by
+// the translation units that instantiate them (edge.hip: generic production
+// conv; edge_roberts.hip: Roberts; edge_variants.hip: tuning entry points).
+// Each TU is its own code object, loaded by HIP on first use, so a program that
+// only runs Roberts loads only the Roberts kernels (cold-launch time).
+#pragma once
+
+#include <algorithm>
+
+#include "edge_kernels.hpp"
+
+namespace mpx {
+namespace edgel {
+using edge::Taps;
+
+inline Taps make_taps(int k, const float *wx, const float *wy, bool two) {
+    Taps t{};
+    for (int i = 0; i < k * k; ++i) {
+        t.wx[i] = wx[i];
+        t.wy[i] = two ? wy[i] : 0.0f;
+    }
+    return t;
+}
+
+// Production tile: RPT = 8 rows per wave -> 128 x 32 output tiles.
+// resident workgroups per CU the chunking targets (VGPR-limited to 4 at ~100 VGPRs)
+inline constexpr int kBlocksPerCU = 4;
+
+template <int K, int A, int MODE, int RPT, bool FAST>
+int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                  const Taps &taps, bool vec, hipStream_t s, int chunk_override = 0) {
+    constexpr int TH = edge::kTY * RPT;
+    const int strips = (w + edge::kTW - 1) / edge::kTW;
+    const int tiles_y = (oy1 - oy0 + TH - 1) / TH;
+    const int64_t total = (int64_t)strips * tiles_y;
+    const int64_t target = (int64_t)kNumCUs * kBlocksPerCU;
+    int chunk = chunk_override > 0 ? chunk_override : (int)std::max<int64_t>(1, (total + target - 1) / target);
+    chunk = std::min(chunk, tiles_y);
+    const int cps = (tiles_y + chunk - 1) / chunk;
+    const int64_t nblk = (int64_t)strips * cps;
+    MPX_CHECK_ARG(nblk < (int64_t)1 << 31, "image too large for one launch");
+    if (vec)
+        hipLaunchKernelGGL((edge::conv_stream_kernel<K, A, MODE, RPT, true, FAST>), dim3((unsigned)nblk), dim3(256), 0,
+                           s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_y, chunk, cps, taps);
+    else
+        hipLaunchKernelGGL((edge::conv_stream_kernel<K, A, MODE, RPT, false, FAST>), dim3((unsigned)nblk), dim3(256), 0,
+                           s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, tiles_y, chunk, cps, taps);
+    return MPX_OK;
+}
+
+// rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
+inline constexpr int kSegRows = 8;
+
+template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0>
+int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1) {
+    using G = edge::WaveGeom<K, A, OWX>;
+    const int strips = (w + G::OW - 1) / G::OW;
+    const int segs = (oy1 - oy0 + seg - 1) / seg;
+    const int64_t nwaves = (int64_t)strips * segs;
+    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
+    const unsigned nblk = (unsigned)((nwaves + 3) / 4);
+    if (vec)
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+    else
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+    return MPX_OK;
+}
+
+// Named filters whose taps are compiled in (zero taps disappear); selected
+// whenever the caller's taps are bit-identical to them.
+template <class F, int N>
+inline bool same_taps(const Taps &t) {
+    for (int i = 0; i < N; ++i)
+        if (__builtin_bit_cast(uint32_t, t.wx[i]) != __builtin_bit_cast(uint32_t, F::wx[i]) ||
+            __builtin_bit_cast(uint32_t, t.wy[i]) != __builtin_bit_cast(uint32_t, F::wy[i]))
+            return false;
+    return true;
+}
+
+template <int K, int A, int MODE>
+int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                 const Taps &taps, bool vec, hipStream_t s) {
+    if constexpr (K == 2 && A == 0 && MODE == MPX_CONV_MAG2) {
+        if (same_taps<edge::RobertsTaps, 4>(taps))
+            return launch_wave<K, A, MODE, true, edge::RobertsTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
+        if (same_taps<edge::Sobel5Taps, 25>(taps))
+            return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+}
+
+
+}  // namespace edgel
+}  // namespace mpx

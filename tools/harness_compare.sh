@@ -19,7 +19,7 @@ for bucket in small medium large; do
     rm -rf $W/data_out $W/src/*.png
   done
 done
-GEOMS1='[[1,32],[4,64],[32,128],[512,512],[1024,1024],[0,0]]'
+GEOMS1='[[1,32],[4,64],[32,128],[512,512],[1024,1024],[-1,-1]]'
 for n in 1000 10000 1000000; do
   for timing in cold warm; do
     W=$O/lab1_${n}_${timing}/lab1; mkdir -p $W/src
