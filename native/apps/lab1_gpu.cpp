@@ -16,7 +16,6 @@
 
 int main() {
     using namespace mpx::host;
-    eager_code_objects();
     Scanner in;
     int grid = 512, block = 512;  // reference submission launch <<<512, 512>>>
 #ifndef MPX_SUBMISSION

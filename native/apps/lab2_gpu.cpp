@@ -22,7 +22,6 @@
 
 int main(int argc, char **argv) {
     using namespace mpx::host;
-    eager_code_objects();
     std::string op = "roberts";
     if (const char *e = std::getenv("MPX_LAB2_OP")) op = e;
     for (int i = 1; i + 1 < argc; ++i)

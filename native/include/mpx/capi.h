@@ -33,6 +33,9 @@ enum mpx_status {
 
 const char *mpx_last_error(void);
 const char *mpx_version(void);
+/* Loads every libmpx code object on the current device now instead of at the
+ * first launch of one of its kernels (HIP loads them lazily, ~0.25 ms each). */
+int mpx_preload_modules(void);
 
 /* ---------------- device queries ---------------- */
 int mpx_device_count(int *count);

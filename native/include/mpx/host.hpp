@@ -67,9 +67,9 @@ class DeviceBuffer {
 // Kernel-only timing like the reference (events bracket the launch only,
 // reference lab2/src/to_plot.cu:101-120). MPX_TIMING selects the policy:
 //   cold      : time the very first launch of the kernel (the reference's
-//               methodology: one launch per process). Code objects load at
-//               start-up and the stream's queue exists (init_stream_queue), as
-//               in a CUDA context; the kernel's own first dispatch is timed;
+//               methodology: one launch per process). Code objects are loaded
+//               and the stream has dispatched once (init_stream_queue), as in
+//               a CUDA context; the kernel's own first dispatch is timed;
 //   warm      : one untimed warm-up launch, then time one launch (default);
 //   median:N  : warm-up, then the median of N timed launches.
 // MPX_WARMUP=W overrides the number of untimed launches (harness --warmup W).
@@ -97,12 +97,16 @@ struct TimingPolicy {
     }
 };
 
-// HIP creates a stream's hardware queue at its first kernel dispatch (CUDA
-// does it at context creation), ~0.4 ms on MI355X. One empty dispatch before
-// the timer starts keeps that runtime set-up out of every policy, 'cold'
+// Runtime set-up that CUDA performs at context creation but HIP defers to the
+// first launch: loading each code object (~0.25 ms per module, measured with
+// AMD_LOG_LEVEL=4, profiles/harness_vs_published.md) and the first dispatch on
+// the stream. Done before the timer starts under every policy, 'cold'
 // included: the measured kernel itself still runs for the first time.
+// (HIP_ENABLE_DEFERRED_LOADING=0 would do the same, but HIP reads it before
+// main(), so it only works when set by the caller's environment.)
 __global__ void mpx_runtime_noop_kernel() {}
 inline void init_stream_queue(hipStream_t stream) {
+    MPX_CHECK(mpx_preload_modules());
     hipLaunchKernelGGL(mpx_runtime_noop_kernel, dim3(1), dim3(64), 0, stream);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -138,13 +142,6 @@ float time_kernel(F &&launch, hipStream_t stream = nullptr) {
 }
 
 // ---- program start-up ----
-// Load every code object when the HIP runtime initialises instead of at the
-// first launch of each (HIP's default is deferred loading): the timed first
-// launch of the 'cold' policy then measures a cold dispatch of a resident
-// kernel, like CUDA_MODULE_LOADING=EAGER, not the one-off ELF load. An
-// explicit HIP_ENABLE_DEFERRED_LOADING in the environment wins. Call before
-// any HIP API.
-inline void eager_code_objects() { setenv("HIP_ENABLE_DEFERRED_LOADING", "0", 0); }
 
 // Harness geometries arrive on stdin only when both values are truthy
 // (reference tester.py:113-121), so "tuned launch" is spelled as non-positive

@@ -26,6 +26,26 @@ void set_error(const char *fmt, ...) {
 
 }  // namespace mpx
 
+namespace mpx {
+const void *module_anchor_vsub();
+const void *module_anchor_jacobi();
+const void *module_anchor_classify();
+const void *module_anchor_edge();
+const void *module_anchor_edge_roberts();
+const void *module_anchor_edge_variants();
+}  // namespace mpx
+
+extern "C" int mpx_preload_modules(void) {
+    const void *anchors[] = {mpx::module_anchor_vsub(),         mpx::module_anchor_jacobi(),
+                             mpx::module_anchor_classify(),     mpx::module_anchor_edge(),
+                             mpx::module_anchor_edge_roberts(), mpx::module_anchor_edge_variants()};
+    for (const void *k : anchors) {
+        hipFuncAttributes attr;
+        MPX_RETURN_IF_HIP_ERROR(hipFuncGetAttributes(&attr, k));
+    }
+    return MPX_OK;
+}
+
 extern "C" const char *mpx_last_error(void) { return mpx::g_last_error.c_str(); }
 
 extern "C" const char *mpx_version(void) { return "mpx 0.1.0 (gfx950)"; }

@@ -468,6 +468,8 @@ int classify_plan_impl(int nc, const double *mu, const double *inv, int path, fl
     return classify_choose(nc, path, ok);
 }
 
+MPX_MODULE_ANCHOR(classify)
+
 }  // namespace mpx
 
 extern "C" int mpx_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid,

@@ -105,6 +105,8 @@ int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int 
     return MPX_OK;
 }
 
+MPX_MODULE_ANCHOR(edge)
+
 }  // namespace mpx
 
 extern "C" int mpx_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,

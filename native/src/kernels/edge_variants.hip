@@ -28,6 +28,8 @@ __global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigne
 }
 
 }  // namespace
+MPX_MODULE_ANCHOR(edge_variants)
+
 }  // namespace mpx
 
 // Variant entry for the tuning harness (tools/kbench.py), k in {2, 5}, MAG2,

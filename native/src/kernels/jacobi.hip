@@ -289,6 +289,8 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
 }
 
 }  // namespace
+MPX_MODULE_ANCHOR(jacobi)
+
 }  // namespace mpx
 
 extern "C" int mpx_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1, double *resid,

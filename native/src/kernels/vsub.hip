@@ -87,6 +87,8 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
 }
 
 }  // namespace
+MPX_MODULE_ANCHOR(vsub)
+
 }  // namespace mpx
 
 extern "C" int mpx_vsub_f64(const double *a, const double *b, double *c, int64_t n, int grid, int block,
