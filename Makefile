@@ -43,6 +43,9 @@ apps: $(GPU_APPS) $(CPU_APPS) $(MISC_APPS)
 $(B):
 	@mkdir -p $(B) bin cuda_mpi_openmp_amd/_lib
 
+$(LABS):
+	@mkdir -p $@
+
 $(B)/k_%.o: native/src/kernels/%.hip $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -59,7 +62,7 @@ $(B)/capi.o: native/src/core/capi.cpp $(HDRS) | $(B)
 $(B)/comm.o: native/src/core/comm.cpp $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(B)/cpu_kernels.o: native/src/cpu/cpu_kernels.c $(HDRS) | $(B)
+$(B)/cpu_kernels.o: native/src/cpu/cpu_kernels.c $(HDRS) | $(LABS)
 	$(CC) $(COPT) -c $< -o $@
 
 $(PYLIB): $(LIB_OBJS) | $(B)
@@ -69,20 +72,20 @@ $(ALIB): $(LIB_OBJS) | $(B)
 	rm -f $@ && ar rcs $@ $(LIB_OBJS)
 
 # ---- GPU programs: two personalities from one source ----
-labs/lab%/src/to_plot_hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS)
+labs/lab%/src/to_plot_hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS) | $(LABS)
 	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
 
-labs/lab%/src/hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS)
+labs/lab%/src/hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS) | $(LABS)
 	$(HIPCC) $(HIPFLAGS) -DMPX_SUBMISSION $< -x none $(ALIB) -lgomp -lm -ldl -o $@
 
 # ---- CPU references: serial -O0 (published methodology) and OpenMP -O3 ----
-labs/lab%/src/cpu_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS)
+labs/lab%/src/cpu_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS) | $(LABS)
 	$(CC) $(CSER) $< native/src/cpu/cpu_kernels.c -lm -o $@
 
-labs/lab%/src/cpu_omp_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS)
+labs/lab%/src/cpu_omp_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS) | $(LABS)
 	$(CC) $(COPT) $< native/src/cpu/cpu_kernels.c -lm -o $@
 
-labs/lab3/src/read_input_exe: native/apps/lab3_read_input.c
+labs/lab3/src/read_input_exe: native/apps/lab3_read_input.c | $(LABS)
 	$(CC) $(CSER) $< -o $@
 
 bin/gpu_info: native/apps/gpu_info.cpp $(ALIB) $(HDRS) | $(B)
