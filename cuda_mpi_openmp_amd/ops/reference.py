@@ -44,13 +44,14 @@ def conv(img: torch.Tensor, filt: Filter) -> torch.Tensor:
     y = luma(img.cpu())
     up, down = filt.anchor, filt.k - 1 - filt.anchor
     yp = F.pad(y[None, None], (up, down, up, down), mode="replicate")
-    wx = torch.tensor(filt.wx, dtype=torch.float32).reshape(1, 1, filt.k, filt.k)
+    dwx, dwy = filt.dense()  # separable filters: their K x K outer products, one direct sum
+    wx = torch.tensor(dwx, dtype=torch.float32).reshape(1, 1, filt.k, filt.k)
     gx = F.conv2d(yp, wx)[0, 0]
-    if filt.mode == MODE_MAG2:
-        wy = torch.tensor(filt.wy, dtype=torch.float32).reshape(1, 1, filt.k, filt.k)
+    if filt.base_mode == MODE_MAG2:
+        wy = torch.tensor(dwy, dtype=torch.float32).reshape(1, 1, filt.k, filt.k)
         gy = F.conv2d(yp, wy)[0, 0]
         g = torch.sqrt(gx * gx + gy * gy)
-    elif filt.mode == MODE_ABS1:
+    elif filt.base_mode == MODE_ABS1:
         g = gx.abs()
     else:
         g = gx

@@ -33,6 +33,18 @@ enum mpx_conv_mode {
     MPX_CONV_LIN1 = 2  /* G = Gx   (blur / sharpen style single filter)           */
 };
 
+/*
+ * Separable filters: OR MPX_CONV_SEP into the mode. The tap arrays then hold
+ * the factors instead of k*k dense taps:
+ *   wx = { hx[0..k-1], vx[0..k-1], sx }   gx = sx * sum_dy vx[dy] * (sum_dx hx[dx] * Y[y+dy-a][x+dx-a])
+ *   wy = { hy[0..k-1], vy[0..k-1], sy }   (MAG2 only)
+ * Both sums are sequential fmaf chains from 0 in index order (horizontal pass
+ * first, clamp-to-edge in x and y), then one fp32 multiply by the scale.
+ */
+#define MPX_CONV_SEP 16
+#define MPX_CONV_BASE(m) ((m) & 3)
+#define MPX_SEP_NTAPS(k) (2 * (k) + 1)
+
 /* Which lab3 classifier implementation to run. */
 enum mpx_classify_path {
     MPX_CLS_DIRECT = 0, /* fp64 (p-mu)^T A (p-mu), reference-exact                   */

@@ -103,7 +103,8 @@ extern "C" int mpx_filter_lookup(const char *name, int *k, int *anchor, int *mod
     *k = f->k;
     *anchor = f->anchor;
     *mode = f->mode;
-    for (int i = 0; i < f->k * f->k; ++i) {
+    const int n = (f->mode & MPX_CONV_SEP) ? MPX_SEP_NTAPS(f->k) : f->k * f->k;
+    for (int i = 0; i < n; ++i) {
         wx[i] = f->wx[i];
         wy[i] = f->wy[i];
     }

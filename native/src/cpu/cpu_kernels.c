@@ -102,6 +102,52 @@ static void conv_rows(const float *lum, int lum_y0, const uint32_t *in, uint32_t
     }
 }
 
+/* Separable form (MPX_CONV_SEP, common.h): per input row the horizontal
+ * factor sums, then per output the vertical sum of those, then the scale.
+ * Every sum is a sequential fmaf chain from 0 in index order. */
+MPX_FMA_CLONES
+static void conv_rows_sep(const float *lum, int lum_y0, int nrows, const uint32_t *in, uint32_t *out,
+                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor,
+                          int mode, const float *wx, const float *wy) {
+    const int two = mode == MPX_CONV_MAG2;
+    /* horizontal pass: hs[0] (gx factor) and hs[1] (gy factor) of every row */
+    float *hs = (float *)malloc(sizeof(float) * (size_t)nrows * (size_t)w * (two ? 2 : 1));
+    if (!hs) return;
+    float *hsy = two ? hs + (size_t)nrows * (size_t)w : 0;
+    int r;
+#pragma omp parallel for schedule(static)
+    for (r = 0; r < nrows; ++r) {
+        const float *row = lum + (int64_t)r * w;
+        for (int x = 0; x < w; ++x) {
+            float ax = 0.0f, ay = 0.0f;
+            for (int dx = 0; dx < k; ++dx) {
+                const float l = row[mpx_clampi(x + dx - anchor, 0, w - 1)];
+                ax = fmaf(wx[dx], l, ax);
+                if (two) ay = fmaf(wy[dx], l, ay);
+            }
+            hs[(int64_t)r * w + x] = ax;
+            if (two) hsy[(int64_t)r * w + x] = ay;
+        }
+    }
+    int y;
+#pragma omp parallel for schedule(static)
+    for (y = oy0; y < oy1; ++y) {
+        for (int x = 0; x < w; ++x) {
+            float ax = 0.0f, ay = 0.0f;
+            for (int dy = 0; dy < k; ++dy) {
+                const int64_t rr = (int64_t)(mpx_clampi(y + dy - anchor, y_lo, y_hi) - lum_y0) * w + x;
+                ax = fmaf(wx[k + dy], hs[rr], ax);
+                if (two) ay = fmaf(wy[k + dy], hsy[rr], ay);
+            }
+            const float gx = ax * wx[2 * k];
+            const float gy = two ? ay * wy[2 * k] : 0.0f;
+            const float g = conv_finish(mode, gx, gy);
+            out[(int64_t)y * pitch + x] = mpx_px_gray(mpx_sat_u8(g), mpx_px_a(in[(int64_t)y * pitch + x]));
+        }
+    }
+    free(hs);
+}
+
 void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
                   int y_hi, int k, int anchor, int mode, const float *wx, const float *wy) {
     if (oy1 <= oy0 || w <= 0) return;
@@ -118,7 +164,10 @@ void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
         float *dst = lum + (int64_t)r * w;
         for (int x = 0; x < w; ++x) dst[x] = mpx_luma(src[x]);
     }
-    conv_rows(lum, r0, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy);
+    if (mode & MPX_CONV_SEP)
+        conv_rows_sep(lum, r0, nrows, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, MPX_CONV_BASE(mode), wx, wy);
+    else
+        conv_rows(lum, r0, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy);
     free(lum);
 }
 

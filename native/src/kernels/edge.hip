@@ -27,7 +27,7 @@ namespace {
 // per thread straight from global memory. Used for (K, anchor) pairs without a
 // tiled instantiation and as the naive baseline in profiles.
 // ---------------------------------------------------------------------------
-template <int MODE>
+template <int MODE, bool SEP>
 __global__ void conv_direct_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int w,
                                    int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor,
                                    Taps taps) {
@@ -37,13 +37,50 @@ __global__ void conv_direct_kernel(const uint32_t *__restrict__ in, uint32_t *__
     float ax = 0.0f, ay = 0.0f;
     for (int dy = 0; dy < k; ++dy) {
         const uint32_t *row = in + (int64_t)mpx_clampi(y + dy - anchor, y_lo, y_hi) * pitch;
+        float hx = 0.0f, hy = 0.0f;  // SEP: horizontal factor sums of this row
         for (int dx = 0; dx < k; ++dx) {
             const float l = mpx_luma(row[mpx_clampi(x + dx - anchor, 0, w - 1)]);
-            ax = fmaf(taps.wx[dy * k + dx], l, ax);
-            if (MODE == MPX_CONV_MAG2) ay = fmaf(taps.wy[dy * k + dx], l, ay);
+            if constexpr (SEP) {
+                hx = fmaf(taps.wx[dx], l, hx);
+                if (MODE == MPX_CONV_MAG2) hy = fmaf(taps.wy[dx], l, hy);
+            } else {
+                ax = fmaf(taps.wx[dy * k + dx], l, ax);
+                if (MODE == MPX_CONV_MAG2) ay = fmaf(taps.wy[dy * k + dx], l, ay);
+            }
+        }
+        if constexpr (SEP) {
+            ax = fmaf(taps.wx[k + dy], hx, ax);
+            if (MODE == MPX_CONV_MAG2) ay = fmaf(taps.wy[k + dy], hy, ay);
         }
     }
+    if constexpr (SEP) {
+        ax = ax * taps.wx[2 * k];
+        if (MODE == MPX_CONV_MAG2) ay = ay * taps.wy[2 * k];
+    }
     out[(int64_t)y * pitch + x] = edge::gray_px<MODE, false>(ax, ay, mpx_px_a(in[(int64_t)y * pitch + x]));
+}
+
+template <int MODE, bool SEP>
+void launch_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k,
+                   int anchor, const Taps &taps, hipStream_t s) {
+    const dim3 blk(64, 4);
+    const dim3 grd((w + 63) / 64, (oy1 - oy0 + 3) / 4);
+    hipLaunchKernelGGL((conv_direct_kernel<MODE, SEP>), grd, blk, 0, s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k,
+                       anchor, taps);
+}
+
+// separable filters: wave kernel for the centred odd windows, direct otherwise
+// (ABS1 separable filters always take the direct kernel: no named filter uses it)
+template <int MODE>
+int dispatch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                 int k, int anchor, const Taps &taps, bool vec, hipStream_t s) {
+    if constexpr (MODE != MPX_CONV_ABS1) {
+        if (k == 3 && anchor == 1) return edgel::launch_sep<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+        if (k == 5 && anchor == 2) return edgel::launch_sep<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+        if (k == 7 && anchor == 3) return edgel::launch_sep<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+    return MPX_OK;
 }
 
 template <int MODE>
@@ -53,11 +90,15 @@ int dispatch_mode(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
     if (k == 3 && anchor == 1) return launch_tiled<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
     if (k == 5 && anchor == 2) return launch_tiled<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
     if (k == 7 && anchor == 3) return launch_tiled<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-    const dim3 blk(64, 4);
-    const dim3 grd((w + 63) / 64, (oy1 - oy0 + 3) / 4);
-    hipLaunchKernelGGL(conv_direct_kernel<MODE>, grd, blk, 0, s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k,
-                       anchor, taps);
+    launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
     return MPX_OK;
+}
+
+template <int MODE>
+void launch_direct_any(bool sep, const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
+                       int y_hi, int k, int anchor, const Taps &taps, hipStream_t s) {
+    if (sep) launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+    else launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
 }
 
 }  // namespace
@@ -67,32 +108,36 @@ int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int 
     MPX_CHECK_ARG(in && out && wx, "null pointer");
     MPX_CHECK_ARG(w > 0 && pitch >= w, "bad width/pitch");
     MPX_CHECK_ARG(k >= 1 && k <= MPX_MAX_K && anchor >= 0 && anchor < k, "bad window");
+    const bool sep = (mode & MPX_CONV_SEP) != 0;
+    mode = MPX_CONV_BASE(mode) | (mode & ~(MPX_CONV_SEP | 3));  // any unknown flag fails the range check
     MPX_CHECK_ARG(mode >= MPX_CONV_MAG2 && mode <= MPX_CONV_LIN1, "bad mode");
     MPX_CHECK_ARG(mode != MPX_CONV_MAG2 || wy, "MAG2 needs wy");
     MPX_CHECK_ARG(y_lo <= y_hi && oy0 >= 0, "bad row range");
     if (oy1 <= oy0) return MPX_OK;
-    const Taps taps = make_taps(k, wx, wy, mode == MPX_CONV_MAG2);
+    const Taps taps = make_taps(k, wx, wy, mode == MPX_CONV_MAG2, sep);
     // 8-B pair loads/stores of the wave kernel: even width and pitch, 8-B aligned rows
     const bool vec = (w % 2 == 0) && (pitch % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
     hipStream_t s = as_stream(stream);
     int rc;
     if (force_direct) {
-        const dim3 blk(64, 4);
-        const dim3 grd((w + 63) / 64, (oy1 - oy0 + 3) / 4);
         switch (mode) {
             case MPX_CONV_MAG2:
-                hipLaunchKernelGGL(conv_direct_kernel<MPX_CONV_MAG2>, grd, blk, 0, s, in, out, w, pitch, oy0, oy1,
-                                   y_lo, y_hi, k, anchor, taps);
+                launch_direct_any<MPX_CONV_MAG2>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
                 break;
             case MPX_CONV_ABS1:
-                hipLaunchKernelGGL(conv_direct_kernel<MPX_CONV_ABS1>, grd, blk, 0, s, in, out, w, pitch, oy0, oy1,
-                                   y_lo, y_hi, k, anchor, taps);
+                launch_direct_any<MPX_CONV_ABS1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
                 break;
             default:
-                hipLaunchKernelGGL(conv_direct_kernel<MPX_CONV_LIN1>, grd, blk, 0, s, in, out, w, pitch, oy0, oy1,
-                                   y_lo, y_hi, k, anchor, taps);
+                launch_direct_any<MPX_CONV_LIN1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
         }
         rc = MPX_OK;
+    } else if (sep) {
+        if (mode == MPX_CONV_MAG2)
+            rc = dispatch_sep<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+        else if (mode == MPX_CONV_ABS1)
+            rc = dispatch_sep<MPX_CONV_ABS1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+        else
+            rc = dispatch_sep<MPX_CONV_LIN1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
     } else if (mode == MPX_CONV_MAG2) {
         rc = dispatch_mode<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
     } else if (mode == MPX_CONV_ABS1) {

@@ -338,16 +338,46 @@ struct WaveGeom {
 // ---- tap sources: runtime (kernel-argument SGPRs) or compile-time (named filters) ----
 struct RuntimeTaps {
     static constexpr bool kConst = false;
+    static constexpr bool kSep = false;
+};
+// Separable filter factors in the kernel-argument taps (common.h MPX_CONV_SEP layout).
+struct RuntimeSepTaps {
+    static constexpr bool kConst = false;
+    static constexpr bool kSep = true;
+};
+// Separable 5x5 Sobel (filters.h "sobel5"): gx = (v (x) d) / 48, gy = (d (x) v) / 48.
+struct Sobel5SepTaps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = true;
+    static constexpr float hx[5] = {-1, -2, 0, 2, 1};
+    static constexpr float vx[5] = {1, 4, 6, 4, 1};
+    static constexpr float sx = 1.0f / 48;
+    static constexpr float hy[5] = {1, 4, 6, 4, 1};
+    static constexpr float vy[5] = {-1, -2, 0, 2, 1};
+    static constexpr float sy = 1.0f / 48;
+};
+// Separable 5x5 binomial blur (filters.h "gauss5").
+struct Gauss5SepTaps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = true;
+    static constexpr float hx[5] = {1, 4, 6, 4, 1};
+    static constexpr float vx[5] = {1, 4, 6, 4, 1};
+    static constexpr float sx = 1.0f / 256;
+    static constexpr float hy[5] = {0, 0, 0, 0, 0};
+    static constexpr float vy[5] = {0, 0, 0, 0, 0};
+    static constexpr float sy = 0.0f;
 };
 // Reference Roberts operator (filters.h "roberts").
 struct RobertsTaps {
     static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
     static constexpr float wx[4] = {-1.0f, 0.0f, 0.0f, 1.0f};
     static constexpr float wy[4] = {0.0f, 1.0f, -1.0f, 0.0f};
 };
 // 5x5 Sobel / 48 (filters.h "sobel5"); bit-identical constants: (float)k / 48.0f
 struct Sobel5Taps {
     static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
     static constexpr float wx[25] = {-1.0f / 48, -2.0f / 48, 0, 2.0f / 48, 1.0f / 48,
                                      -4.0f / 48, -8.0f / 48, 0, 8.0f / 48, 4.0f / 48,
                                      -6.0f / 48, -12.0f / 48, 0, 12.0f / 48, 6.0f / 48,
@@ -371,7 +401,43 @@ __device__ __forceinline__ float tap_y(const Taps &t, int i) {
     else return t.wy[i];
 }
 
+// Separable factors: WHICH 0 = hx, 1 = vx, 2 = hy, 3 = vy (index i < K); the
+// scales through sep_scale<F, K, Y>.
+template <class F, int K, int WHICH>
+__device__ __forceinline__ float sep_tap(const Taps &t, int i) {
+    if constexpr (F::kConst) {
+        if constexpr (WHICH == 0) return F::hx[i];
+        else if constexpr (WHICH == 1) return F::vx[i];
+        else if constexpr (WHICH == 2) return F::hy[i];
+        else return F::vy[i];
+    } else {
+        if constexpr (WHICH == 0) return t.wx[i];
+        else if constexpr (WHICH == 1) return t.wx[K + i];
+        else if constexpr (WHICH == 2) return t.wy[i];
+        else return t.wy[K + i];
+    }
+}
+template <class F, int K, bool Y>
+__device__ __forceinline__ float sep_scale(const Taps &t) {
+    if constexpr (F::kConst) return Y ? F::sy : F::sx;
+    else return Y ? t.wy[2 * K] : t.wx[2 * K];
+}
+
 typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// Sequential fmaf chain from 0 over K packed operands (one of the separable
+// factor passes). Compile-time zero taps are skipped: they would add exactly
+// +-0, which changes at most the sign of a zero sum, never a gray level.
+template <class F, int K, int WHICH, class Get>
+__device__ __forceinline__ f2_t sep_chain(const Taps &t, Get &&operand) {
+    f2_t acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const float c = sep_tap<F, K, WHICH>(t, i);
+        if (!F::kConst || c != 0.0f) acc = __builtin_elementwise_fma(f2_t{c, c}, operand(i), acc);
+    }
+    return acc;
+}
 
 // Luminance of two pixels with packed fp32 (v_pk_mul_f32 / v_pk_add_f32): the
 // same three products and two sums per pixel as mpx_luma, rounded per element.
@@ -396,6 +462,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     constexpr int NE = (NV + 1) / 2;  // even-aligned pairs (w[2q], w[2q+1])
     constexpr int NO = NV / 2;        // odd pairs (w[2q+1], w[2q+2])
     constexpr bool TWO = (MODE == MPX_CONV_MAG2);
+    constexpr bool SEP = F::kSep;
     const int lane = threadIdx.x & 63;
     // readfirstlane: make the wave index (and everything derived from it: the
     // segment bounds and the row-loop exits) provably wave-uniform, so the loop
@@ -455,6 +522,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     uint2 pre[D];         // prefetch ring: raw pixels of input rows i .. i+D-1
     f2_t we[K][NE];       // window ring, even pairs (register-pair aligned for v_pk_fma_f32)
     f2_t wo[K][NO > 0 ? NO : 1];  // window ring, odd pairs
+    f2_t hxr[K], hyr[K];  // separable filters: ring of per-row horizontal factor sums
     uint32_t alp0[K], alp1[K];  // raw source pixels of the centre row (alpha = byte 3)
 
     // consume the input row in window slot u: luminance (packed), alpha, and the
@@ -473,10 +541,18 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         if constexpr (G::R >= 1) wv[A + 2] = from_next(l.x);
         if constexpr (G::R >= 2) wv[A + 3] = from_next(l.y);
         if constexpr (G::R >= 3) wv[A + 4] = from_next(wv[A + 2]);
+        if constexpr (SEP) {
+            // the horizontal passes run once per input row; the K-row ring then
+            // only holds their results (2 x K packed values, not the windows)
+            auto pair = [&](int dx) { return f2_t{wv[dx], wv[dx + 1]}; };
+            hxr[u] = sep_chain<F, K, 0>(taps, pair);
+            if constexpr (TWO) hyr[u] = sep_chain<F, K, 2>(taps, pair);
+        } else {
 #pragma unroll
-        for (int q = 0; q < NE; ++q) we[u][q] = f2_t{wv[2 * q], 2 * q + 1 < NV ? wv[2 * q + 1] : 0.0f};
+            for (int q = 0; q < NE; ++q) we[u][q] = f2_t{wv[2 * q], 2 * q + 1 < NV ? wv[2 * q + 1] : 0.0f};
 #pragma unroll
-        for (int q = 0; q < NO; ++q) wo[u][q] = f2_t{wv[2 * q + 1], wv[2 * q + 2]};
+            for (int q = 0; q < NO; ++q) wo[u][q] = f2_t{wv[2 * q + 1], wv[2 * q + 2]};
+        }
     };
 
 #pragma unroll
@@ -505,18 +581,29 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             const int y = ys + g * D + v;       // output row completed by row i
             // both output columns at once: packed FMAs over the (w[dx], w[dx+1]) pairs
             f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
+            if constexpr (SEP) {
+                gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[(u + 1 + dy) % K]; });
+                const float sx = sep_scale<F, K, false>(taps);
+                gx = gx * f2_t{sx, sx};
+                if constexpr (TWO) {
+                    gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[(u + 1 + dy) % K]; });
+                    const float sy = sep_scale<F, K, true>(taps);
+                    gy = gy * f2_t{sy, sy};
+                }
+            } else {
 #pragma unroll
-            for (int dy = 0; dy < K; ++dy) {
-                const int r = (u + 1 + dy) % K;
+                for (int dy = 0; dy < K; ++dy) {
+                    const int r = (u + 1 + dy) % K;
 #pragma unroll
-                for (int dx = 0; dx < K; ++dx) {
-                    const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
-                    const float cx = tap_x<F>(taps, dy * K + dx);
-                    if (!F::kConst || cx != 0.0f)  // compile-time for named filters: a zero tap adds exactly 0
-                        gx = __builtin_elementwise_fma(f2_t{cx, cx}, pv, gx);
-                    if constexpr (TWO) {
-                        const float cy = tap_y<F>(taps, dy * K + dx);
-                        if (!F::kConst || cy != 0.0f) gy = __builtin_elementwise_fma(f2_t{cy, cy}, pv, gy);
+                    for (int dx = 0; dx < K; ++dx) {
+                        const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
+                        const float cx = tap_x<F>(taps, dy * K + dx);
+                        if (!F::kConst || cx != 0.0f)  // compile-time for named filters: a zero tap adds exactly 0
+                            gx = __builtin_elementwise_fma(f2_t{cx, cx}, pv, gx);
+                        if constexpr (TWO) {
+                            const float cy = tap_y<F>(taps, dy * K + dx);
+                            if (!F::kConst || cy != 0.0f) gy = __builtin_elementwise_fma(f2_t{cy, cy}, pv, gy);
+                        }
                     }
                 }
             }

@@ -13,9 +13,11 @@ namespace mpx {
 namespace edgel {
 using edge::Taps;
 
-inline Taps make_taps(int k, const float *wx, const float *wy, bool two) {
+// sep: wx / wy hold the MPX_CONV_SEP factors (2k+1 values) instead of k*k taps
+inline Taps make_taps(int k, const float *wx, const float *wy, bool two, bool sep = false) {
     Taps t{};
-    for (int i = 0; i < k * k; ++i) {
+    const int n = sep ? MPX_SEP_NTAPS(k) : k * k;
+    for (int i = 0; i < n; ++i) {
         t.wx[i] = wx[i];
         t.wy[i] = two ? wy[i] : 0.0f;
     }
@@ -92,6 +94,32 @@ int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
             return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
     }
     return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+}
+
+template <class F, int K>
+inline bool same_sep_taps(const Taps &t, bool two) {
+    auto eq = [](float a, float b) { return __builtin_bit_cast(uint32_t, a) == __builtin_bit_cast(uint32_t, b); };
+    for (int i = 0; i < K; ++i) {
+        if (!eq(t.wx[i], F::hx[i]) || !eq(t.wx[K + i], F::vx[i])) return false;
+        if (two && (!eq(t.wy[i], F::hy[i]) || !eq(t.wy[K + i], F::vy[i]))) return false;
+    }
+    return eq(t.wx[2 * K], F::sx) && (!two || eq(t.wy[2 * K], F::sy));
+}
+
+// Separable filters (MPX_CONV_SEP): the wave kernel keeps a ring of per-row
+// horizontal sums instead of the K x K window.
+template <int K, int A, int MODE>
+int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+               const Taps &taps, bool vec, hipStream_t s) {
+    if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
+        if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
+            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
+        if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
+            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    }
+    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
 }
 
 

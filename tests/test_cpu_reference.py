@@ -43,9 +43,40 @@ def test_filter_table():
     assert {"roberts", "sobel3", "sobel5", "gauss5"} <= set(names)
     f = ops.get_filter("sobel5")
     assert (f.k, f.anchor, f.halo_up, f.halo_down) == (5, 2, 2, 2)
-    assert abs(sum(f.wx)) < 1e-6 and f.wx[4] == np.float32(1.0 / 48)
+    assert f.separable and len(f.wx) == len(f.wy) == 11 and f.wx[10] == np.float32(1.0 / 48)
+    # the factored sobel5 is the same operator as the 25-tap sobel5_dense
+    d = ops.get_filter("sobel5_dense")
+    assert not d.separable and abs(sum(d.wx)) < 1e-6 and d.wx[4] == np.float32(1.0 / 48)
+    for a, b in zip(f.dense(), (d.wx, d.wy)):
+        assert np.array_equal(np.float32(a), np.float32(b))
+    g, gd = ops.get_filter("gauss5"), ops.get_filter("gauss5_dense")
+    assert g.separable and np.array_equal(np.float32(g.dense()[0]), np.float32(gd.wx))
     with pytest.raises(Exception):
         ops.get_filter("no-such-filter")
+
+
+@pytest.mark.parametrize("pair", [("sobel5", "sobel5_dense"), ("gauss5", "gauss5_dense")])
+def test_separable_equals_dense_within_one_level(pair):
+    """Factored and direct evaluation differ only by fp32 rounding order."""
+    img = rand_img(257, 263, seed=12)
+    a = ops.conv(img, pair[0])[..., 0].int()
+    b = ops.conv(img, pair[1])[..., 0].int()
+    diff = (a - b).abs()
+    assert int(diff.max()) <= 1
+    assert float((diff > 0).float().mean()) < 0.01
+
+
+def test_separable_custom_cpu():
+    f = ops.Filter.separable_custom([1, 2, 1], [-1, 0, 1], 0.25, [-1, 0, 1], [1, 2, 1], 0.25)
+    assert f.separable and f.ntaps == 7
+    img = smooth_img(60, 70, seed=2)
+    a = ops.conv(img, f)
+    dwx, dwy = f.dense()
+    dense = ops.Filter.custom(3, dwx, dwy)
+    assert int((a[..., 0].int() - ops.conv(img, dense)[..., 0].int()).abs().max()) <= 1
+    assert int((a[..., 0].int() - ref.conv(img, f)[..., 0].int()).abs().max()) <= 1
+    blur = ops.Filter.separable_custom([1] * 7, [1] * 7, 1.0 / 49, mode="lin1")
+    assert int((ops.conv(img, blur)[..., 0].int() - ref.conv(img, blur)[..., 0].int()).abs().max()) <= 1
 
 
 def test_conv_rows_slabs_cpu():

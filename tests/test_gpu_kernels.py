@@ -42,7 +42,7 @@ def test_roberts_matches_cpu_and_torch(gpu, hw, geom):
 
 
 @pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "box3", "sharpen3", "sobel5",
-                                  "gauss5", "log5"])
+                                  "gauss5", "log5", "sobel5_dense", "gauss5_dense"])
 @pytest.mark.parametrize("hw", [(1, 1), (2, 7), (7, 2), (31, 129), (64, 128), (200, 300), (257, 260)])
 def test_conv_matches_cpu_exact_and_torch(gpu, filt, hw):
     f = ops.get_filter(filt)
@@ -74,7 +74,25 @@ def test_conv_custom_7x7_and_odd_anchor(gpu):
         assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f))
 
 
-@pytest.mark.parametrize("filt", ["roberts", "sobel5", "sobel3"])
+def test_conv_separable_custom(gpu):
+    """Runtime separable factors (wave kernel for k = 3/5/7, direct for k = 4 and
+    abs1): GPU == CPU bit for bit, within one level of the dense torch sum."""
+    rng = np.random.default_rng(7)
+    img = smooth_img(203, 330, seed=6)
+    fs = [ops.Filter.separable_custom(rng.standard_normal(k).tolist(), rng.standard_normal(k).tolist(), 0.5,
+                                      rng.standard_normal(k).tolist(), rng.standard_normal(k).tolist(), 0.25)
+          for k in (3, 5, 7, 4)]
+    fs.append(ops.Filter.separable_custom([1, 4, 6, 4, 1], [1, 4, 6, 4, 1], 1.0 / 256, mode="lin1"))  # == gauss5, runtime
+    fs.append(ops.Filter.separable_custom([1, 2, 1], [-1, 0, 1], 1.0, mode="abs1"))
+    for f in fs:
+        c = ops.conv(img, f)
+        assert torch.equal(ops.conv(img.to(gpu), f).cpu(), c), f
+        assert torch.equal(ops.conv(img.to(gpu), f, direct=True).cpu(), c), f
+        assert int((c[..., 0].int() - ref.conv(img, f)[..., 0].int()).abs().max()) <= 1
+    assert torch.equal(ops.conv(img.to(gpu), fs[4]).cpu(), ops.conv(img, "gauss5"))
+
+
+@pytest.mark.parametrize("filt", ["roberts", "sobel5", "sobel3", "gauss5"])
 def test_conv_rows_slab_equals_full_image(gpu, filt):
     """A slab with resident halo rows reproduces the full-image result."""
     f = ops.get_filter(filt)

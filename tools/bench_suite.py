@@ -78,7 +78,7 @@ def bench_lab2(dev, size=4096):
     img = torch.randint(0, 256, (size, size, 4), dtype=torch.uint8, device=dev)
     out = torch.empty_like(img)
     host = img.cpu()
-    for f in ("sobel5", "roberts", "sobel3", "gauss5"):
+    for f in ("sobel5", "sobel5_dense", "roberts", "sobel3", "gauss5", "gauss5_dense"):
         us = gpu_time_us(lambda: ops.conv(img, f, out))
         ok = torch.equal(out.cpu(), ops.conv(host, f))
         cpu = cpu_time_ms(lambda: ops.conv(host, f))

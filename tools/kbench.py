@@ -50,7 +50,7 @@ def main():
     print(json.dumps({"fast_sqrt_selftest_mismatches": int(bad.item())}), flush=True)
 
     variants = {}
-    for fname, k in (("sobel5", 5), ("roberts", 2)):
+    for fname, k in (("sobel5_dense", 5), ("roberts", 2)):
         f = ops.get_filter(fname)
         wx, wy = f.c_taps()
         ref = ops.conv(img, f)
@@ -65,6 +65,10 @@ def main():
         variants[f"{fname}/lds-stream/rpt4"] = (mk(0, 4, 0, 1), ref)
         variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ref)
         variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ref)
+    for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
+        f = ops.get_filter(fname)
+        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ops.conv(img, f))
+        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ops.conv(img, f))
     variants["copy/torch"] = ((lambda: out.copy_(img)), img)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
@@ -72,7 +76,7 @@ def main():
 
     # correctness first
     cpu_img = img.cpu()
-    for fname in ("sobel5", "roberts"):
+    for fname in ("sobel5_dense", "roberts"):
         cpu = ops.conv(cpu_img, fname)
         print(json.dumps({"production_vs_cpu": fname, "bit_exact": bool(torch.equal(ops.conv(img, fname).cpu(), cpu))}),
               flush=True)
