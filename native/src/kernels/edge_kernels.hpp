@@ -425,17 +425,33 @@ __device__ __forceinline__ float sep_scale(const Taps &t) {
 
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
+// One step of a tap chain acc = fma(c, x, acc) started at 0. With compile-time
+// taps, zero taps are skipped and the first nonzero tap is a plain product
+// (c = +-1 folds into the next instruction's operand): fma(c, x, 0) and c * x
+// differ only in the sign of a zero result, and skipping a zero tap changes at
+// most the sign of a zero sum — neither can change a gray level (squares,
+// fabs and the saturating cast all map -0 and +0 alike).
+template <bool CONST>
+__device__ __forceinline__ void tap_step(f2_t &acc, bool &started, float c, f2_t x) {
+    if constexpr (CONST) {
+        if (c == 0.0f) return;
+        if (!started) {
+            acc = f2_t{c, c} * x;
+            started = true;
+            return;
+        }
+    }
+    acc = __builtin_elementwise_fma(f2_t{c, c}, x, acc);
+}
+
 // Sequential fmaf chain from 0 over K packed operands (one of the separable
-// factor passes). Compile-time zero taps are skipped: they would add exactly
-// +-0, which changes at most the sign of a zero sum, never a gray level.
+// factor passes).
 template <class F, int K, int WHICH, class Get>
 __device__ __forceinline__ f2_t sep_chain(const Taps &t, Get &&operand) {
     f2_t acc = {0.0f, 0.0f};
+    bool started = false;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const float c = sep_tap<F, K, WHICH>(t, i);
-        if (!F::kConst || c != 0.0f) acc = __builtin_elementwise_fma(f2_t{c, c}, operand(i), acc);
-    }
+    for (int i = 0; i < K; ++i) tap_step<F::kConst>(acc, started, sep_tap<F, K, WHICH>(t, i), operand(i));
     return acc;
 }
 
@@ -591,19 +607,15 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
                     gy = gy * f2_t{sy, sy};
                 }
             } else {
+                bool sx = false, sy = false;
 #pragma unroll
                 for (int dy = 0; dy < K; ++dy) {
                     const int r = (u + 1 + dy) % K;
 #pragma unroll
                     for (int dx = 0; dx < K; ++dx) {
                         const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
-                        const float cx = tap_x<F>(taps, dy * K + dx);
-                        if (!F::kConst || cx != 0.0f)  // compile-time for named filters: a zero tap adds exactly 0
-                            gx = __builtin_elementwise_fma(f2_t{cx, cx}, pv, gx);
-                        if constexpr (TWO) {
-                            const float cy = tap_y<F>(taps, dy * K + dx);
-                            if (!F::kConst || cy != 0.0f) gy = __builtin_elementwise_fma(f2_t{cy, cy}, pv, gy);
-                        }
+                        tap_step<F::kConst>(gx, sx, tap_x<F>(taps, dy * K + dx), pv);
+                        if constexpr (TWO) tap_step<F::kConst>(gy, sy, tap_y<F>(taps, dy * K + dx), pv);
                     }
                 }
             }

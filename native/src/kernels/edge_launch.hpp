@@ -58,6 +58,15 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
                 const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1) {
     using G = edge::WaveGeom<K, A, OWX>;
     const int strips = (w + G::OW - 1) / G::OW;
+    if (seg <= 0) {
+        // one resident round of ~6 waves per SIMD: long segments (few warm-up
+        // rows), at least 8 rows each. MI355X sobel5 4096^2 sweep (kbench):
+        // 8 waves/SIMD (seg 17) 28.1 us, 6.8 (seg 20) 25.3-26.0, 5.7 (seg 24)
+        // 25.8, 17 in two rounds (seg 8) 28.1-30.3
+        const int64_t slots = (int64_t)kNumCUs * 4 * 6;
+        const int64_t work = (int64_t)(oy1 - oy0) * strips;
+        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
+    }
     const int segs = (oy1 - oy0 + seg - 1) / seg;
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
@@ -107,19 +116,22 @@ inline bool same_sep_taps(const Taps &t, bool two) {
 }
 
 // Separable filters (MPX_CONV_SEP): the wave kernel keeps a ring of per-row
-// horizontal sums instead of the K x K window.
+// horizontal sums instead of the K x K window. Their K-1 warm-up rows per
+// segment cost a whole horizontal pass each, so segments are longer: sized
+// for one resident round (launch_wave, seg <= 0).
+inline constexpr int kSepSegRows = 0;  // auto (launch_wave)
 template <int K, int A, int MODE>
 int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                const Taps &taps, bool vec, hipStream_t s) {
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
-            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
         if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
-            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
     }
-    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
 }
 
 

@@ -41,8 +41,19 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
     using namespace mpx;
     MPX_CHECK_ARG(in && out && wx && wy && w > 0 && h > 0, "bad arguments");
     MPX_CHECK_ARG(k == 2 || k == 5, "variant harness covers k = 2 and k = 5");
-    const Taps taps = make_taps(k, wx, wy, true);
     hipStream_t s = as_stream(stream);
+    if (kind == 3 || kind == 4) {
+        // separable sobel5 (wx / wy = MPX_CONV_SEP factors): kind 3 compiled-in
+        // factors, kind 4 runtime factors; p1 = segment rows, p2 >= 1000 strip-major
+        MPX_CHECK_ARG(k == 5 && p1 >= 0, "separable variants: k = 5, segment rows >= 0 (0 = auto)");
+        const Taps st = make_taps(k, wx, wy, true, true);
+        const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
+        const int sm = p2 >= 1000 ? 0 : 1;
+        if (kind == 3)
+            return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
+        return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::RuntimeSepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
+    }
+    const Taps taps = make_taps(k, wx, wy, true);
     if (kind == 1 || kind == 2) {
         // kind 1: runtime taps, kind 2: compiled-in taps of the named filter;
         // p1 = segment rows; p2 >= 1000 orders waves strip-major

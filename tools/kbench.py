@@ -65,6 +65,17 @@ def main():
         variants[f"{fname}/lds-stream/rpt4"] = (mk(0, 4, 0, 1), ref)
         variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ref)
         variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ref)
+    fs5 = ops.get_filter("sobel5")
+    swx, swy = fs5.c_taps()
+    sref = ops.conv(img, fs5)
+    for seg in (0, 8, 12, 16, 17, 18, 20, 24, 32):
+        for kind, nm in ((3, "const"), (4, "rt")):
+            variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
+                (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5,
+                                                                             kind, seg, 0, 1, swx, swy, 0))), sref)
+        variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
+            (lambda seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg, 1000, 1,
+                                                              swx, swy, 0))), sref)
     for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
         f = ops.get_filter(fname)
         variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ops.conv(img, f))
