@@ -25,7 +25,7 @@ ALIB      := $(B)/libmpx.a
 
 HIP_SRCS  := $(wildcard native/src/kernels/*.hip)
 HIP_OBJS  := $(patsubst native/src/kernels/%.hip,$(B)/k_%.o,$(HIP_SRCS))
-CORE_OBJS := $(B)/capi.o $(B)/comm.o
+CORE_OBJS := $(B)/capi.o $(B)/comm.o $(B)/ipc.o
 CPU_OBJ   := $(B)/cpu_kernels.o
 LIB_OBJS  := $(HIP_OBJS) $(CORE_OBJS) $(CPU_OBJ)
 HDRS      := $(wildcard native/include/mpx/*.h native/include/mpx/*.hpp native/src/kernels/*.hpp native/src/cpu/*.h)
@@ -56,6 +56,9 @@ $(B)/k_edge.o $(B)/k_edge_roberts.o $(B)/k_edge_variants.o: HIPFLAGS += -fno-slp
 $(B)/k_classify.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
 $(B)/capi.o: native/src/core/capi.cpp $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(B)/ipc.o: native/src/core/ipc.cpp $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 # RCCL is not linked: comm.cpp binds the librccl torch already loaded (dlsym)

@@ -8,10 +8,13 @@ windows shifted across lanes with DPP, no LDS, no barriers), synthetic random
 RGBA8 data.
 
 Scaling is WEAK: every rank owns one 4096x4096 row slab of a global
-(4096*N) x 4096 image. One step = refresh the slab's halo rows from the
-neighbouring ranks over RCCL (xGMI point-to-point; the libmpx native RCCL
-tier, in order on the compute stream — measured faster than overlapping such
-small transfers) + convolve every owned row. ``value`` is the
+(4096*N) x 4096 image. One step = read the slab's 2+2 halo rows from the
+neighbouring ranks over xGMI + convolve every owned row. Halo transport
+(``--halo``): ``peer`` maps the neighbours' slabs once (IPC) and the conv
+kernel loads their boundary rows over xGMI on every step — one launch per
+step; ``rccl`` runs a grouped RCCL send/recv first (libmpx native tier, in
+order on the compute stream); ``auto`` = peer when every rank can map and
+verify its neighbours, else rccl. ``value`` is the
 whole-job pixel throughput (N * 4096^2 * K / time); the GPU/CPU speedup
 compares one GPU's per-image time with the OpenMP CPU reference on the same
 4096^2 image (``speedup_vs_cpu``).
@@ -60,7 +63,7 @@ def verify_band(det: SlabEdgeDetector, rows: int = 64) -> bool:
     halo-dependent boundary rows) against the CPU reference run on the same
     halo-filled buffer."""
     s = det.slab
-    buf = det.buf.to("cpu")
+    buf = det.halo_filled().to("cpu")
     out_cpu = torch.empty((s.rows, det.w, 4), dtype=torch.uint8)
     ok = True
     for a, b in ((0, min(rows, s.rows)), (max(0, s.rows - rows), s.rows)):
@@ -81,6 +84,9 @@ def main() -> int:
                    help="halo transfer overlapped with the interior rows (on), in order before one full launch "
                         "(off), exchanged one step ahead on the comm stream with double-buffered input (pipeline; "
                         "native RCCL tier), or the measured-faster choice for the transport in use (auto)")
+    p.add_argument("--halo", choices=["auto", "peer", "rccl"], default="auto",
+                   help="halo transport for N > 1: one-sided xGMI loads from IPC-mapped neighbour slabs (peer), "
+                        "RCCL send/recv (rccl), or peer when available (auto)")
     p.add_argument("--watchdog", type=float, default=None,
                    help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -93,7 +99,8 @@ def main() -> int:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
     n = ctx.world
     det = SlabEdgeDetector(ctx, args.size * n, args.size, args.filter,
-                           overlap={"auto": "auto", "on": True, "off": False, "pipeline": "pipeline"}[args.overlap])
+                           overlap={"auto": "auto", "on": True, "off": False, "pipeline": "pipeline"}[args.overlap],
+                           halo=args.halo)
     det.fill_random(seed=1234 + ctx.rank)
     sync(ctx)
     ctx.barrier()
@@ -149,12 +156,14 @@ def main() -> int:
             "data": "synthetic (uniform random RGBA8, one 4096x4096 slab per GPU)",
             "config": {
                 "model": f"lab2 2D convolution {args.size}x{args.size} image, "
-                         f"{det.filter.k}x{det.filter.k} filter ({det.filter.name}, wave-streaming HIP kernel)",
+                         f"{det.filter.k}x{det.filter.k} filter ({det.filter.name}"
+                         f"{', separable 1x5+5x1 passes' if det.filter.separable else ''}, wave-streaming HIP kernel)",
                 "global_batch": n,
                 "seq_len": args.size,
-                "parallelism": f"slab{n}" + (("+halo-pipelined" if det.pipeline else "+halo-overlap" if det.overlap
-                                              else "+halo-inorder") if n > 1 else ""),
-                "transport": ("native-rccl" if ctx.native is not None else "torch.distributed") if n > 1 else None,
+                "parallelism": f"slab{n}" + (("+halo-peer-fused" if det.peer is not None else "+halo-pipelined"
+                                              if det.pipeline else "+halo-overlap" if det.overlap else "+halo-inorder")
+                                             if n > 1 else ""),
+                "transport": det.transport if n > 1 else None,
                 "image_hw": [args.size * n, args.size],
                 "halo_rows": [det.filter.halo_up, det.filter.halo_down],
             },
@@ -167,6 +176,7 @@ def main() -> int:
             rec["gpu_ms_per_image"] = round(ms_per_step, 5)
             rec["speedup_vs_cpu"] = round(cpu_ms / ms_per_step, 1)
         print(json.dumps(rec), flush=True)
+    det.close()
     parallel.shutdown()
     return 0 if ok else 1
 

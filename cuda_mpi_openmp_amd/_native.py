@@ -48,8 +48,18 @@ _SIGNATURES = {
         c_int,
         [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
     ),
+    "mpx_conv_peer": (
+        c_int,
+        [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
+    ),
+    "mpx_ipc_handle_size": (c_int, []),
+    "mpx_ipc_get_handle": (c_int, [c_vp, c_vp, ctypes.POINTER(c_i64)]),
+    "mpx_ipc_open": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "mpx_ipc_close": (c_int, [c_vp]),
+    "mpx_memcpy_d2d": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
     "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_int, c_vp]),
+    "mpx_strip_copy_probe": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "mpx_filter_lookup": (c_int, [c_char_p, _ip, _ip, _ip, _fp, _fp]),
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),

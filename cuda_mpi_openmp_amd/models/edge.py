@@ -56,10 +56,20 @@ class SlabEdgeDetector:
       stream only ever waits on an exchange that finished a step earlier.
     * ``"auto"``: ``False`` with the native tier, ``True`` without (measured,
       profiles/comm_step.md).
+
+    ``halo`` selects the transport of the halo rows:
+
+    * ``"peer"``: one-sided — the neighbours' slabs are IPC-mapped once and the
+      convolution kernel reads their boundary rows over xGMI on every step
+      (``parallel.peer``); no exchange kernel, one launch per step;
+    * ``"rccl"``: two-sided send/recv (native RCCL tier, else torch.distributed),
+      arranged by ``overlap``;
+    * ``"auto"``: ``"peer"`` when every rank can map and verify its neighbours,
+      else ``"rccl"``.
     """
 
     def __init__(self, ctx: DistContext, global_h: int, w: int, filt: str | Filter = "sobel5",
-                 overlap: bool | str = "auto"):
+                 overlap: bool | str = "auto", halo: str = "auto"):
         self.ctx = ctx
         self.filter = get_filter(filt) if isinstance(filt, str) else filt
         self.w = w
@@ -80,12 +90,25 @@ class SlabEdgeDetector:
         self.out = torch.empty((self.slab.rows, w, 4), dtype=torch.uint8, device=dev)
         # pre-validated launches for the three row ranges of a step
         s = self.slab
-        mk = lambda b, lo, hi: ops.ConvLauncher(b, self.out, self.filter, src_row0=s.own_offset,  # noqa: E731
-                                               out_row0=0, oy0=lo, oy1=hi, y_lo=s.y_lo, y_hi=s.y_hi)
+        mk = lambda b, lo, hi, peer=None: ops.ConvLauncher(b, self.out, self.filter,  # noqa: E731
+                                                           src_row0=s.own_offset, out_row0=0, oy0=lo, oy1=hi,
+                                                           y_lo=s.y_lo, y_hi=s.y_hi, peer=peer)
         self._all_b = [mk(b, 0, s.rows) for b in self.bufs]
         self._all = self._all_b[0]
         self._interior = mk(self.bufs[0], *s.interior())
         self._boundary = [mk(self.bufs[0], a, b) for a, b in s.boundary()]
+        self.peer = None
+        if halo not in ("auto", "peer", "rccl"):
+            raise ValueError(f"unknown halo transport {halo!r}")
+        if halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
+            from ..parallel.peer import try_peer_halo
+
+            self.peer = try_peer_halo(ctx, s, self.bufs[0][s.own_offset: s.own_offset + s.rows])
+            if self.peer is None and halo == "peer":
+                raise RuntimeError("peer halo transport unavailable (IPC mapping or verification failed)")
+        if self.peer is not None:
+            self.pipeline = self.overlap = False
+            self._all = mk(self.bufs[0], 0, s.rows, self.peer)
         self._traced = trace.enabled()  # roctx ranges only when MPX_ROCTX=1
         self._k = 0          # steps issued (pipeline mode)
         self._primed = False
@@ -108,11 +131,31 @@ class SlabEdgeDetector:
             self.ctx.native.comm_stream().synchronize()
             self._primed = False
 
+    @property
+    def transport(self) -> str:
+        if not self.ctx.is_distributed:
+            return "none"
+        if self.peer is not None:
+            return "xgmi-peer"
+        return "native-rccl" if self.ctx.native is not None else "torch.distributed"
+
+    def halo_filled(self) -> torch.Tensor:
+        """The input buffer with its halo rows as the last step read them
+        (peer mode copies them in from the neighbours' slabs first)."""
+        if self.peer is not None:
+            self.peer.pull(self.bufs[0])
+        return self.buf
+
+    def _publish(self) -> None:
+        if self.peer is not None:
+            self.peer.publish()
+
     def load(self, slab_rows: torch.Tensor) -> None:
         self._drain_comm()
         s = self.slab
         for b in self.bufs:
             b[s.own_offset: s.own_offset + s.rows].copy_(slab_rows)
+        self._publish()
 
     def fill_random(self, seed: int) -> None:
         self._drain_comm()
@@ -122,6 +165,7 @@ class SlabEdgeDetector:
         rows = torch.randint(0, 256, (s.rows, self.w, 4), dtype=torch.uint8, device=self.bufs[0].device, generator=g)
         for b in self.bufs:
             b[s.own_offset: s.own_offset + s.rows].copy_(rows)
+        self._publish()
 
     def _rows(self, a: int, b: int) -> None:
         s = self.slab
@@ -139,8 +183,8 @@ class SlabEdgeDetector:
         if self.pipeline:
             return self._step_pipelined()
         st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
-        if not self.ctx.is_distributed:
-            self._all(st)
+        if not self.ctx.is_distributed or self.peer is not None:
+            self._all(st)  # peer mode: the kernel reads the neighbours' rows itself
             return self.out
         if self.overlap:
             self.halo.start(self.buf)       # RCCL waits only for work queued so far
@@ -177,6 +221,13 @@ class SlabEdgeDetector:
         self._ev_conv[cur].record(compute)
         self._k += 1
         return self.out
+
+    def close(self) -> None:
+        """Unmap the neighbours' slabs (peer mode)."""
+        if self.peer is not None:
+            torch.cuda.synchronize(self.out.device)
+            self.peer.close()
+            self.peer = None
 
     def finish(self) -> None:
         """Join the comm stream into the current stream (end of a timed run)."""

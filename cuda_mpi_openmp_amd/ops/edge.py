@@ -93,13 +93,22 @@ class ConvLauncher:
     """
 
     def __init__(self, src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
-                 oy0: int, oy1: int, y_lo: int, y_hi: int):
+                 oy0: int, oy1: int, y_lo: int, y_hi: int, peer=None):
+        """``peer``: a ``parallel.PeerHalo`` — rows outside [0, own rows) are then
+        read from the neighbours' IPC-mapped slabs (``mpx_conv_peer``) instead
+        of ``src``'s resident halo rows."""
         self.args = _conv_args(src, out, filt, src_row0, out_row0, oy0, oy1, y_lo, y_hi)
         self.empty = oy1 <= oy0
         self.cuda = src.is_cuda
         L = _native.lib()
         self.fn = L.mpx_conv if self.cuda else L.mpx_cpu_conv
-        self._keep = (src, out)
+        if peer is not None:
+            if not self.cuda:
+                raise ValueError("peer halos need CUDA tensors")
+            a = self.args
+            self.args = (a[0], peer.up_ptr, peer.dn_ptr, peer.slab.rows) + a[1:]
+            self.fn = L.mpx_conv_peer
+        self._keep = (src, out, peer)
 
     def __call__(self, stream: Optional[int] = None) -> None:
         if self.empty:

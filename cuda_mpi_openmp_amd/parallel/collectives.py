@@ -46,7 +46,7 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
     """Max of a host scalar over ranks (e.g. each rank's step time)."""
     if not ctx.is_distributed:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -76,12 +76,14 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
     else:
         dev = torch.device("cpu")
     if backend is None:
-        backend = "nccl" if use_cuda else "gloo"
+        # MPX_DIST_BACKEND=gloo: control plane over gloo, e.g. to rehearse several
+        # ranks on one GPU (RCCL refuses two ranks per device)
+        backend = os.environ.get("MPX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     ctx = DistContext(rank=rank, world=world, local_rank=local_rank, device=dev, backend=backend)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda:
+        if use_cuda and backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
     if world > 1 and use_cuda and backend == "nccl":

@@ -70,6 +70,14 @@ int mpx_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int o
              int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
              void *stream);
 
+/* mpx_conv with peer-sourced halo rows (one-sided xGMI loads): input rows with
+ * logical index < 0 are read at in_up + row*pitch, rows >= own_rows at
+ * in_dn + row*pitch (pointers into IPC-mapped neighbour slabs, biased so the
+ * logical row index applies unchanged), rows [0, own_rows) from `in`. */
+int mpx_conv_peer(const uint32_t *in, const uint32_t *in_up, const uint32_t *in_dn, int own_rows,
+                  uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor,
+                  int mode, const float *wx, const float *wy, void *stream);
+
 /* Generic direct (untiled, one pixel per thread) variant of mpx_conv: any
  * anchor, naive global loads; the baseline the tiled kernel is measured against. */
 int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
@@ -140,6 +148,16 @@ int mpx_comm_check(void *comm);
 int mpx_comm_abort(void *comm);
 /* the communicator's comm stream (for caller-managed cross-step pipelining) */
 void *mpx_comm_stream(void *comm);
+
+/* ---------------- device memory shared between the processes of a node ---------------- */
+int mpx_ipc_handle_size(void);
+/* handle: mpx_ipc_handle_size() bytes; *offset = ptr - base of ptr's allocation */
+int mpx_ipc_get_handle(const void *ptr, void *handle, int64_t *offset);
+/* maps a peer's allocation on the current device (peer access enabled lazily) */
+int mpx_ipc_open(const void *handle, void **base);
+int mpx_ipc_close(void *base);
+/* stream-ordered device-to-device copy (either side may be IPC-mapped) */
+int mpx_memcpy_d2d(void *dst, const void *src, int64_t bytes, void *stream);
 
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*

@@ -30,13 +30,14 @@ namespace {
 template <int MODE, bool SEP>
 __global__ void conv_direct_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int w,
                                    int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor,
-                                   Taps taps) {
+                                   Taps taps, edge::RowSrc rs) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = oy0 + blockIdx.y * blockDim.y + threadIdx.y;
     if (x >= w || y >= oy1) return;
     float ax = 0.0f, ay = 0.0f;
     for (int dy = 0; dy < k; ++dy) {
-        const uint32_t *row = in + (int64_t)mpx_clampi(y + dy - anchor, y_lo, y_hi) * pitch;
+        const int gy = mpx_clampi(y + dy - anchor, y_lo, y_hi);
+        const uint32_t *row = (gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in)) + (int64_t)gy * pitch;
         float hx = 0.0f, hy = 0.0f;  // SEP: horizontal factor sums of this row
         for (int dx = 0; dx < k; ++dx) {
             const float l = mpx_luma(row[mpx_clampi(x + dx - anchor, 0, w - 1)]);
@@ -62,50 +63,54 @@ __global__ void conv_direct_kernel(const uint32_t *__restrict__ in, uint32_t *__
 
 template <int MODE, bool SEP>
 void launch_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k,
-                   int anchor, const Taps &taps, hipStream_t s) {
+                   int anchor, const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
     const dim3 blk(64, 4);
     const dim3 grd((w + 63) / 64, (oy1 - oy0 + 3) / 4);
     hipLaunchKernelGGL((conv_direct_kernel<MODE, SEP>), grd, blk, 0, s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k,
-                       anchor, taps);
+                       anchor, taps, rs);
 }
 
 // separable filters: wave kernel for the centred odd windows, direct otherwise
 // (ABS1 separable filters always take the direct kernel: no named filter uses it)
 template <int MODE>
 int dispatch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                 int k, int anchor, const Taps &taps, bool vec, hipStream_t s) {
+                 int k, int anchor, const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs) {
     if constexpr (MODE != MPX_CONV_ABS1) {
-        if (k == 3 && anchor == 1) return edgel::launch_sep<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-        if (k == 5 && anchor == 2) return edgel::launch_sep<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-        if (k == 7 && anchor == 3) return edgel::launch_sep<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+        if (k == 3 && anchor == 1) return edgel::launch_sep<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+        if (k == 5 && anchor == 2) return edgel::launch_sep<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+        if (k == 7 && anchor == 3) return edgel::launch_sep<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
     }
-    launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+    launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
     return MPX_OK;
 }
 
 template <int MODE>
 int dispatch_mode(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                  int k, int anchor, const Taps &taps, bool vec, hipStream_t s) {
-    if (k == 2 && anchor == 0) return launch_tiled<2, 0, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-    if (k == 3 && anchor == 1) return launch_tiled<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-    if (k == 5 && anchor == 2) return launch_tiled<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-    if (k == 7 && anchor == 3) return launch_tiled<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
-    launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+                  int k, int anchor, const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs) {
+    if (k == 2 && anchor == 0) return launch_tiled<2, 0, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+    if (k == 3 && anchor == 1) return launch_tiled<3, 1, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+    if (k == 5 && anchor == 2) return launch_tiled<5, 2, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+    if (k == 7 && anchor == 3) return launch_tiled<7, 3, MODE>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+    launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
     return MPX_OK;
 }
 
 template <int MODE>
 void launch_direct_any(bool sep, const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
-                       int y_hi, int k, int anchor, const Taps &taps, hipStream_t s) {
-    if (sep) launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
-    else launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+                       int y_hi, int k, int anchor, const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
+    if (sep) launch_direct<MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
+    else launch_direct<MODE, false>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
 }
 
 }  // namespace
 
 int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k,
-              int anchor, int mode, const float *wx, const float *wy, void *stream, bool force_direct) {
+              int anchor, int mode, const float *wx, const float *wy, void *stream, bool force_direct,
+              edge::RowSrc rs = edge::RowSrc{}) {
     MPX_CHECK_ARG(in && out && wx, "null pointer");
+    if (!rs.up) rs.up = in;
+    if (!rs.dn) rs.dn = in;
+    MPX_CHECK_ARG(rs.own_rows >= 1, "own_rows must be positive");
     MPX_CHECK_ARG(w > 0 && pitch >= w, "bad width/pitch");
     MPX_CHECK_ARG(k >= 1 && k <= MPX_MAX_K && anchor >= 0 && anchor < k, "bad window");
     const bool sep = (mode & MPX_CONV_SEP) != 0;
@@ -116,34 +121,36 @@ int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int 
     if (oy1 <= oy0) return MPX_OK;
     const Taps taps = make_taps(k, wx, wy, mode == MPX_CONV_MAG2, sep);
     // 8-B pair loads/stores of the wave kernel: even width and pitch, 8-B aligned rows
-    const bool vec = (w % 2 == 0) && (pitch % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
+    const bool vec = (w % 2 == 0) && (pitch % 2 == 0) &&
+                     ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out) |
+                       reinterpret_cast<uintptr_t>(rs.up) | reinterpret_cast<uintptr_t>(rs.dn)) & 7u) == 0;
     hipStream_t s = as_stream(stream);
     int rc;
     if (force_direct) {
         switch (mode) {
             case MPX_CONV_MAG2:
-                launch_direct_any<MPX_CONV_MAG2>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+                launch_direct_any<MPX_CONV_MAG2>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
                 break;
             case MPX_CONV_ABS1:
-                launch_direct_any<MPX_CONV_ABS1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+                launch_direct_any<MPX_CONV_ABS1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
                 break;
             default:
-                launch_direct_any<MPX_CONV_LIN1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s);
+                launch_direct_any<MPX_CONV_LIN1>(sep, in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, s, rs);
         }
         rc = MPX_OK;
     } else if (sep) {
         if (mode == MPX_CONV_MAG2)
-            rc = dispatch_sep<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+            rc = dispatch_sep<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
         else if (mode == MPX_CONV_ABS1)
-            rc = dispatch_sep<MPX_CONV_ABS1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+            rc = dispatch_sep<MPX_CONV_ABS1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
         else
-            rc = dispatch_sep<MPX_CONV_LIN1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+            rc = dispatch_sep<MPX_CONV_LIN1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
     } else if (mode == MPX_CONV_MAG2) {
-        rc = dispatch_mode<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+        rc = dispatch_mode<MPX_CONV_MAG2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
     } else if (mode == MPX_CONV_ABS1) {
-        rc = dispatch_mode<MPX_CONV_ABS1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+        rc = dispatch_mode<MPX_CONV_ABS1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
     } else {
-        rc = dispatch_mode<MPX_CONV_LIN1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s);
+        rc = dispatch_mode<MPX_CONV_LIN1>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, taps, vec, s, rs);
     }
     if (rc != MPX_OK) return rc;
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
@@ -157,6 +164,16 @@ MPX_MODULE_ANCHOR(edge)
 extern "C" int mpx_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                         int k, int anchor, int mode, const float *wx, const float *wy, void *stream) {
     return mpx::conv_impl(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy, stream, false);
+}
+
+extern "C" int mpx_conv_peer(const uint32_t *in, const uint32_t *in_up, const uint32_t *in_dn, int own_rows,
+                             uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi, int k, int anchor,
+                             int mode, const float *wx, const float *wy, void *stream) {
+    mpx::edge::RowSrc rs;
+    rs.up = in_up;
+    rs.dn = in_dn;
+    rs.own_rows = own_rows;
+    return mpx::conv_impl(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy, stream, false, rs);
 }
 
 extern "C" int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,

@@ -12,6 +12,16 @@ struct Taps {
     float wy[MPX_MAX_K * MPX_MAX_K];
 };
 
+// Where input rows live (wave kernel). Logical rows [0, own_rows) come from
+// `in`; rows < 0 from `up` and rows >= own_rows from `dn`, both biased so the
+// logical row index applies unchanged (mpx_conv_peer: IPC-mapped neighbour
+// slabs read over xGMI). nullptr = `in` for every row.
+struct RowSrc {
+    const uint32_t *up = nullptr;
+    const uint32_t *dn = nullptr;
+    int own_rows = 0x7fffffff;
+};
+
 // Exact magnitude -> gray level: trunc(min(sqrt_rn(s), 255)) with s = gx*gx + gy*gy.
 //   FAST: hardware v_sqrt_f32 (not correctly rounded) decides the integer part
 //   whenever its result is further than kSqrtMargin from an integer; otherwise
@@ -467,11 +477,11 @@ __device__ __forceinline__ f2_t luma2(uint32_t p0, uint32_t p1) {
     return (t0 + t1) + t2;
 }
 
-template <int K, int A, int MODE, bool VEC, bool FAST, class F = RuntimeTaps, int OWX = 0>
+template <int K, int A, int MODE, bool VEC, bool FAST, class F = RuntimeTaps, int OWX = 0, int PF = 4>
 __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                         int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                         int seg, int segs_per_strip, int nwaves, int strips,
-                                                        int strip_minor, Taps taps) {
+                                                        int strip_minor, Taps taps, RowSrc rs) {
     using G = WaveGeom<K, A, OWX>;
     static_assert(G::P + G::OW + G::R2 <= 128, "strip plus halo exceeds one wave's 128 columns");
     constexpr int NV = G::NV;
@@ -511,7 +521,9 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // pressure), which turns the ring back into load-then-wait.
     auto load_row = [&](int i) -> uint2 {
         const int gy = mpx_clampi(iy0 + i, y_lo, y_hi);
-        const uint32_t *row = in + (int64_t)gy * pitch;
+        // wave-uniform row source select (scalar): own slab or a neighbour's
+        const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
+        const uint32_t *row = src + (int64_t)gy * pitch;
         uint2 r;
         if constexpr (VEC) {  // w even: the pair is entirely inside, left or right
             r = *reinterpret_cast<const uint2 *>(row + cc);
@@ -532,9 +544,9 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         }
     };
 
-    // Prefetch ring of D >= 4 rows (a multiple of K so both rings keep
+    // Prefetch ring of D >= PF rows (a multiple of K so both rings keep
     // compile-time slots when the row loop is unrolled D times).
-    constexpr int D = K * ((4 + K - 1) / K);
+    constexpr int D = K * ((PF + K - 1) / K);
     uint2 pre[D];         // prefetch ring: raw pixels of input rows i .. i+D-1
     f2_t we[K][NE];       // window ring, even pairs (register-pair aligned for v_pk_fma_f32)
     f2_t wo[K][NO > 0 ? NO : 1];  // window ring, odd pairs

@@ -53,9 +53,12 @@ int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
 // rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
 inline constexpr int kSegRows = 8;
 
-template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0>
+template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4>
 int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1) {
+                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1,
+                edge::RowSrc rs = edge::RowSrc{}) {
+    if (!rs.up) rs.up = in;
+    if (!rs.dn) rs.dn = in;
     using G = edge::WaveGeom<K, A, OWX>;
     const int strips = (w + G::OW - 1) / G::OW;
     if (seg <= 0) {
@@ -72,11 +75,11 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
     const unsigned nblk = (unsigned)((nwaves + 3) / 4);
     if (vec)
-        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
-                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX, PF>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps, rs);
     else
-        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX>), dim3(nblk), dim3(256), 0, s, in,
-                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps);
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX, PF>), dim3(nblk), dim3(256), 0, s, in,
+                           out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps, rs);
     return MPX_OK;
 }
 
@@ -93,16 +96,16 @@ inline bool same_taps(const Taps &t) {
 
 template <int K, int A, int MODE>
 int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                 const Taps &taps, bool vec, hipStream_t s) {
+                 const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs = edge::RowSrc{}) {
     if constexpr (K == 2 && A == 0 && MODE == MPX_CONV_MAG2) {
         if (same_taps<edge::RobertsTaps, 4>(taps))
-            return launch_wave<K, A, MODE, true, edge::RobertsTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+            return launch_wave<K, A, MODE, true, edge::RobertsTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (same_taps<edge::Sobel5Taps, 25>(taps))
-            return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+            return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
     }
-    return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s);
+    return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
 }
 
 template <class F, int K>
@@ -122,16 +125,16 @@ inline bool same_sep_taps(const Taps &t, bool two) {
 inline constexpr int kSepSegRows = 0;  // auto (launch_wave)
 template <int K, int A, int MODE>
 int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-               const Taps &taps, bool vec, hipStream_t s) {
+               const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs = edge::RowSrc{}) {
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
-            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
+            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
         if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
-            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
+            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
     }
-    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows);
+    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
 }
 
 

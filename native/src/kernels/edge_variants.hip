@@ -27,8 +27,58 @@ __global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigne
     if (nbad) atomicAdd(bad, nbad);
 }
 
+// Memory-pattern probe: the wave-strip streaming order of conv_wave_kernel with
+// no arithmetic (copy in -> out). V = 32-bit pixels per lane (2: 8-B loads,
+// 4: 16-B loads), ring of D rows in flight per wave.
+template <int V, int D>
+__global__ __launch_bounds__(256) void strip_copy_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                         int w, int h, int seg, int nwaves, int strips) {
+    typedef uint32_t vt __attribute__((ext_vector_type(V)));
+    const int lane = threadIdx.x & 63;
+    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (gw >= nwaves) return;
+    const int strip = gw % strips, sg = gw / strips;
+    const int ys = sg * seg, ye = min(ys + seg, h);
+    const int col = strip * 64 * V + V * lane;
+    const int cc = min(col, w - V);
+    vt ring[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) ring[q] = *reinterpret_cast<const vt *>(in + (int64_t)min(ys + q, h - 1) * w + cc);
+    const int ngroups = (ye - ys + D - 1) / D;
+    for (int g = 0; g < ngroups; ++g) {
+#pragma unroll
+        for (int v = 0; v < D; ++v) {
+            const int y = ys + g * D + v;
+            const vt px = ring[v];
+            ring[v] = *reinterpret_cast<const vt *>(in + (int64_t)min(y + D, h - 1) * w + cc);
+            __builtin_amdgcn_sched_barrier(0);
+            const bool ok = y < ye && col < w;
+            const __amdgpu_buffer_rsrc_t orow =
+                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)(ok ? y : ys) * w, 0, w * 4, 0x00020000);
+            if constexpr (V == 2) __builtin_amdgcn_raw_buffer_store_b64(px, orow, ok ? col * 4 : 0x7ffffff0, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(px, orow, ok ? col * 4 : 0x7ffffff0, 0, 0);
+        }
+    }
+}
+
 }  // namespace
 MPX_MODULE_ANCHOR(edge_variants)
+
+extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, int h, int v, int d, int seg,
+                                    void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(in && out && w > 0 && h > 0 && seg > 0 && w % 4 == 0, "bad arguments");
+    const int strips = (w + 64 * v - 1) / (64 * v);
+    const int nwaves = strips * ((h + seg - 1) / seg);
+    const dim3 grid((nwaves + 3) / 4), blk(256);
+    hipStream_t s = as_stream(stream);
+#define MPX_PROBE(VV, DD) \
+    if (v == VV && d == DD) { hipLaunchKernelGGL((strip_copy_kernel<VV, DD>), grid, blk, 0, s, in, out, w, h, seg, nwaves, strips); return MPX_OK; }
+    MPX_PROBE(2, 4) MPX_PROBE(2, 8) MPX_PROBE(4, 4) MPX_PROBE(4, 8) MPX_PROBE(4, 2)
+#undef MPX_PROBE
+    set_error("unsupported probe v=%d d=%d", v, d);
+    return MPX_ERR_ARG;
+}
 
 }  // namespace mpx
 
@@ -49,6 +99,12 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         const Taps st = make_taps(k, wx, wy, true, true);
         const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
         const int sm = p2 >= 1000 ? 0 : 1;
+        // p2 % 1000 = minimum prefetch depth in rows (0 / 4: production 5, 8: 10, 12: 15)
+        const int pf = p2 % 1000;
+        if (kind == 3 && pf == 8)
+            return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 8>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
+        if (kind == 3 && pf == 12)
+            return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 12>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
         if (kind == 3)
             return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
         return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::RuntimeSepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);

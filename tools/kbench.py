@@ -68,7 +68,7 @@ def main():
     fs5 = ops.get_filter("sobel5")
     swx, swy = fs5.c_taps()
     sref = ops.conv(img, fs5)
-    for seg in (0, 8, 12, 16, 17, 18, 20, 24, 32):
+    for seg in (0, 8, 16, 20, 24, 32):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
                 (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5,
@@ -76,11 +76,20 @@ def main():
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
             (lambda seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg, 1000, 1,
                                                               swx, swy, 0))), sref)
+    for pf in (8, 12):  # deeper prefetch ring
+        for seg in (0, 20, 24, 32):
+            variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
+                (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg,
+                                                                         pf, 1, swx, swy, 0))), sref)
     for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
         f = ops.get_filter(fname)
         variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ops.conv(img, f))
         variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ops.conv(img, f))
     variants["copy/torch"] = ((lambda: out.copy_(img)), img)
+    for v, d, seg in ((2, 4, 8), (2, 4, 24), (2, 8, 24), (4, 4, 8), (4, 4, 24), (4, 8, 24), (4, 2, 24), (4, 4, 48)):
+        variants[f"copy/strip-v{v}-d{d}-seg{seg}"] = (
+            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(img.data_ptr(), out.data_ptr(), n, n, v, d,
+                                                                            seg, 0))), img)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(img, out, geometry=g)), rob_ref)
