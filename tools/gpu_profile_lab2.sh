@@ -1,0 +1,16 @@
+#!/bin/bash
+# lab2 conv kernels only: kernel-trace stats + PMC counter groups (profiles/lab2_conv.md).
+set -o pipefail
+cd "$(dirname "$0")/.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+R=$PWD
+O=$R/gpurun_out/proflab2
+rm -rf $O; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/tools/prof_all.py lab2 > $O/trace.log 2>&1 || { tail -20 $O/trace.log; exit 1; }
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $O/pmc$i -o run -- python3 $R/tools/prof_all.py lab2 > $O/pmc$i.log 2>&1 || { echo "pmc group $i failed"; tail -5 $O/pmc$i.log; exit 2; }
+  echo "pmc group $i ok"
+done

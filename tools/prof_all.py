@@ -19,7 +19,7 @@ def main():
     if "lab2" in which:
         img = torch.randint(0, 256, (4096, 4096, 4), dtype=torch.uint8, device=dev)
         out = torch.empty_like(img)
-        for f in ("sobel5", "sobel5_dense", "roberts", "sobel3"):
+        for f in ("sobel5", "sobel5_dense", "gauss5", "roberts", "sobel3"):
             for _ in range(REPS + 1):
                 ops.conv(img, f, out)
     if "lab1" in which:
