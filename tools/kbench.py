@@ -68,7 +68,7 @@ def main():
     fs5 = ops.get_filter("sobel5")
     swx, swy = fs5.c_taps()
     sref = ops.conv(img, fs5)
-    for seg in (0, 8, 16, 20, 24, 32):
+    for seg in (0, 8, 20, 24):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
                 (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5,
@@ -76,8 +76,12 @@ def main():
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
             (lambda seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg, 1000, 1,
                                                               swx, swy, 0))), sref)
-    for pf in (8, 12):  # deeper prefetch ring
-        for seg in (0, 20, 24, 32):
+    for seg, per in ((0, 0), (0, 3), (0, 5), (0, 6), (8, 0), (12, 0), (16, 0), (24, 0), (32, 0)):
+        variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
+            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 5, seg,
+                                                                       per, 1, swx, swy, 0))), sref)
+    for pf in (8,):  # deeper prefetch ring
+        for seg in (0,):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
                 (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg,
                                                                          pf, 1, swx, swy, 0))), sref)
