@@ -531,7 +531,13 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         const uint32_t *row = src + (int64_t)gy * pitch;
         uint2 r;
         if constexpr (VEC) {  // w even: the pair is entirely inside, left or right
-            r = *reinterpret_cast<const uint2 *>(row + cc);
+            // buffer load: the row base lives in the (scalar) descriptor and the
+            // lane's byte offset is loop-invariant — no per-row address VALU
+            const __amdgpu_buffer_rsrc_t rrow = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0,
+                                                                                  w * 4, 0x00020000);
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rrow, cc * 4, 0, 0);
+            r = make_uint2(v.x, v.y);
         } else {
             r = make_uint2(row[mpx_clampi(cin, 0, w - 1)], row[mpx_clampi(cin + 1, 0, w - 1)]);
         }
@@ -659,18 +665,20 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             // out-of-range offset and the hardware bounds check drops them.
             // Stores under a branch would make the outstanding-op count
             // unknowable to hipcc and cost a vmcnt(0) drain of the ring.
+            // rows past the segment get a zero-length descriptor (scalar select),
+            // lanes with nothing to store a constant out-of-range offset
             const bool row_ok = y < ye;
             const int yc = row_ok ? y : ys;
             const __amdgpu_buffer_rsrc_t orow =
-                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, w * 4, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
             constexpr int kDrop = 0x7ffffff0;
             if constexpr (VEC) {
                 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
                 const u32x2_t pv = {v0, v1};
-                __builtin_amdgcn_raw_buffer_store_b64(pv, orow, (st0 && row_ok) ? ox * 4 : kDrop, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(pv, orow, st0 ? ox * 4 : kDrop, 0, 0);
             } else {
-                __builtin_amdgcn_raw_buffer_store_b32(v0, orow, (st0 && row_ok) ? ox * 4 : kDrop, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(v1, orow, (st1 && row_ok) ? ox * 4 + 4 : kDrop, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(v0, orow, st0 ? ox * 4 : kDrop, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(v1, orow, st1 ? ox * 4 + 4 : kDrop, 0, 0);
             }
         }
     }
