@@ -21,12 +21,15 @@ template <> struct Vec16<float> { using type = f4_t; static constexpr int n = 4;
 
 template <typename V> __device__ __forceinline__ V vsub(V a, V b) { return a - b; }
 
-template <typename T>
+// kUnroll independent 16-B vectors per operand in flight per thread and
+// grid-stride step: 4 for launches that fill the GPU, 16 for "thin" harness
+// geometries ([1, 32], [4, 64] ...: a few waves streaming a whole vector are
+// latency-bound, and only loads in flight per lane help them)
+template <typename T, int kUnroll>
 __global__ void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ c,
                                 int64_t n) {
     using V = typename Vec16<T>::type;
     constexpr int kV = Vec16<T>::n;
-    constexpr int kUnroll = 4;
     const int64_t nvec = n / kV;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const V *__restrict__ av = reinterpret_cast<const V *>(a);
@@ -78,8 +81,11 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
         grid = (int)(g < 1 ? 1 : (g > cap ? cap : g));
     }
     if (block == 0) block = 256;
-    if (vec)
-        hipLaunchKernelGGL(vsub_vec_kernel<T>, dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
+    const bool thin = (int64_t)grid * block < 16384;
+    if (vec && thin)
+        hipLaunchKernelGGL((vsub_vec_kernel<T, 16>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
+    else if (vec)
+        hipLaunchKernelGGL((vsub_vec_kernel<T, 4>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     else
         hipLaunchKernelGGL(vsub_scalar_kernel<T>, dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());

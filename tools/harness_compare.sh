@@ -5,10 +5,12 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+# usage: harness_compare.sh [lab2] [lab1]   (default: both)
+WHICH="${*:-lab2 lab1}"
 O=$PWD/gpurun_out/harness_cmp
-rm -rf $O; mkdir -p $O
+mkdir -p $O
 GEOMS2='[[[16,16],[1024,1024]],[[16,16],[32,32]],[[2,2],[16,16]],[[32,32],[16,16]],[[32,32],[64,64]],[[0,0],[0,0]]]'
-for bucket in small medium large; do
+for bucket in $([[ " $WHICH " == *" lab2 "* ]] && echo small medium large); do
   for timing in cold warm; do
     W=$O/lab2_${bucket}_${timing}/lab2; mkdir -p $W/src
     cp labs/lab2/src/to_plot_hip_exe labs/lab2/src/cpu_exe $W/src/
@@ -20,7 +22,7 @@ for bucket in small medium large; do
   done
 done
 GEOMS1='[[1,32],[4,64],[32,128],[512,512],[1024,1024],[-1,-1]]'
-for n in 1000 10000 1000000; do
+for n in $([[ " $WHICH " == *" lab1 "* ]] && echo 1000 10000 1000000); do
   for timing in cold warm; do
     W=$O/lab1_${n}_${timing}/lab1; mkdir -p $W/src
     cp labs/lab1/src/to_plot_hip_exe labs/lab1/src/cpu_exe $W/src/
