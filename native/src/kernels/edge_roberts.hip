@@ -76,7 +76,7 @@ __global__ void roberts_geom_kernel(const uint32_t *__restrict__ in, uint32_t *_
                     const float gyv = y10 - y01;
                     const float a = gxv * gxv;
                     const float b2 = gyv * gyv;
-                    res[k] = mpx_px_gray(mpx_sat_u8(sqrtf(a + b2)), mpx_px_a(own[k]));
+                    res[k] = mpx_px_gray(edge::mag_to_gray<true>(a + b2), mpx_px_a(own[k]));  // == trunc(sqrtf), see mag_to_gray
                 }
                 if constexpr (VEC == 4) {
                     if (xs < w) *reinterpret_cast<uint4 *>(out + (int64_t)y * w + xs) = make_uint4(res[0], res[1], res[2], res[3]);
@@ -97,48 +97,69 @@ __global__ void roberts_geom_kernel(const uint32_t *__restrict__ in, uint32_t *_
 // neighbours, no LDS, no barrier) and keeps U tiles' loads in flight.
 // Identical tile walk and arithmetic, so identical pixels.
 // ---------------------------------------------------------------------------
-template <int U>
+template <int U, bool VEC>
 __global__ void roberts_thin_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int w, int h) {
     const int bx = blockDim.x, by = blockDim.y;
     const int TW = 4 * bx, TH = by;
     const int tiles_x = (w + TW - 1) / TW, tiles_y = (h + TH - 1) / TH;
     const int nx = blockIdx.x < tiles_x ? (tiles_x - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
     const int ny = blockIdx.y < tiles_y ? (tiles_y - blockIdx.y + gridDim.y - 1) / gridDim.y : 0;
-    const int64_t ntiles = (int64_t)nx * ny;  // this block's tiles, row-major as the LDS kernel walks them
-    for (int64_t j0 = 0; j0 < ntiles; j0 += U) {
-        uint4 q0[U], q1[U];
-        uint32_t r0[U], r1[U];
+    const int ntiles = nx * ny;  // this block's tiles, row-major as the LDS kernel walks them
+    int k = 0, m = 0;            // (column, row) index of tile j0 in that walk — block-uniform, no division
+    for (int j0 = 0; j0 < ntiles; j0 += U) {
+        uint32_t a[U][5], b[U][5];  // pixels x .. x+4 (clamped) of rows y and y+1
         int xs[U], y[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t j = min(j0 + u, ntiles - 1);
-            const int tyt = blockIdx.y + (int)(j / nx) * gridDim.y, txt = blockIdx.x + (int)(j % nx) * gridDim.x;
+            // tiles past the end repeat the last one (loaded, never stored)
+            const int tyt = blockIdx.y + m * gridDim.y, txt = blockIdx.x + k * gridDim.x;
+            if (j0 + u + 1 < ntiles && ++k == nx) {
+                k = 0;
+                ++m;
+            }
             xs[u] = txt * TW + 4 * threadIdx.x;
             y[u] = tyt * TH + threadIdx.y;
-            const int ya = min(y[u], h - 1), yb = min(y[u] + 1, h - 1);
-            const int xc = min(xs[u], w - 4), xr = min(xs[u] + 4, w - 1);
-            q0[u] = *reinterpret_cast<const uint4 *>(in + (int64_t)ya * w + xc);
-            q1[u] = *reinterpret_cast<const uint4 *>(in + (int64_t)yb * w + xc);
-            r0[u] = in[(int64_t)ya * w + xr];
-            r1[u] = in[(int64_t)yb * w + xr];
+            const uint32_t *ra = in + (int64_t)min(y[u], h - 1) * w;
+            const uint32_t *rb = in + (int64_t)min(y[u] + 1, h - 1) * w;
+            if constexpr (VEC) {  // w % 4 == 0: the quad is inside the row or the thread has no output
+                const int xc = min(xs[u], w - 4);
+                const uint4 qa = *reinterpret_cast<const uint4 *>(ra + xc);
+                const uint4 qb = *reinterpret_cast<const uint4 *>(rb + xc);
+                a[u][0] = qa.x; a[u][1] = qa.y; a[u][2] = qa.z; a[u][3] = qa.w;
+                b[u][0] = qb.x; b[u][1] = qb.y; b[u][2] = qb.z; b[u][3] = qb.w;
+                a[u][4] = ra[min(xs[u] + 4, w - 1)];
+                b[u][4] = rb[min(xs[u] + 4, w - 1)];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) {
+                    a[u][k] = ra[min(xs[u] + k, w - 1)];
+                    b[u][k] = rb[min(xs[u] + k, w - 1)];
+                }
+            }
         }
+        __builtin_amdgcn_sched_barrier(0);  // all U tiles' loads in flight before the first use
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (j0 + u >= ntiles || y[u] >= h || xs[u] >= w) continue;
-            const uint32_t a[5] = {q0[u].x, q0[u].y, q0[u].z, q0[u].w, r0[u]};
-            const uint32_t b[5] = {q1[u].x, q1[u].y, q1[u].z, q1[u].w, r1[u]};
             uint32_t res[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float y00 = mpx_luma(a[k]), y10 = mpx_luma(a[k + 1]);
-                const float y01 = mpx_luma(b[k]), y11 = mpx_luma(b[k + 1]);
+                const float y00 = mpx_luma(a[u][k]), y10 = mpx_luma(a[u][k + 1]);
+                const float y01 = mpx_luma(b[u][k]), y11 = mpx_luma(b[u][k + 1]);
                 const float gxv = y11 - y00;
                 const float gyv = y10 - y01;
                 const float s0 = gxv * gxv;
                 const float s1 = gyv * gyv;
-                res[k] = mpx_px_gray(mpx_sat_u8(sqrtf(s0 + s1)), mpx_px_a(a[k]));
+                res[k] = mpx_px_gray(edge::mag_to_gray<true>(s0 + s1), mpx_px_a(a[u][k]));  // == trunc(sqrtf), see mag_to_gray
             }
-            *reinterpret_cast<uint4 *>(out + (int64_t)y[u] * w + xs[u]) = make_uint4(res[0], res[1], res[2], res[3]);
+            uint32_t *o = out + (int64_t)y[u] * w + xs[u];
+            if (VEC) {
+                *reinterpret_cast<uint4 *>(o) = make_uint4(res[0], res[1], res[2], res[3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (xs[u] + k < w) o[k] = res[k];
+            }
         }
     }
 }
@@ -172,8 +193,11 @@ int roberts_impl(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by
     const int VEC = vec ? 4 : 1;
     const size_t lds = sizeof(float) * (size_t)(by + 1) * (size_t)(VEC * bx + 4);
     MPX_CHECK_ARG(lds <= 64 * 1024, "tile does not fit the 64 KiB per-workgroup LDS limit");
-    if (vec && (int64_t)bx * by * gx * gy < 16384)
-        hipLaunchKernelGGL(roberts_thin_kernel<8>, dim3(gx, gy), dim3(bx, by), 0, as_stream(stream), in, out, w, h);
+    const bool thin = (int64_t)bx * by * gx * gy < 16384;
+    if (thin && vec)
+        hipLaunchKernelGGL((roberts_thin_kernel<8, true>), dim3(gx, gy), dim3(bx, by), 0, as_stream(stream), in, out, w, h);
+    else if (thin)
+        hipLaunchKernelGGL((roberts_thin_kernel<4, false>), dim3(gx, gy), dim3(bx, by), 0, as_stream(stream), in, out, w, h);
     else if (vec)
         hipLaunchKernelGGL(roberts_geom_kernel<4>, dim3(gx, gy), dim3(bx, by), lds, as_stream(stream), in, out, w, h);
     else

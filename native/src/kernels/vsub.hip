@@ -22,7 +22,7 @@ template <> struct Vec16<float> { using type = f4_t; static constexpr int n = 4;
 template <typename V> __device__ __forceinline__ V vsub(V a, V b) { return a - b; }
 
 // kUnroll independent 16-B vectors per operand in flight per thread and
-// grid-stride step: 4 for launches that fill the GPU, 16 for "thin" harness
+// grid-stride step: 4 for launches that fill the GPU, 8 for "thin" harness
 // geometries ([1, 32], [4, 64] ...: a few waves streaming a whole vector are
 // latency-bound, and only loads in flight per lane help them)
 template <typename T, int kUnroll>
@@ -44,6 +44,10 @@ __global__ void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b
             x[u] = av[i + u * stride];
             y[u] = bv[i + u * stride];
         }
+        // every load issued before the first use: left alone the scheduler
+        // interleaves load pairs with the (possibly aliasing, to its mind)
+        // stores and waits for each pair
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) __builtin_nontemporal_store(vsub(x[u], y[u]), &cv[i + u * stride]);
     }
@@ -83,7 +87,7 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
     if (block == 0) block = 256;
     const bool thin = (int64_t)grid * block < 16384;
     if (vec && thin)
-        hipLaunchKernelGGL((vsub_vec_kernel<T, 16>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
+        hipLaunchKernelGGL((vsub_vec_kernel<T, 8>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     else if (vec)
         hipLaunchKernelGGL((vsub_vec_kernel<T, 4>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     else
