@@ -8,7 +8,48 @@ import sys
 
 import pandas as pd
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/harness_cmp"
+# the reference's published medians (RTX A6000, one cold launch per process, ms)
+BASELINE = {
+    ("lab1", "1000"): {"CPU": 0.004, "[1, 32]": 0.14936, "[4, 64]": 0.14438, "[32, 128]": 0.14429,
+                       "[512, 512]": 0.14653, "[1024, 1024]": 0.14592},
+    ("lab1", "10000"): {"CPU": 0.081, "[1, 32]": 0.20557, "[4, 64]": 0.14816, "[32, 128]": 0.14064,
+                        "[512, 512]": 0.14203, "[1024, 1024]": 0.14280},
+    ("lab1", "1000000"): {"CPU": 8.338, "[1, 32]": 11.57053, "[4, 64]": 1.54635, "[32, 128]": 0.20198,
+                          "[512, 512]": 0.13456, "[1024, 1024]": 0.13926},
+    ("lab2", "small"): {"CPU": 0.001, "[[16, 16], [1024, 1024]]": 0.85797, "[[16, 16], [32, 32]]": 0.16846,
+                        "[[2, 2], [16, 16]]": 0.16718, "[[32, 32], [16, 16]]": 0.16693, "[[32, 32], [64, 64]]": 0.17912},
+    ("lab2", "medium"): {"CPU": 16.7635, "[[16, 16], [1024, 1024]]": 0.86232, "[[16, 16], [32, 32]]": 0.16573,
+                         "[[2, 2], [16, 16]]": 0.26202, "[[32, 32], [16, 16]]": 0.17045, "[[32, 32], [64, 64]]": 0.18253},
+    ("lab2", "large"): {"CPU": 37.891, "[[16, 16], [1024, 1024]]": 0.87987, "[[16, 16], [32, 32]]": 0.18054,
+                        "[[2, 2], [16, 16]]": 0.51288, "[[32, 32], [16, 16]]": 0.17866, "[[32, 32], [64, 64]]": 0.19272},
+}
+
+
+def vs_baseline(out: "pd.DataFrame") -> None:
+    """Per published configuration: reference median, ours cold / warm, cold speedup."""
+    for (lab, size), ref in BASELINE.items():
+        g = out[(out.lab == lab) & (out["size"] == size)]
+        if g.empty:
+            continue
+        print(f"\n### {lab} {'n = ' + size if lab == 'lab1' else size + ' bucket'}\n")
+        print("| launch geometry | reference RTX A6000 (cold) | MI355X cold | MI355X warm | cold speedup |")
+        print("|---|---|---|---|---|")
+        keys = list(ref) + sorted(k for k in set(g.geometry) if k not in ref and not k.startswith("CPU"))
+        for k in keys:
+            sel = g[g.geometry == k] if k != "CPU" else g[g.device.str.startswith("CPU")]
+            cold = sel[sel.timing == "cold"].median_ms
+            warm = sel[sel.timing == "warm"].median_ms
+            c = float(cold.iloc[0]) if len(cold) else None
+            w = float(warm.iloc[0]) if len(warm) else None
+            r = ref.get(k)
+            label = {"CPU": "CPU (serial -O0)", "[-1, -1]": "auto (tuned)", "[[0, 0], [0, 0]]": "auto (tuned)"}.get(k, k)
+            sp = f"**{r / c:.1f}x**" if r and c else "—"
+            fmt = lambda v: "—" if v is None else f"{v:.5f}"  # noqa: E731
+            print(f"| {label} | {r if r is not None else '—'} | {fmt(c)} | {fmt(w)} | {sp} |")
+
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+root = args[0] if args else "gpurun_out/harness_cmp"
 rows = []
 for d in sorted(glob.glob(os.path.join(root, "*", "lab*"))):
     tag = os.path.basename(os.path.dirname(d))
@@ -20,6 +61,10 @@ for d in sorted(glob.glob(os.path.join(root, "*", "lab*"))):
             rows.append({"lab": lab, "size": size, "timing": timing, "device": dev, "geometry": ks,
                          "median_ms": g["time_kernel_exe_ms"].median(), "runs": len(g)})
 out = pd.DataFrame(rows)
+if "--vs-baseline" in sys.argv:
+    out["geometry"] = [("CPU" if d.startswith("CPU") else g) for d, g in zip(out.device, out.geometry)]
+    vs_baseline(out)
+    sys.exit(0)
 for (lab, size), g in out.groupby(["lab", "size"], sort=False):
     print(f"\n### {lab} {size}\n")
     piv = g.pivot_table(index=["device", "geometry"], columns="timing", values="median_ms", aggfunc="first")
