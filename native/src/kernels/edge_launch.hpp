@@ -53,7 +53,7 @@ int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
 // rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
 inline constexpr int kSegRows = 8;
 
-template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4>
+template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, bool BUFLD = true>
 int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                 const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1,
                 edge::RowSrc rs = edge::RowSrc{}) {
@@ -75,10 +75,10 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
     const unsigned nblk = (unsigned)((nwaves + 3) / 4);
     if (vec)
-        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX, PF>), dim3(nblk), dim3(256), 0, s, in,
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, true, FAST, F, OWX, PF, BUFLD>), dim3(nblk), dim3(256), 0, s, in,
                            out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps, rs);
     else
-        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX, PF>), dim3(nblk), dim3(256), 0, s, in,
+        hipLaunchKernelGGL((edge::conv_wave_kernel<K, A, MODE, false, FAST, F, OWX, PF, BUFLD>), dim3(nblk), dim3(256), 0, s, in,
                            out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, strip_minor, taps, rs);
     return MPX_OK;
 }

@@ -109,6 +109,20 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
             return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
         return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::RuntimeSepTaps>(in, out, w, w, 0, h, 0, h - 1, st, vec2, s, p1, sm);
     }
+    if (kind == 6 || kind == 7) {
+        // A/B of the row loads: kind 6 separable sobel5, kind 7 Roberts, both
+        // compiled-in taps; p2 = 1 plain global loads, 0 buffer loads (production)
+        MPX_CHECK_ARG(p1 >= 0 && w % 2 == 0, "A/B variant: even width");
+        const bool sep = kind == 6;
+        MPX_CHECK_ARG(k == (sep ? 5 : 2), "kind 6: k = 5, kind 7: k = 2");
+        const Taps st = make_taps(k, wx, wy, true, sep);
+        const int seg = p1 > 0 ? p1 : (sep ? 0 : edgel::kSegRows);
+        if (sep)
+            return p2 == 1 ? launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, false>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg)
+                           : launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, true>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+        return p2 == 1 ? launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, false>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg)
+                       : launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, true>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+    }
     if (kind == 5) {
         // 16-B-lane separable sobel5 (conv_wave4_kernel): p1 = segment rows (0 = auto),
         // p2 = waves per SIMD the auto segments target (0 = production default)

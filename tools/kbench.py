@@ -80,6 +80,16 @@ def main():
         variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 5, seg,
                                                                        per, 1, swx, swy, 0))), sref)
+    rf = ops.get_filter("roberts")
+    rwx, rwy = rf.c_taps()
+    rref = ops.conv(img, rf)
+    for p2, nm in ((0, "buffer"), (1, "global")):  # row-load A/B
+        variants[f"sobel5-sep/loads-{nm}"] = (
+            (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 6, 0, p2, 1,
+                                                            swx, swy, 0))), sref)
+        variants[f"roberts/loads-{nm}"] = (
+            (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 2, 7, 0, p2, 1,
+                                                            rwx, rwy, 0))), rref)
     for pf in (8,):  # deeper prefetch ring
         for seg in (0,):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
