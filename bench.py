@@ -87,6 +87,9 @@ def main() -> int:
     p.add_argument("--halo", choices=["auto", "peer", "rccl"], default="auto",
                    help="halo transport for N > 1: one-sided xGMI loads from IPC-mapped neighbour slabs (peer), "
                         "RCCL send/recv (rccl), or peer when available (auto)")
+    p.add_argument("--graph", type=int, default=0,
+                   help="capture this many steps into one HIP graph and replay it (0 = eager launches; "
+                        "in-order and peer halo modes)")
     p.add_argument("--watchdog", type=float, default=None,
                    help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -113,11 +116,25 @@ def main() -> int:
     sync(ctx)
     ctx.barrier()
 
+    graph = None
+    single_stream = not ctx.is_distributed or det.peer is not None or not (det.pipeline or det.overlap)
+    if args.graph > 0 and ctx.device.type == "cuda" and single_stream:
+        from cuda_mpi_openmp_amd.utils.graphs import try_step_graph
+
+        graph = try_step_graph(det.step, args.graph, ctx.device)
+        sync(ctx)
+        ctx.barrier()
+
     # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
     ctx.barrier()
     sync(ctx)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    done = 0
+    if graph is not None:  # every replay runs args.graph complete steps
+        while done + args.graph <= args.steps:
+            graph.replay()
+            done += args.graph
+    for _ in range(args.steps - done):
         det.step()
     det.finish()
     sync(ctx)
@@ -166,6 +183,7 @@ def main() -> int:
                 "transport": det.transport if n > 1 else None,
                 "image_hw": [args.size * n, args.size],
                 "halo_rows": [det.filter.halo_up, det.filter.halo_down],
+                "graph_steps": args.graph if graph is not None else 0,
             },
             "verified_bit_exact": ok,
             "device": str(torch.cuda.get_device_name(ctx.device)) if ctx.device.type == "cuda" else "cpu",

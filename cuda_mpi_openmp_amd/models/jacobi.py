@@ -56,6 +56,7 @@ class SlabJacobi:
         self.iteration = 0
         self.last_residual: Optional[float] = None
         self._halos_valid = False  # u's halo rows hold the neighbours' current rows
+        self._graphs: dict = {}  # (u pointer at cycle start, check_every) -> StepGraph of one cycle
 
     # ------------------------------------------------------------------ setup
     def set_boundary(self, top: float = 1.0, bottom: float = 0.0, left: float = 0.0, right: float = 0.0) -> None:
@@ -107,9 +108,19 @@ class SlabJacobi:
         _fault_hook(self.ctx.rank, self.iteration)
         if not self._halos_valid:
             self.sync_halos()
+        track = (self.iteration + 1) % self.check_every == 0
+        self._advance(track)
+        if track:
+            self.last_residual = float(self.resid.item())
+            return self.last_residual
+        return None
+
+    def _advance(self, track: bool) -> None:
+        """One iteration's device work (sweeps, halo exchange, swap and, when
+        tracking, the residual all-reduce) with no host synchronisation, so it
+        can be captured into a HIP graph."""
         s = self.slab
         n = s.rows
-        track = (self.iteration + 1) % self.check_every == 0
         if track:
             self.resid.zero_()
         if self.ctx.is_distributed and self.overlap:
@@ -126,16 +137,73 @@ class SlabJacobi:
         self.iteration += 1
         if track:
             all_reduce_max(self.resid, self.ctx)
-            self.last_residual = float(self.resid.item())
-            return self.last_residual
-        return None
 
-    def run(self, iters: int, tol: Optional[float] = None) -> int:
-        for _ in range(iters):
+    def run(self, iters: int, tol: Optional[float] = None, graph: bool = False) -> int:
+        """``iters`` iterations (fewer once the residual drops below ``tol``).
+
+        ``graph=True`` (GPU): the iterations run as replays of one HIP graph of
+        a whole residual cycle — check_every iterations, doubled to an even
+        count so u/un are back in place at the end of every replay — with the
+        host reading the residual once per replay. Launch-bound sweeps (small
+        slabs, many ranks) no longer wait on the host's per-launch cost.
+        Falls back to eager steps when the step cannot be captured."""
+        done = 0
+        if graph and self.u.is_cuda:
+            done = self._run_graph(iters, tol)
+            if done < 0:  # tolerance reached inside the graphed part
+                return self.iteration
+        for _ in range(iters - done):
             r = self.step()
             if tol is not None and r is not None and r < tol:
                 break
         return self.iteration
+
+    def _cycle_graph(self):
+        """The HIP graph of one residual cycle (check_every iterations) starting
+        from the current u/un roles; with an odd check_every the roles
+        alternate between cycles, so two graphs exist. Captured once, reused
+        by every later run() (capture + instantiate cost milliseconds)."""
+        from ..utils.graphs import try_step_graph
+
+        key = (self.u.data_ptr(), self.check_every)
+        if key in self._graphs:
+            return self._graphs[key]
+        state = (self.u, self.un, self.iteration)
+        it = [0]
+
+        def body():  # the last iteration of the cycle tracks the residual, as in step()
+            it[0] += 1
+            self._advance(it[0] == self.check_every)
+
+        g = try_step_graph(body, self.check_every, self.u.device, warmup=0)
+        self.u, self.un, self.iteration = state  # the capture recorded the cycle, it did not run it
+        self._graphs[key] = g
+        return g
+
+    def _run_graph(self, iters: int, tol: Optional[float]) -> int:
+        if not self._halos_valid:
+            self.sync_halos()
+        # align to a cycle boundary eagerly, so every replay starts a cycle
+        done = 0
+        while self.iteration % self.check_every and done < iters:
+            r = self.step()
+            done += 1
+            if tol is not None and r is not None and r < tol:
+                return -1
+        while iters - done >= self.check_every:
+            g = self._cycle_graph()
+            if g is None:
+                return done
+            _fault_hook(self.ctx.rank, self.iteration)
+            g.replay()
+            if self.check_every % 2:
+                self.u, self.un = self.un, self.u
+            self.iteration += self.check_every
+            done += self.check_every
+            self.last_residual = float(self.resid.item())
+            if tol is not None and self.last_residual < tol:
+                return -1
+        return done
 
     # ------------------------------------------------------------------ I/O
     def gather(self) -> Optional[torch.Tensor]:

@@ -30,6 +30,7 @@ def main() -> int:
     p.add_argument("--fp32", action="store_true")
     p.add_argument("--overlap", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    p.add_argument("--graph", action="store_true", help="replay HIP graphs of whole residual cycles")
     a = p.parse_args()
     ctx = parallel.init(device=a.device)
     dt = torch.float32 if a.fp32 else torch.float64
@@ -38,11 +39,11 @@ def main() -> int:
     sol.set_boundary(top=1.0)
     sol.fill(seed=0)
     sync = (lambda: torch.cuda.synchronize(ctx.device)) if ctx.device.type == "cuda" else (lambda: None)
-    sol.run(a.warmup)
+    sol.run(a.warmup, graph=a.graph)
     sync()
     ctx.barrier()
     t0 = time.perf_counter()
-    sol.run(a.iters)
+    sol.run(a.iters, graph=a.graph)
     sync()
     ctx.barrier()
     el = parallel.max_over_ranks(time.perf_counter() - t0, ctx)
@@ -58,7 +59,8 @@ def main() -> int:
             "TBps_aggregate": round(2 * a.size * a.size * es / (ms * 1e-3) / 1e12, 3),
             "residual": sol.last_residual,
             "transport": ("native-rccl" if ctx.native is not None else "torch.distributed") if ctx.world > 1 else None,
-            "halo": ("overlap" if sol.overlap else "inorder") if ctx.world > 1 else None}), flush=True)
+            "halo": ("overlap" if sol.overlap else "inorder") if ctx.world > 1 else None,
+            "hip_graph": bool(a.graph and ctx.device.type == "cuda")}), flush=True)
     parallel.shutdown()
     return 0
 
