@@ -42,6 +42,7 @@ _SIGNATURES = {
     "mpx_stream_sync": (c_int, [c_vp]),
     "mpx_vsub_f64": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "mpx_vsub_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
+    "mpx_vsub_variant": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "mpx_roberts": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "mpx_conv": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
     "mpx_conv_direct": (

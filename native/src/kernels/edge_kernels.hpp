@@ -477,7 +477,7 @@ __device__ __forceinline__ f2_t luma2(uint32_t p0, uint32_t p1) {
     return (t0 + t1) + t2;
 }
 
-template <int K, int A, int MODE, bool VEC, bool FAST, class F = RuntimeTaps, int OWX = 0, int PF = 4, bool BUFLD = true>
+template <int K, int A, int MODE, bool VEC, bool FAST, class F = RuntimeTaps, int OWX = 0, int PF = 4, int BUFLD = 1>
 __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                         int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                         int seg, int segs_per_strip, int nwaves, int strips,
@@ -530,7 +530,11 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
         const uint32_t *row = src + (int64_t)gy * pitch;
         uint2 r;
-        if constexpr (VEC && !BUFLD) {
+        if constexpr (VEC && BUFLD == 2) {  // non-temporal global load (A/B variant)
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t *>(row + cc));
+            r = make_uint2(v.x, v.y);
+        } else if constexpr (VEC && BUFLD == 0) {
             r = *reinterpret_cast<const uint2 *>(row + cc);
         } else if constexpr (VEC) {  // w even: the pair is entirely inside, left or right
             // buffer load: the row base lives in the (scalar) descriptor and the

@@ -53,7 +53,7 @@ int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
 // rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
 inline constexpr int kSegRows = 8;
 
-template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, bool BUFLD = true>
+template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, int BUFLD = 1>
 int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                 const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1,
                 edge::RowSrc rs = edge::RowSrc{}) {

@@ -117,11 +117,15 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         MPX_CHECK_ARG(k == (sep ? 5 : 2), "kind 6: k = 5, kind 7: k = 2");
         const Taps st = make_taps(k, wx, wy, true, sep);
         const int seg = p1 > 0 ? p1 : (sep ? 0 : edgel::kSegRows);
-        if (sep)
-            return p2 == 1 ? launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, false>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg)
-                           : launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, true>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
-        return p2 == 1 ? launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, false>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg)
-                       : launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, true>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+        // p2: 0 buffer loads (production), 1 plain global loads, 2 non-temporal global loads
+        if (sep) {
+            if (p2 == 1) return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 0>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+            if (p2 == 2) return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 2>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+            return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 1>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+        }
+        if (p2 == 1) return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 0>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+        if (p2 == 2) return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 2>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+        return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 1>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
     }
     if (kind == 5) {
         // 16-B-lane separable sobel5 (conv_wave4_kernel): p1 = segment rows (0 = auto),

@@ -3,10 +3,14 @@
 // Reference: lab1/src/main.cu:22-29 (one scalar element per thread per
 // grid-stride step). MI355X design: pure HBM streaming (AI = 1/24 flop/B), so
 // every lane moves 16 B per access (double2 / float4), keeps four independent
-// 16-B loads per operand in flight per grid-stride step, and writes with
-// non-temporal stores because the result is never re-read by this kernel.
+// 16-B loads per operand in flight per grid-stride step, and both reads and
+// writes are non-temporal: nothing is re-read by this kernel, so none of it
+// should displace L2/MALL lines (tools/vsub_sweep.py: non-temporal loads take
+// 2^26 fp32 from 131.7 to 122.4 us, 6.12 -> 6.58 TB/s).
 // Launch geometry is honoured exactly when the caller passes one (the harness
 // sweeps [grid, block] pairs); 0/0 picks one vector per thread (see below).
+#include <algorithm>
+
 #include "internal.hpp"
 
 namespace mpx {
@@ -41,8 +45,8 @@ __global__ void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b
         V x[kUnroll], y[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            x[u] = av[i + u * stride];
-            y[u] = bv[i + u * stride];
+            x[u] = __builtin_nontemporal_load(&av[i + u * stride]);
+            y[u] = __builtin_nontemporal_load(&bv[i + u * stride]);
         }
         // every load issued before the first use: left alone the scheduler
         // interleaves load pairs with the (possibly aliasing, to its mind)
@@ -51,10 +55,41 @@ __global__ void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) __builtin_nontemporal_store(vsub(x[u], y[u]), &cv[i + u * stride]);
     }
-    for (; i < nvec; i += stride) __builtin_nontemporal_store(vsub(av[i], bv[i]), &cv[i]);
+    for (; i < nvec; i += stride)
+        __builtin_nontemporal_store(vsub(__builtin_nontemporal_load(&av[i]), __builtin_nontemporal_load(&bv[i])), &cv[i]);
     // scalar tail (n not a multiple of the vector width)
     for (int64_t t = nvec * kV + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride)
         c[t] = a[t] - b[t];
+}
+
+// Tuning variants (mpx_vsub_variant): V 16-B vectors per thread, contiguous
+// (thread t owns vectors V*t .. V*t+V-1), optionally non-temporal loads.
+template <typename T, int V, bool NTLD>
+__global__ void vsub_var_kernel(const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ c, int64_t n) {
+    using W = typename Vec16<T>::type;
+    constexpr int kV = Vec16<T>::n;
+    const int64_t nvec = n / kV;
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
+    const W *__restrict__ av = reinterpret_cast<const W *>(a);
+    const W *__restrict__ bv = reinterpret_cast<const W *>(b);
+    W *__restrict__ cv = reinterpret_cast<W *>(c);
+    W x[V], y[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int64_t i = min(i0 + v, nvec - 1);
+        if constexpr (NTLD) {
+            x[v] = __builtin_nontemporal_load(&av[i]);
+            y[v] = __builtin_nontemporal_load(&bv[i]);
+        } else {
+            x[v] = av[i];
+            y[v] = bv[i];
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+        if (i0 + v < nvec) __builtin_nontemporal_store(vsub(x[v], y[v]), &cv[i0 + v]);
+    if (i0 == 0)
+        for (int64_t t = nvec * kV; t < n; ++t) c[t] = a[t] - b[t];
 }
 
 template <typename T>
@@ -96,6 +131,26 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
     return MPX_OK;
 }
 
+template <typename T>
+int launch_vsub_variant(const T *a, const T *b, T *c, int64_t n, int kind, int block, void *stream) {
+    MPX_CHECK_ARG(n > 0 && a && b && c && aligned16(a) && aligned16(b) && aligned16(c), "bad arguments");
+    if (block <= 0) block = 1024;
+    const int v = (kind & 1) ? 2 : 1;
+    const int64_t nvec = n / Vec16<T>::n;
+    const int64_t threads = (nvec + v - 1) / v;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, (threads + block - 1) / block);
+    hipStream_t s = as_stream(stream);
+    switch (kind) {
+        case 0: hipLaunchKernelGGL((vsub_var_kernel<T, 1, false>), dim3(grid), dim3(block), 0, s, a, b, c, n); break;
+        case 1: hipLaunchKernelGGL((vsub_var_kernel<T, 2, false>), dim3(grid), dim3(block), 0, s, a, b, c, n); break;
+        case 2: hipLaunchKernelGGL((vsub_var_kernel<T, 1, true>), dim3(grid), dim3(block), 0, s, a, b, c, n); break;
+        case 3: hipLaunchKernelGGL((vsub_var_kernel<T, 2, true>), dim3(grid), dim3(block), 0, s, a, b, c, n); break;
+        default: set_error("unknown vsub variant %d", kind); return MPX_ERR_ARG;
+    }
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
 }  // namespace
 MPX_MODULE_ANCHOR(vsub)
 
@@ -104,6 +159,16 @@ MPX_MODULE_ANCHOR(vsub)
 extern "C" int mpx_vsub_f64(const double *a, const double *b, double *c, int64_t n, int grid, int block,
                             void *stream) {
     return mpx::launch_vsub<double>(a, b, c, n, grid, block, stream);
+}
+
+// tuning entry (tools/vsub_sweep.py): kind bit 0 = two vectors per thread, bit 1 = non-temporal loads
+extern "C" int mpx_vsub_variant(const void *a, const void *b, void *c, int64_t n, int fp64, int kind, int block,
+                                void *stream) {
+    if (fp64)
+        return mpx::launch_vsub_variant<double>(static_cast<const double *>(a), static_cast<const double *>(b),
+                                                static_cast<double *>(c), n, kind, block, stream);
+    return mpx::launch_vsub_variant<float>(static_cast<const float *>(a), static_cast<const float *>(b),
+                                           static_cast<float *>(c), n, kind, block, stream);
 }
 
 extern "C" int mpx_vsub_f32(const float *a, const float *b, float *c, int64_t n, int grid, int block,

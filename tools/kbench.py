@@ -83,7 +83,7 @@ def main():
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
-    for p2, nm in ((0, "buffer"), (1, "global")):  # row-load A/B
+    for p2, nm in ((0, "buffer"), (1, "global"), (2, "global-nt")):  # row-load A/B
         variants[f"sobel5-sep/loads-{nm}"] = (
             (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 6, 0, p2, 1,
                                                             swx, swy, 0))), sref)

@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cuda_mpi_openmp_amd import ops  # noqa: E402
+from cuda_mpi_openmp_amd import _native, ops  # noqa: E402
 
 
 def time_us(fn, iters=20):
@@ -41,6 +41,17 @@ def main():
             us = time_us(fn)
             nb = byts if tag == "torch_sub" else 2 * n * a.element_size()
             print(json.dumps({"dtype": name, "what": tag, "us": round(us, 1), "TBps": round(nb / us / 1e6, 3)}))
+        L = _native.lib()
+        fp64 = int(dtype == torch.float64)
+        for kind, what in ((0, "1vec"), (1, "2vec"), (2, "1vec_ntload"), (3, "2vec_ntload")):
+            for block in (256, 1024):
+                us = time_us(lambda: _native.check(L.mpx_vsub_variant(a.data_ptr(), b.data_ptr(), c.data_ptr(), n, fp64,
+                                                                      kind, block, 0)))
+                ok = torch.equal(c, a - b)
+                print(json.dumps({"dtype": name, "variant": what, "block": block, "us": round(us, 1),
+                                  "TBps": round(byts / us / 1e6, 3), "ok": ok}), flush=True)
+        if os.environ.get("VSUB_VARIANTS_ONLY"):
+            continue
         for grid in (0, 256, 512, 1024, 2048, 4096, 8192, 16384):
             for block in (256, 512, 1024):
                 if grid == 0 and block != 256:
