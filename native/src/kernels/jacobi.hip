@@ -166,7 +166,7 @@ __device__ __forceinline__ T dpp_shift(T v, int ctrl) {
     }
 }
 
-template <typename T, int AUX = 0>
+template <typename T, int AUX = 0, bool LNT = false>
 __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
                                                           int nwaves, T *__restrict__ resid) {
@@ -185,7 +185,11 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
         const int i0 = r0 + rb * rows_per_wave;
         const int i1 = min(i0 + rows_per_wave, r1);
         const T *base = u + (int64_t)cvc * NV;
-        auto ld = [&](int i) { return *reinterpret_cast<const V *>(base + (int64_t)i * pitch); };
+        auto ld = [&](int i) {
+            const V *p = reinterpret_cast<const V *>(base + (int64_t)i * pitch);
+            if constexpr (LNT) return __builtin_nontemporal_load(p);  // tuning variant
+            else return *p;
+        };
         // ring: row x_{i0-1+t} lives in slot t % 5; the loop advances 5 rows so
         // every slot index is a compile-time constant (no register rotation,
         // whose moves would force a wait on the in-flight prefetch)
@@ -309,7 +313,7 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
                                   int R, int aux, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(u && un && cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0 && R >= 1, "bad arguments");
-    MPX_CHECK_ARG(aux == 0 || aux == 2, "aux must be 0 or 2");
+    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6, "aux must be 0, 2 or 6 (2 + non-temporal loads)");
     const int NV = fp64 ? 2 : 4;
     MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un), "needs the vector layout");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
@@ -319,12 +323,16 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
 #define MPX_JV(T, A)                                                                                          \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, A>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, \
                        R, nwaves, (T *)resid)
+#define MPX_JVN(T)                                                                                             \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, true>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
+                       strips, R, nwaves, (T *)resid)
     if (fp64) {
-        if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
+        if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
     } else {
-        if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
+        if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
     }
 #undef MPX_JV
+#undef MPX_JVN
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }

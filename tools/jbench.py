@@ -26,7 +26,7 @@ def main():
         var = {"production": lambda: ops.jacobi_sweep(u, un, 1, n + 1),
                "production+residual": lambda: (res_t.zero_(), ops.jacobi_sweep(u, un, 1, n + 1, res_t))}
         for R in (4, 8, 16, 32, 64):
-            for aux in (0, 2):
+            for aux in (2, 6):
                 var[f"R{R}/aux{aux}"] = (lambda R=R, aux=aux: _native.check(L.mpx_jacobi_variant(
                     u.data_ptr(), un.data_ptr(), n, n, 1, n + 1, None, int(dt == torch.float64), R, aux, 0)))
         res = {k: [] for k in var}
