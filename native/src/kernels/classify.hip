@@ -165,8 +165,14 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
                                                               ClassParams cp, FastParams fp, uint32_t *amb) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     uint4 *v = reinterpret_cast<uint4 *>(img);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-        const uint4 q = v[i];
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // software-pipelined grid-stride loop: the next 16-B vector is in flight
+    // while this one is ranked (a thread walks ~32 vectors at 8192^2; without
+    // the prefetch each step exposes a full HBM round trip)
+    uint4 qn = i < nvec ? v[i] : uint4{};
+    for (; i < nvec; i += stride) {
+        const uint4 q = qn;
+        if (i + stride < nvec) qn = v[i + stride];
         const uint32_t px[4] = {q.x, q.y, q.z, q.w};
         f2_t f[2][9];
 #pragma unroll
