@@ -377,10 +377,14 @@ struct Gauss5SepTaps {
     static constexpr float vy[5] = {0, 0, 0, 0, 0};
     static constexpr float sy = 0.0f;
 };
+// Compile-time dense filters (filters.h named entries, matched bit-exactly by
+// edgel::launch_tiled): zero taps drop out of the chains and +-1 taps fold into
+// adds; kK / kA / kMode name the window and output mode they apply to.
 // Reference Roberts operator (filters.h "roberts").
 struct RobertsTaps {
     static constexpr bool kConst = true;
     static constexpr bool kSep = false;
+    static constexpr int kK = 2, kA = 0, kMode = MPX_CONV_MAG2;
     static constexpr float wx[4] = {-1.0f, 0.0f, 0.0f, 1.0f};
     static constexpr float wy[4] = {0.0f, 1.0f, -1.0f, 0.0f};
 };
@@ -388,6 +392,7 @@ struct RobertsTaps {
 struct Sobel5Taps {
     static constexpr bool kConst = true;
     static constexpr bool kSep = false;
+    static constexpr int kK = 5, kA = 2, kMode = MPX_CONV_MAG2;
     static constexpr float wx[25] = {-1.0f / 48, -2.0f / 48, 0, 2.0f / 48, 1.0f / 48,
                                      -4.0f / 48, -8.0f / 48, 0, 8.0f / 48, 4.0f / 48,
                                      -6.0f / 48, -12.0f / 48, 0, 12.0f / 48, 6.0f / 48,
@@ -398,6 +403,50 @@ struct Sobel5Taps {
                                      0, 0, 0, 0, 0,
                                      2.0f / 48, 8.0f / 48, 12.0f / 48, 8.0f / 48, 2.0f / 48,
                                      1.0f / 48, 4.0f / 48, 6.0f / 48, 4.0f / 48, 1.0f / 48};
+};
+
+struct Sobel3Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 3, kA = 1, kMode = MPX_CONV_MAG2;
+    static constexpr float wx[9] = {-1, 0, 1, -2, 0, 2, -1, 0, 1};
+    static constexpr float wy[9] = {-1, -2, -1, 0, 0, 0, 1, 2, 1};
+};
+struct Prewitt3Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 3, kA = 1, kMode = MPX_CONV_MAG2;
+    static constexpr float wx[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1};
+    static constexpr float wy[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+};
+struct Scharr3Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 3, kA = 1, kMode = MPX_CONV_MAG2;
+    static constexpr float wx[9] = {-3, 0, 3, -10, 0, 10, -3, 0, 3};
+    static constexpr float wy[9] = {-3, -10, -3, 0, 0, 0, 3, 10, 3};
+};
+struct Laplace3Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 3, kA = 1, kMode = MPX_CONV_ABS1;
+    static constexpr float wx[9] = {0, 1, 0, 1, -4, 1, 0, 1, 0};
+    static constexpr float wy[9] = {};
+};
+struct Sharpen3Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 3, kA = 1, kMode = MPX_CONV_LIN1;
+    static constexpr float wx[9] = {0, -1, 0, -1, 5, -1, 0, -1, 0};
+    static constexpr float wy[9] = {};
+};
+struct Log5Taps {
+    static constexpr bool kConst = true;
+    static constexpr bool kSep = false;
+    static constexpr int kK = 5, kA = 2, kMode = MPX_CONV_ABS1;
+    static constexpr float wx[25] = {0, 0, -1, 0, 0, 0, -1, -2, -1, 0, -1, -2, 16, -2, -1,
+                                     0, -1, -2, -1, 0, 0, 0, -1, 0, 0};
+    static constexpr float wy[25] = {};
 };
 
 template <class F>
@@ -620,6 +669,10 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             const int u = (K - 1 + v) % K;      // window slot of the newest row
             const int q = (K - 1 + v) % D;      // its prefetch slot
             const int i = K - 1 + g * D + v;    // its input row index
+            // last group of a segment that is not a multiple of D: leave once
+            // the segment is done (wave-uniform scalar exit, no memory op skipped
+            // that a later wait would count) instead of computing dead rows
+            if (g * D + v >= ye - ys) break;
             const uint2 px = fix_pair(pre[q]);
             pre[q] = load_row(i + D);
             consume(u, px);

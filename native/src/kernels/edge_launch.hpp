@@ -50,7 +50,12 @@ int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
     return MPX_OK;
 }
 
-// rows per wave segment of the wave-streaming kernel (tuned on MI355X, tools/kbench.py)
+// rows per wave segment of the wave-streaming kernel (dense filters and the
+// single-filter separable passes). Tuned on MI355X with tools/named_taps_ab.py
+// (4096^2, segments 6 .. 23): short segments in several rounds win for the
+// dense kernels (sobel3 27.0 us, roberts 21.4-23.0, laplace3 21.8); the kernel
+// leaves a segment as soon as its rows are done, so 8 need not be a multiple
+// of the unrolled row group.
 inline constexpr int kSegRows = 8;
 
 template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, int BUFLD = 1>
@@ -63,9 +68,9 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     const int strips = (w + G::OW - 1) / G::OW;
     if (seg <= 0) {
         // one resident round of ~6 waves per SIMD: long segments (few warm-up
-        // rows), at least 8 rows each. MI355X sobel5 4096^2 sweep (kbench):
-        // 8 waves/SIMD (seg 17) 28.1 us, 6.8 (seg 20) 25.3-26.0, 5.7 (seg 24)
-        // 25.8, 17 in two rounds (seg 8) 28.1-30.3
+        // rows), at least 8 rows each. MI355X separable sobel5 4096^2 sweep
+        // (tools/named_taps_ab.py, MPX_SSEG hook since removed): auto (seg 23)
+        // 24.7 us, seg 25-30 25.0, 20 26.1, 15-16 27.1-27.6, 8-12 26.1-28.1
         const int64_t slots = (int64_t)kNumCUs * 4 * 6;
         const int64_t work = (int64_t)(oy1 - oy0) * strips;
         seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
@@ -94,18 +99,27 @@ inline bool same_taps(const Taps &t) {
     return true;
 }
 
+// Dense filters: the first compile-time tap class of the list whose window,
+// mode and taps match (bit-exactly) the call, else runtime taps.
+template <int K, int A, int MODE, class F, class... More>
+int launch_named(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                 const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs) {
+    if constexpr (F::kK == K && F::kA == A && F::kMode == MODE) {
+        if (same_taps<F, K * K>(taps))
+            return launch_wave<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
+    }
+    if constexpr (sizeof...(More) > 0)
+        return launch_named<K, A, MODE, More...>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
+    else
+        return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
+}
+
 template <int K, int A, int MODE>
 int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                  const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs = edge::RowSrc{}) {
-    if constexpr (K == 2 && A == 0 && MODE == MPX_CONV_MAG2) {
-        if (same_taps<edge::RobertsTaps, 4>(taps))
-            return launch_wave<K, A, MODE, true, edge::RobertsTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
-    }
-    if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
-        if (same_taps<edge::Sobel5Taps, 25>(taps))
-            return launch_wave<K, A, MODE, true, edge::Sobel5Taps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
-    }
-    return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
+    return launch_named<K, A, MODE, edge::RobertsTaps, edge::Sobel3Taps, edge::Prewitt3Taps, edge::Scharr3Taps,
+                        edge::Laplace3Taps, edge::Sharpen3Taps, edge::Sobel5Taps, edge::Log5Taps>(
+        in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
 }
 
 // 16-B-lane separable kernel (conv_wave4_kernel, tuning variant only): 248
@@ -147,21 +161,24 @@ inline bool same_sep_taps(const Taps &t, bool two) {
 
 // Separable filters (MPX_CONV_SEP): the wave kernel keeps a ring of per-row
 // horizontal sums instead of the K x K window. Their K-1 warm-up rows per
-// segment cost a whole horizontal pass each, so segments are longer: sized
-// for one resident round (launch_wave, seg <= 0).
-inline constexpr int kSepSegRows = 0;  // auto (launch_wave)
+// segment cost a whole horizontal pass each, so the two-filter (MAG2)
+// segments are longer: sized for one resident round (launch_wave, seg <= 0).
 template <int K, int A, int MODE>
 int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs = edge::RowSrc{}) {
+    // segment rows: two-filter magnitudes one resident round (auto), the
+    // lighter single-filter passes short segments (MI355X 4096^2, named_taps_ab:
+    // sobel5 auto 24.7 us vs 26.1 at 8; gauss5 8 rows 23.4 us vs 25.1 auto)
+    constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
-            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
+            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
         if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
-            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
+            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
     }
-    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSepSegRows, 1, rs);
+    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
 }
 
 

@@ -58,6 +58,18 @@ def test_conv_matches_cpu_exact_and_torch(gpu, filt, hw):
     assert torch.equal(g[..., 3], img[..., 3])
 
 
+@pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "sharpen3", "sobel5_dense",
+                                  "log5"])
+def test_conv_named_taps_equal_runtime_taps(gpu, filt):
+    # named filters run compile-time tap classes; -0.0 in place of the zero taps
+    # defeats the bit-exact match, so the same operator runs with runtime taps
+    f = ops.get_filter(filt)
+    nz = lambda t: tuple(-0.0 if v == 0.0 else v for v in t)  # noqa: E731
+    rt = ops.Filter(filt + "_rt", f.k, f.anchor, f.mode, nz(f.wx), nz(f.wy))
+    img = rand_img(131, 390, seed=5).to(gpu)
+    assert torch.equal(ops.conv(img, f).cpu(), ops.conv(img, rt).cpu())
+
+
 def test_conv_roberts_equals_roberts_kernel(gpu):
     img = rand_img(333, 517, seed=3)
     a = ops.conv(img.to(gpu), "roberts").cpu()
