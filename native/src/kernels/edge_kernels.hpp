@@ -662,83 +662,92 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // in whole groups of D (ring slots are then compile-time constants) with no
     // branch around any memory operation; output rows past the segment end are
     // computed and dropped by the store's bounds check.
-    const int ngroups = (ye - ys + D - 1) / D;
-    for (int g = 0; g < ngroups; ++g) {
+    auto row_step = [&](int g, int v) {
+        const int u = (K - 1 + v) % K;      // window slot of the newest row
+        const int q = (K - 1 + v) % D;      // its prefetch slot
+        const int i = K - 1 + g * D + v;    // its input row index
+        const uint2 px = fix_pair(pre[q]);
+        pre[q] = load_row(i + D);
+        consume(u, px);
+        const int y = ys + g * D + v;       // output row completed by row i
+        // both output columns at once: packed FMAs over the (w[dx], w[dx+1]) pairs
+        f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
+        if constexpr (SEP) {
+            gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[(u + 1 + dy) % K]; });
+            const float sx = sep_scale<F, K, false>(taps);
+            gx = gx * f2_t{sx, sx};
+            if constexpr (TWO) {
+                gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[(u + 1 + dy) % K]; });
+                const float sy = sep_scale<F, K, true>(taps);
+                gy = gy * f2_t{sy, sy};
+            }
+        } else {
+            bool sx = false, sy = false;
+#pragma unroll
+            for (int dy = 0; dy < K; ++dy) {
+                const int r = (u + 1 + dy) % K;
+#pragma unroll
+                for (int dx = 0; dx < K; ++dx) {
+                    const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
+                    tap_step<F::kConst>(gx, sx, tap_x<F>(taps, dy * K + dx), pv);
+                    if constexpr (TWO) tap_step<F::kConst>(gy, sy, tap_y<F>(taps, dy * K + dx), pv);
+                }
+            }
+        }
+        uint32_t g0, g1;
+        if constexpr (TWO) {
+            const f2_t sq = gx * gx + gy * gy;  // v_pk_mul x2, v_pk_add: no contraction (-ffp-contract=off)
+            if constexpr (FAST) {
+                mag2_to_gray(sq.x, sq.y, g0, g1);
+            } else {
+                g0 = mag_to_gray<false>(sq.x);
+                g1 = mag_to_gray<false>(sq.y);
+            }
+        } else {
+            g0 = finish_gray<MODE, FAST>(gx.x, 0.0f);
+            g1 = finish_gray<MODE, FAST>(gx.y, 0.0f);
+        }
+        // (g, g, g, alpha): one v_perm_b32 per pixel — selector bytes 0-2
+        // take g's low byte (g <= 255), byte 3 takes the source pixel's
+        // alpha (selector 7 = byte 3 of the first operand); no alpha mask
+        const uint32_t v0 = __builtin_amdgcn_perm(alp0[(u + 1 + A) % K], g0, 0x07000000u);
+        const uint32_t v1 = __builtin_amdgcn_perm(alp1[(u + 1 + A) % K], g1, 0x07000000u);
+        // Branch-free stores: a buffer descriptor spanning exactly this
+        // output row; lanes (or padded rows) with nothing to store get an
+        // out-of-range offset and the hardware bounds check drops them.
+        // Stores under a branch would make the outstanding-op count
+        // unknowable to hipcc and cost a vmcnt(0) drain of the ring.
+        // rows past the segment get a zero-length descriptor (scalar select),
+        // lanes with nothing to store a constant out-of-range offset
+        const bool row_ok = y < ye;
+        const int yc = row_ok ? y : ys;
+        const __amdgpu_buffer_rsrc_t orow =
+            __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
+        constexpr int kDrop = 0x7ffffff0;
+        if constexpr (VEC) {
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t pv = {v0, v1};
+            __builtin_amdgcn_raw_buffer_store_b64(pv, orow, st0 ? ox * 4 : kDrop, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(v0, orow, st0 ? ox * 4 : kDrop, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(v1, orow, st1 ? ox * 4 + 4 : kDrop, 0, 0);
+        }
+    };
+    // whole groups with no branch between the rows (a branch there costs the
+    // wait counts their precision), then the segment's last 1 .. D-1 rows with
+    // a wave-uniform exit: rows past the segment are never computed
+    const int nrows = ye - ys;
+    const int nfull = nrows / D;
+    for (int g = 0; g < nfull; ++g) {
+#pragma unroll
+        for (int v = 0; v < D; ++v) row_step(g, v);
+    }
+    const int rem = nrows - nfull * D;
+    if (rem > 0) {
 #pragma unroll
         for (int v = 0; v < D; ++v) {
-            const int u = (K - 1 + v) % K;      // window slot of the newest row
-            const int q = (K - 1 + v) % D;      // its prefetch slot
-            const int i = K - 1 + g * D + v;    // its input row index
-            // last group of a segment that is not a multiple of D: leave once
-            // the segment is done (wave-uniform scalar exit, no memory op skipped
-            // that a later wait would count) instead of computing dead rows
-            if (g * D + v >= ye - ys) break;
-            const uint2 px = fix_pair(pre[q]);
-            pre[q] = load_row(i + D);
-            consume(u, px);
-            const int y = ys + g * D + v;       // output row completed by row i
-            // both output columns at once: packed FMAs over the (w[dx], w[dx+1]) pairs
-            f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
-            if constexpr (SEP) {
-                gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[(u + 1 + dy) % K]; });
-                const float sx = sep_scale<F, K, false>(taps);
-                gx = gx * f2_t{sx, sx};
-                if constexpr (TWO) {
-                    gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[(u + 1 + dy) % K]; });
-                    const float sy = sep_scale<F, K, true>(taps);
-                    gy = gy * f2_t{sy, sy};
-                }
-            } else {
-                bool sx = false, sy = false;
-#pragma unroll
-                for (int dy = 0; dy < K; ++dy) {
-                    const int r = (u + 1 + dy) % K;
-#pragma unroll
-                    for (int dx = 0; dx < K; ++dx) {
-                        const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
-                        tap_step<F::kConst>(gx, sx, tap_x<F>(taps, dy * K + dx), pv);
-                        if constexpr (TWO) tap_step<F::kConst>(gy, sy, tap_y<F>(taps, dy * K + dx), pv);
-                    }
-                }
-            }
-            uint32_t g0, g1;
-            if constexpr (TWO) {
-                const f2_t sq = gx * gx + gy * gy;  // v_pk_mul x2, v_pk_add: no contraction (-ffp-contract=off)
-                if constexpr (FAST) {
-                    mag2_to_gray(sq.x, sq.y, g0, g1);
-                } else {
-                    g0 = mag_to_gray<false>(sq.x);
-                    g1 = mag_to_gray<false>(sq.y);
-                }
-            } else {
-                g0 = finish_gray<MODE, FAST>(gx.x, 0.0f);
-                g1 = finish_gray<MODE, FAST>(gx.y, 0.0f);
-            }
-            // (g, g, g, alpha): one v_perm_b32 per pixel — selector bytes 0-2
-            // take g's low byte (g <= 255), byte 3 takes the source pixel's
-            // alpha (selector 7 = byte 3 of the first operand); no alpha mask
-            const uint32_t v0 = __builtin_amdgcn_perm(alp0[(u + 1 + A) % K], g0, 0x07000000u);
-            const uint32_t v1 = __builtin_amdgcn_perm(alp1[(u + 1 + A) % K], g1, 0x07000000u);
-            // Branch-free stores: a buffer descriptor spanning exactly this
-            // output row; lanes (or padded rows) with nothing to store get an
-            // out-of-range offset and the hardware bounds check drops them.
-            // Stores under a branch would make the outstanding-op count
-            // unknowable to hipcc and cost a vmcnt(0) drain of the ring.
-            // rows past the segment get a zero-length descriptor (scalar select),
-            // lanes with nothing to store a constant out-of-range offset
-            const bool row_ok = y < ye;
-            const int yc = row_ok ? y : ys;
-            const __amdgpu_buffer_rsrc_t orow =
-                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
-            constexpr int kDrop = 0x7ffffff0;
-            if constexpr (VEC) {
-                typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-                const u32x2_t pv = {v0, v1};
-                __builtin_amdgcn_raw_buffer_store_b64(pv, orow, st0 ? ox * 4 : kDrop, 0, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b32(v0, orow, st0 ? ox * 4 : kDrop, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(v1, orow, st1 ? ox * 4 + 4 : kDrop, 0, 0);
-            }
+            if (v >= rem) break;
+            row_step(nfull, v);
         }
     }
 }

@@ -166,7 +166,7 @@ __device__ __forceinline__ T dpp_shift(T v, int ctrl) {
     }
 }
 
-template <typename T, int AUX = 0, bool LNT = false>
+template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true>
 __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
                                                           int nwaves, T *__restrict__ resid) {
@@ -235,14 +235,30 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
         using I4 = std::integral_constant<int, 4>;
-        // straight-line groups of 5 rows; the last group's surplus rows are
-        // computed on clamped data and dropped by the buffer store
-        for (int i = i0; i < i1; i += 5) {
+        // straight-line groups of 5 rows with no branch inside a group (a branch
+        // between the steps costs the wait counts their precision: 10-rows-per-
+        // wave sweeps measured 9% slower with per-step exits), then the 1-4 tail
+        // rows; TAIL_EXIT = false (tuning variant) instead runs the tail as a
+        // whole group, computing the surplus rows on clamped data and dropping
+        // them at the buffer store
+        int i = i0;
+        const int iend = TAIL_EXIT ? i0 + (i1 - i0) / 5 * 5 : i1;
+        for (; i < iend; i += 5) {
             step(I0{}, i);
             step(I1{}, i);
             step(I2{}, i);
             step(I3{}, i);
             step(I4{}, i);
+        }
+        if (TAIL_EXIT && i < i1) {
+            step(I0{}, i);
+            if (i + 1 < i1) {
+                step(I1{}, i);
+                if (i + 2 < i1) {
+                    step(I2{}, i);
+                    if (i + 3 < i1) step(I3{}, i);
+                }
+            }
         }
     }
     if (resid) {
@@ -265,13 +281,14 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
     if ((pitch % NV == 0) && (cols % NV == 0) && aligned16(u) && aligned16(un)) {
         const int strips = (cols / NV + kStripVec - 1) / kStripVec;
         const int rows = r1 - r0;
-        // 4 rows per wave (tools/jbench.py, profiles/jacobi.md: 16384^2 fp64
-        // R4 781 us / R16 818 / R64 913 — many short waves hide HBM latency
+        // 5 rows per wave = one straight-line group (tools/jbench.py,
+        // profiles/jacobi.md: 16384^2 fp64 R5 756 us / R4 769 / R8 763 / R16 795
+        // / R64 910; fp32 R5 370 / R4 402) — many short waves hide HBM latency
         // better than amortising the two halo rows, which neighbouring waves
-        // re-read from L2); stores nontemporal (aux NT): the next sweep reads
+        // re-read from L2; stores nontemporal (aux NT): the next sweep reads
         // u_new from HBM anyway, and keeping it out of L2 leaves L2 to those
         // shared halo rows
-        int R = 4;
+        int R = 5;
         while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
         hipLaunchKernelGGL((jacobi_wave_kernel<T, 2>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
@@ -313,7 +330,8 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
                                   int R, int aux, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(u && un && cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0 && R >= 1, "bad arguments");
-    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6, "aux must be 0, 2 or 6 (2 + non-temporal loads)");
+    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6 || aux == 10,
+                  "aux must be 0, 2, 6 (2 + non-temporal loads) or 10 (2 without the tail exit)");
     const int NV = fp64 ? 2 : 4;
     MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un), "needs the vector layout");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
@@ -326,13 +344,17 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
 #define MPX_JVN(T)                                                                                             \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, true>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
                        strips, R, nwaves, (T *)resid)
+#define MPX_JVX(T)                                                                                             \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, false>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, \
+                       r1, strips, R, nwaves, (T *)resid)
     if (fp64) {
-        if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
+        if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
     } else {
-        if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
+        if (aux == 10) MPX_JVX(float); else if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
     }
 #undef MPX_JV
 #undef MPX_JVN
+#undef MPX_JVX
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }

@@ -25,8 +25,8 @@ def main():
         res_t = torch.zeros(1, dtype=dt, device=dev)
         var = {"production": lambda: ops.jacobi_sweep(u, un, 1, n + 1),
                "production+residual": lambda: (res_t.zero_(), ops.jacobi_sweep(u, un, 1, n + 1, res_t))}
-        for R in (4, 8, 16, 32, 64):
-            for aux in (2, 6):
+        for R in (3, 4, 5, 8, 10, 16, 64):
+            for aux in (2, 10):
                 var[f"R{R}/aux{aux}"] = (lambda R=R, aux=aux: _native.check(L.mpx_jacobi_variant(
                     u.data_ptr(), un.data_ptr(), n, n, 1, n + 1, None, int(dt == torch.float64), R, aux, 0)))
         res = {k: [] for k in var}
