@@ -35,6 +35,7 @@ def main():
     p.add_argument("--size", type=int, default=4096)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--only", default="", help="run only the variants whose name contains this string")
     args = p.parse_args()
     L = _native.lib()
     dev = torch.device("cuda:0")
@@ -90,8 +91,8 @@ def main():
         variants[f"roberts/loads-{nm}"] = (
             (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 2, 7, 0, p2, 1,
                                                             rwx, rwy, 0))), rref)
-    for pf in (8,):  # deeper prefetch ring
-        for seg in (0,):
+    for pf in (4, 8, 12):  # prefetch ring depth (D = 5 / 10 / 15 rows)
+        for seg in (0, 16, 24, 32, 40):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
                 (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg,
                                                                          pf, 1, swx, swy, 0))), sref)
@@ -108,6 +109,8 @@ def main():
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(img, out, geometry=g)), rob_ref)
 
+    if args.only:
+        variants = {k: v for k, v in variants.items() if args.only in k}
     # correctness first
     cpu_img = img.cpu()
     for fname in ("sobel5_dense", "roberts"):
