@@ -247,7 +247,9 @@ def test_classify_single_point_class_nan(gpu):
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-@pytest.mark.parametrize("shape", [(3, 3), (10, 7), (66, 130), (257, 1001)])
+# (2413, 4096) / (4822, 4096): enough waves for the production 5 rows per wave
+# (fp64 / fp32), with a 3- / 2-row tail in the last wave of each strip
+@pytest.mark.parametrize("shape", [(3, 3), (10, 7), (66, 130), (257, 1001), (2413, 4096), (4822, 4096)])
 def test_jacobi_sweep(gpu, dtype, shape):
     rows, cols = shape
     g = torch.Generator().manual_seed(rows)
