@@ -2,7 +2,6 @@
 """Summarise gpurun_out/harness_cmp (tools/harness_compare.sh) as markdown:
 median kernel ms per (bucket/n, timing, geometry), next to BASELINE.md."""
 import glob
-import json
 import os
 import sys
 

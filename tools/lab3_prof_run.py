@@ -1,10 +1,10 @@
 """Profiling driver: each lab3 path once at nc=32 on 8192^2 (after warm-up)."""
+import os
 import sys
 
-import numpy as np
 import torch
 
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cuda_mpi_openmp_amd import ops  # noqa: E402
 from cuda_mpi_openmp_amd.models.classifier import class_points_for  # noqa: E402
 
