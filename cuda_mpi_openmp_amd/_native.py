@@ -22,7 +22,8 @@ import torch  # noqa: F401  (must be loaded before libmpx; see module docstring)
 
 _PKG_DIR = Path(__file__).resolve().parent
 REPO_ROOT = _PKG_DIR.parent
-LIB_PATH = _PKG_DIR / "_lib" / "libmpx.so"
+# MPX_LIB_PATH: load another build of libmpx (kernel A/B runs: tools/*_ab.py)
+LIB_PATH = Path(os.environ["MPX_LIB_PATH"]) if os.environ.get("MPX_LIB_PATH") else _PKG_DIR / "_lib" / "libmpx.so"
 
 _lib = None
 _lock = threading.Lock()
