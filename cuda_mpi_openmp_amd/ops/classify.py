@@ -12,7 +12,7 @@ import torch
 from .. import _native
 from .edge import check_image
 
-PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3}
+PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3, "mfma64": 4}
 PATH_NAMES = {v: k for k, v in PATHS.items()}
 MAX_CLASSES = 32
 
@@ -46,9 +46,10 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``direct`` — the reference fp64 FMA chain;
       * ``fast``   — fp32 packed-VALU distances;
       * ``mfma``   — fp32 MFMA distance GEMM (v_mfma_f32_32x32x2f32);
+      * ``mfma64`` — fp64 MFMA distance GEMM (v_mfma_f64_16x16x4_f64);
       * ``auto``   — ``fast`` (measured fastest at every nc on MI355X: the f32
         MFMA shares the VALU's fp32 datapath on gfx950).
-    The fp32 paths classify a pixel only when its best/second margin exceeds a
+    The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes
     (statistics for which no bound can be proven run ``direct``). With

@@ -6,7 +6,7 @@
 //     stdout "HIP execution time: <X ms>\n" (reference lab3/src/to_plot.cu:76-117,174)
 //   submission personality (-DMPX_SUBMISSION, "hip_exe"): no geometry, no output line.
 // Output: the input image with alpha = class index (255 when every distance is NaN).
-// MPX_LAB3_PATH = direct (default, geometry honoured) | fast | mfma | auto.
+// MPX_LAB3_PATH = direct (default, geometry honoured) | fast | mfma | mfma64 | auto.
 // MPX_NGPUS=N shards the pixels over N devices (harness --n_gpus N).
 #include <cstring>
 #include <memory>
@@ -33,6 +33,7 @@ int main() {
         if (!std::strcmp(e, "mfma")) path = MPX_CLS_MFMA;
         else if (!std::strcmp(e, "auto")) path = MPX_CLS_AUTO;
         else if (!std::strcmp(e, "fast")) path = MPX_CLS_FAST;
+        else if (!std::strcmp(e, "mfma64")) path = MPX_CLS_MFMA64;
     }
     std::string in_path, out_path;
     if (!in.next_token(in_path) || !in.next_token(out_path)) {

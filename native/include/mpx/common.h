@@ -50,7 +50,8 @@ enum mpx_classify_path {
     MPX_CLS_DIRECT = 0, /* fp64 (p-mu)^T A (p-mu), reference-exact                   */
     MPX_CLS_MFMA = 1,   /* fp32 MFMA distance GEMM, proven margin + exact fallback  */
     MPX_CLS_AUTO = 2,   /* FAST, or DIRECT when the fp32 margin cannot be proven    */
-    MPX_CLS_FAST = 3    /* fp32 packed-VALU distances, proven margin + fallback     */
+    MPX_CLS_FAST = 3,   /* fp32 packed-VALU distances, proven margin + fallback     */
+    MPX_CLS_MFMA64 = 4  /* fp64 MFMA distance GEMM, proven margin + exact fallback  */
 };
 
 #ifdef __cplusplus

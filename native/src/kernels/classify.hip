@@ -302,18 +302,152 @@ __global__ __launch_bounds__(256) void classify_mfma32_kernel(uint32_t *__restri
 }
 
 // ---------------------------------------------------------------------------
+// MFMA64: the distance GEMM in fp64 on v_mfma_f64_16x16x4_f64.
+//   D[class][pixel] = sum_k W[class][k] * PHI[k][pixel], K = 12 (10 features,
+//   k = 10, 11 carry zero weights) = 3 MFMAs per 16 classes x 16 pixels.
+//   A (W):   lane l holds W[class = 16 T + (l & 15)][k = 4t + (l >> 4)]
+//   B (PHI): lane l holds phi_{4t + (l >> 4)}(pixel l & 15)
+//   D:       lane l, reg r holds class 16 T + (l >> 4) + 4 r, pixel l & 15
+//            (the f64 C/D map, not the f32 one)
+// Every feature is one integer product x_a x_b of the centred bytes
+// {r, g, b, 1}: lane group g = l >> 4 picks the byte pair of its k once
+// (kPair), so the feature build is branch-free and exact. A wave takes 64-pixel
+// chunks: lane l loads the 16 B at pixel 4 (l & 15) (all four lane groups load
+// the same bytes) and group m = 0..3 uses pixel 4 (l & 15) + m as column
+// l & 15. The four lane groups' top-2 lists are merged with two xor shuffles.
+// fp64 keeps the bound ~2^29 x tighter than fp32, so the exact fallback is
+// taken only on genuine near-ties; NT = 16-class tiles (1 for nc <= 16, else 2).
+// ---------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+struct Fast64Params {
+    double w[MPX_MAX_CLASSES][kFeat];  // padded classes: 0 ... 0, 1e300
+    double T2;                         // decision margin 2 * max_c tol_c
+};
+
+// byte pair (a, b) of feature k: phi_k = (byte_a - 128) (byte_b - 128), byte 3 = 129 (the constant 1)
+__constant__ const uint8_t kPair[12][2] = {{0, 0}, {1, 1}, {2, 2}, {0, 1}, {0, 2}, {1, 2},
+                                           {0, 3}, {1, 3}, {2, 3}, {3, 3}, {3, 3}, {3, 3}};
+
+// fp64 keys: the low 5 mantissa bits carry the class (a relative change of at
+// most 2^-47, inside the decision slack), so the running top-2 is three f64
+// min/max per entry and the class comes back with the winning value.
+__device__ __forceinline__ double tag_f64(double d, uint32_t cls) {
+    const uint64_t u = (uint64_t)__double_as_longlong(d);
+    return __longlong_as_double((long long)((u & ~31ull) | cls));
+}
+
+__device__ __forceinline__ void rank_f64(double k, double &B, double &S) {
+    S = fmin(S, fmax(B, k));
+    B = fmin(B, k);
+}
+
+// (B, S) of this lane and of its partner lane across a permlane swap: the
+// swap returns {own, partner} in an order that differs between the two
+// lanes, and the merge is symmetric, so both end with the merged pair
+template <bool X32>
+__device__ __forceinline__ void merge_lanes_f64(double &B, double &S) {
+    const uint64_t ub = (uint64_t)__double_as_longlong(B), us = (uint64_t)__double_as_longlong(S);
+    const uint32_t w[4] = {(uint32_t)ub, (uint32_t)(ub >> 32), (uint32_t)us, (uint32_t)(us >> 32)};
+    uint32_t x[4], y[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const auto r = X32 ? __builtin_amdgcn_permlane32_swap(w[i], w[i], false, false)
+                           : __builtin_amdgcn_permlane16_swap(w[i], w[i], false, false);
+        x[i] = r[0];
+        y[i] = r[1];
+    }
+    auto dbl = [](uint32_t lo, uint32_t hi) { return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)); };
+    const double B0 = dbl(x[0], x[1]), S0 = dbl(x[2], x[3]), B1 = dbl(y[0], y[1]), S1 = dbl(y[2], y[3]);
+    S = fmin(fmax(B0, B1), fmin(S0, S1));
+    B = fmin(B0, B1);
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void classify_mfma64_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
+                                                              ClassParams cp, Fast64Params fp, uint32_t *amb) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int col = lane & 15;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    double a[NT][3];
+    uint32_t sa[3], sb[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int k = 4 * t + g;
+#pragma unroll
+        for (int T = 0; T < NT; ++T) a[T][t] = k < kFeat ? fp.w[16 * T + col][k] : 0.0;
+        sa[t] = 8u * kPair[k][0];
+        sb[t] = 8u * kPair[k][1];
+    }
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    int64_t ch = wave;
+    uint4 qn = ch < nchunks ? v[ch * 16 + col] : uint4{};
+    for (; ch < nchunks; ch += nwaves) {
+        const uint4 q = qn;
+        if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 16 + col];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        double vb[4], vs[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t p = (px[m] & 0x00ffffffu) | (129u << 24);
+            double phi[3];
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int x = (int)__builtin_amdgcn_ubfe(p, sa[t], 8) - 128;
+                const int y = (int)__builtin_amdgcn_ubfe(p, sb[t], 8) - 128;
+                phi[t] = (double)__mul24(x, y);
+            }
+            vb[m] = 1.7976931348623157e308;  // DBL_MAX: low 5 bits already 31
+            vs[m] = 1.7976931348623157e308;
+#pragma unroll
+            for (int T = 0; T < NT; ++T) {
+                f64x4 c = {};
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T][0], phi[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T][1], phi[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(a[T][2], phi[2], c, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (16 * T + 4 * r < nc)  // wave-uniform: skip rows holding only padded classes
+                        rank_f64(tag_f64(c[r], (uint32_t)(16 * T + g + 4 * r)), vb[m], vs[m]);
+            }
+            merge_lanes_f64<false>(vb[m], vs[m]);
+            merge_lanes_f64<true>(vb[m], vs[m]);
+        }
+        if (g == 0) {
+            uint4 o;
+            uint32_t *op = &o.x;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                // proven: the reference chain ranks the same class first (see
+                // build_fast64); 2^-46 covers both keys' tags and the subtraction
+                if (__builtin_expect((vs[m] - vb[m]) > fma(fabs(vs[m]) + fabs(vb[m]), 0x1p-46, fp.T2), 1)) {
+                    const uint32_t cls = (uint32_t)__double_as_longlong(vb[m]) & 31u;
+                    op[m] = (px[m] & 0x00ffffffu) | (cls << 24);
+                } else {
+                    if (amb) atomicAdd(amb, 1u);
+                    op[m] = classify_direct(px[m], nc, cp);
+                }
+            }
+            v[ch * 16 + col] = o;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host: expanded fp32 weights and the rigorous decision margin.
 // ---------------------------------------------------------------------------
 typedef long double ld;
 
-// false when the fp32 decision cannot be proven (non-finite statistics, a
-// symmetrised A that is not positive definite, or magnitudes near fp32 range)
-bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
-    const ld u32 = std::ldexp((ld)1, -24), u64 = std::ldexp((ld)1, -53);
-    const ld g10 = 10 * u32 / (1 - 10 * u32);
-    // |q_i q_j| <= 128^2, |q_i| <= 128 for q = p - 128, p in [0, 255]^3
-    static const ld phimax[kFeat] = {16384, 16384, 16384, 16384, 16384, 16384, 128, 128, 128, 1};
-    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
+// |q_i q_j| <= 128^2, |q_i| <= 128 for q = p - 128, p in [0, 255]^3
+constexpr ld kPhiMax[kFeat] = {16384, 16384, 16384, 16384, 16384, 16384, 128, 128, 128, 1};
+
+// Expanded weights w[c][k] of the centred quadratic form, the reference
+// chain's own error bound refb[c] and the indefiniteness slack psd[c]. False
+// for non-finite statistics or a symmetrised A that is not positive definite.
+bool expand_classes(int nc, const double *mu, const double *inv, ld (*w)[kFeat], ld *refb, ld *psd) {
+    const ld u64 = std::ldexp((ld)1, -53);
     for (int c = 0; c < nc; ++c) {
         const double *A = inv + 9 * c;
         const double *mraw = mu + 3 * c;
@@ -360,6 +494,17 @@ bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
         // a slightly indefinite S hidden by long-double rounding: Q >= -1e-15 |S| |d|^2
         psd[c] = 1e-15L * sabs * (dmax[0] * dmax[0] + dmax[1] * dmax[1] + dmax[2] * dmax[2]);
     }
+    return true;
+}
+
+// false when the fp32 decision cannot be proven (non-finite statistics, a
+// symmetrised A that is not positive definite, or magnitudes near fp32 range)
+bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
+    const ld u32 = std::ldexp((ld)1, -24);
+    const ld g10 = 10 * u32 / (1 - 10 * u32);
+    const ld *phimax = kPhiMax;
+    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
+    if (!expand_classes(nc, mu, inv, w, refb, psd)) return false;
     auto tol = [&](int c, ld bias, float *out) -> ld {
         ld mag = 0, rep = 0, ev = 0;
         for (int k = 0; k < kFeat; ++k) {
@@ -392,6 +537,40 @@ bool build_fast(int nc, const double *mu, const double *inv, FastParams &fp) {
     return true;
 }
 
+// fp64 weights for MFMA64. The f64 MFMA's summation order and internal
+// rounding are not specified, so its error is bounded as any 12-term sum with
+// unit roundoff 2^-52 (twice RNE's, covering a truncating adder):
+// gamma_12 sum_k |w_k| phimax_k, plus the weight rounding and the reference
+// chain's error; a pixel is decided in fp64 only beyond 2 max_c tol_c.
+bool build_fast64(int nc, const double *mu, const double *inv, Fast64Params &fp) {
+    const ld u = std::ldexp((ld)1, -52);
+    const ld g12 = 12 * u / (1 - 12 * u);
+    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
+    if (!expand_classes(nc, mu, inv, w, refb, psd)) return false;
+    ld tmax = 0;
+    for (int c = 0; c < nc; ++c) {
+        ld ev = 0, rep = 0, mag = 0;
+        for (int k = 0; k < kFeat; ++k) {
+            const double f = (double)w[c][k];
+            fp.w[c][k] = f;
+            ev += std::fabs((ld)f) * kPhiMax[k];
+            rep += std::fabs((ld)f - w[c][k]) * kPhiMax[k];
+            mag += std::fabs(w[c][k]) * kPhiMax[k];
+        }
+        if (!(mag < 1e300L)) return false;
+        // long-double expansion slack: ~20 operations at 2^-64 each
+        const ld t = (g12 * ev + rep + 1e-17L * mag + refb[c]) * 1.001L + 1e-300L;
+        tmax = std::fmax(tmax, t);
+    }
+    for (int c = nc; c < MPX_MAX_CLASSES; ++c)
+        for (int k = 0; k < kFeat; ++k) fp.w[c][k] = (k == 9) ? 1e300 : 0.0;
+    const ld t2x = 2 * tmax * (1 + std::ldexp((ld)1, -40));
+    double t2 = (double)t2x;
+    if ((ld)t2 < t2x) t2 = std::nextafter(t2, INFINITY);
+    fp.T2 = t2;
+    return true;
+}
+
 }  // namespace
 
 // AUTO: FAST32, DIRECT when the fp32 decision cannot be proven for these
@@ -413,7 +592,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
     MPX_CHECK_ARG(grid >= 0 && block >= 0 && block <= 1024, "bad launch geometry");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_FAST, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA64, "bad path");
     if (npix == 0) return MPX_OK;
     MPX_CHECK_ARG(img, "null image");
     ClassParams cp{};
@@ -421,10 +600,26 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     for (int i = 0; i < 9 * nc; ++i) cp.A[i] = inv[i];
     hipStream_t s = as_stream(stream);
     FastParams fp;
-    const bool fast_ok = path != MPX_CLS_DIRECT && aligned16(img) && build_fast(nc, mu, inv, fp);
+    Fast64Params fp64;
+    const bool fast_ok = path != MPX_CLS_DIRECT && aligned16(img) &&
+                         (path == MPX_CLS_MFMA64 ? build_fast64(nc, mu, inv, fp64) : build_fast(nc, mu, inv, fp));
     const int chosen = classify_choose(nc, path, fast_ok);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
-    if (chosen == MPX_CLS_MFMA) {
+    if (chosen == MPX_CLS_MFMA64) {
+        const int64_t nchunks = npix / 64;
+        if (nchunks > 0) {
+            const int64_t blocks = (nchunks + 3) / 4;
+            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            if (nc <= 16)
+                hipLaunchKernelGGL(classify_mfma64_kernel<1>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, fp64,
+                                   amb);
+            else
+                hipLaunchKernelGGL(classify_mfma64_kernel<2>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, fp64,
+                                   amb);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nchunks * 64;
+        }
+    } else if (chosen == MPX_CLS_MFMA) {
         const int64_t nchunks = npix / 128;
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;
@@ -467,10 +662,17 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 int classify_plan_impl(int nc, const double *mu, const double *inv, int path, float *margin) {
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_FAST, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA64, "bad path");
     FastParams fp;
-    const bool ok = path != MPX_CLS_DIRECT && build_fast(nc, mu, inv, fp);
-    if (margin) *margin = ok ? fp.T2 : 0.0f;
+    Fast64Params fp64;
+    bool ok = false;
+    if (path == MPX_CLS_MFMA64) {
+        ok = build_fast64(nc, mu, inv, fp64);
+        if (margin) *margin = ok ? (float)fp64.T2 : 0.0f;
+    } else {
+        ok = path != MPX_CLS_DIRECT && build_fast(nc, mu, inv, fp);
+        if (margin) *margin = ok ? fp.T2 : 0.0f;
+    }
     return classify_choose(nc, path, ok);
 }
 

@@ -147,9 +147,13 @@ def test_classify_plan_routes():
     mu20, inv20 = stats(20)
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
     assert ops.classify_plan(mu20, inv20, "mfma")[0] == "mfma"
+    # fp64 GEMM: same validation, a bound ~2^29 x tighter than the fp32 one
+    path64, margin64 = ops.classify_plan(mu20, inv20, "mfma64")
+    assert path64 == "mfma64" and 0 < margin64 < ops.classify_plan(mu20, inv20, "fast")[1] * 1e-6
     # single-point class -> non-finite statistics -> only the exact chain
     mu_n, inv_n = ops.class_stats(img, [np.array([[0, 0]]), rng.integers(0, 64, (30, 2))])
     assert ops.classify_plan(mu_n, inv_n, "fast")[0] == "direct"
+    assert ops.classify_plan(mu_n, inv_n, "mfma64")[0] == "direct"
     # an indefinite form has no positive lower bound -> direct
     bad = inv.copy()
     bad[0] = np.diag([1e-3, -1e-3, 1e-3])

@@ -32,7 +32,7 @@ def main():
     if "lab3" in which:
         img = torch.randint(0, 256, (8192, 8192, 4), dtype=torch.uint8, device=dev)
         mu, inv = ops.class_stats(img.cpu(), class_points_for(8192, 8192, 16, 64, seed=16))
-        for path in ("direct", "fast", "mfma"):
+        for path in ("direct", "fast", "mfma", "mfma64"):
             for _ in range(REPS):
                 ops.classify_(img, mu, inv, path=path)
         del img
