@@ -30,9 +30,9 @@ CPU_OBJ   := $(B)/cpu_kernels.o
 LIB_OBJS  := $(HIP_OBJS) $(CORE_OBJS) $(CPU_OBJ)
 HDRS      := $(wildcard native/include/mpx/*.h native/include/mpx/*.hpp native/src/kernels/*.hpp native/src/cpu/*.h)
 
-LABS      := labs/lab1/src labs/lab2/src labs/lab3/src
-GPU_APPS  := $(foreach L,1 2 3,labs/lab$(L)/src/to_plot_hip_exe labs/lab$(L)/src/hip_exe)
-CPU_APPS  := $(foreach L,1 2 3,labs/lab$(L)/src/cpu_exe labs/lab$(L)/src/cpu_omp_exe)
+LABS      := labs/lab1/src labs/lab2/src labs/lab3/src labs/lab5/src
+GPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/to_plot_hip_exe labs/lab$(L)/src/hip_exe)
+CPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/cpu_exe labs/lab$(L)/src/cpu_omp_exe)
 MISC_APPS := labs/lab3/src/read_input_exe bin/gpu_info bin/hw1 bin/hw2 bin/mpx_mgpu
 
 .PHONY: all lib apps clean
@@ -109,7 +109,7 @@ bin/hw2: native/apps/hw2_bubble_sort.c | $(B)
 # sanitizers cover the host code paths: the CPU references, the .data / text
 # I/O and the stdin parsers shared with the GPU programs.
 SAN       := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
-SAN_APPS  := $(foreach L,1 2 3,build/san/lab$(L)_cpu_exe build/san/lab$(L)_cpu_omp_exe) build/san/lab3_read_input_exe \
+SAN_APPS  := $(foreach L,1 2 3 5,build/san/lab$(L)_cpu_exe build/san/lab$(L)_cpu_omp_exe) build/san/lab3_read_input_exe \
              build/san/hw1 build/san/hw2
 .PHONY: sanitize
 sanitize: $(SAN_APPS)

@@ -5,6 +5,7 @@ from .classify import class_stats, classify_
 from .classify import plan as classify_plan
 from .edge import ConvLauncher, conv, conv_rows, roberts
 from .filters import Filter, get_filter, list_filters
+from .sort import sort_
 from .stencil import jacobi_sweep
 from .vector import vsub
 
@@ -20,5 +21,6 @@ __all__ = [
     "get_filter",
     "list_filters",
     "jacobi_sweep",
+    "sort_",
     "vsub",
 ]

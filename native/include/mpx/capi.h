@@ -174,6 +174,11 @@ int mpx_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int
 int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r1, float *resid,
                    void *stream);
 
+/* ---------------- lab5: ascending sort (no reference program) ---------------- */
+/* In place on the device; dtype is an mpx_sort_dtype. int32/float32: bitonic network
+ * on order-preserving uint32 keys; uint8: counting sort. */
+int mpx_sort(void *data, int64_t n, int dtype, void *stream);
+
 /* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */
 int mpx_cpu_threads(void);
 void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n);
@@ -183,6 +188,7 @@ void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
                   int y_hi, int k, int anchor, int mode, const float *wx, const float *wy);
 void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv);
 double mpx_cpu_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1);
+void mpx_cpu_sort(void *data, int64_t n, int dtype);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,13 @@ enum mpx_classify_path {
     MPX_CLS_MFMA64 = 4  /* fp64 MFMA distance GEMM, proven margin + exact fallback  */
 };
 
+/* lab5 element types (binary fixtures lab5/data/{int10,float10,uchar10}). */
+enum mpx_sort_dtype {
+    MPX_SORT_I32 = 0,
+    MPX_SORT_F32 = 1, /* IEEE total order of the bit patterns (-NaN < -inf < -0 < +0 < +inf < +NaN) */
+    MPX_SORT_U8 = 2
+};
+
 #ifdef __cplusplus
 }
 #endif

@@ -277,3 +277,34 @@ int mpx_cpu_class_stats(const uint32_t *img, int w, int h, int nc, const int *np
     }
     return 0;
 }
+
+/* ---- lab5 sort: order-preserving uint32 keys (floats: IEEE total order of
+ * the bit patterns), the same key map as native/src/kernels/sort.hip ---- */
+static int cmp_u32(const void *a, const void *b) {
+    const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return (x > y) - (x < y);
+}
+
+void mpx_cpu_sort(void *data, int64_t n, int dtype) {
+    if (n < 2) return;
+    if (dtype == MPX_SORT_U8) { /* counting sort */
+        uint8_t *x = (uint8_t *)data;
+        int64_t cnt[256] = {0};
+        for (int64_t i = 0; i < n; ++i) cnt[x[i]]++;
+        int64_t o = 0;
+        for (int v = 0; v < 256; ++v)
+            for (int64_t c = 0; c < cnt[v]; ++c) x[o++] = (uint8_t)v;
+        return;
+    }
+    uint32_t *x = (uint32_t *)data;
+    const int is_float = dtype == MPX_SORT_F32;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t v = x[i];
+        x[i] = is_float ? (v ^ ((uint32_t)((int32_t)v >> 31) | 0x80000000u)) : (v ^ 0x80000000u);
+    }
+    qsort(x, (size_t)n, sizeof(uint32_t), cmp_u32);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t k = x[i];
+        x[i] = is_float ? (k ^ ((k >> 31) ? 0x80000000u : 0xffffffffu)) : (k ^ 0x80000000u);
+    }
+}

@@ -25,6 +25,8 @@ void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
                   int y_hi, int k, int anchor, int mode, const float *wx, const float *wy);
 void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv);
 double mpx_cpu_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1);
+/* lab5: ascending sort in place, same order as mpx_sort (dtype: enum mpx_sort_dtype). */
+void mpx_cpu_sort(void *data, int64_t n, int dtype);
 
 /* lab3 host statistics H1 (reference lab3/src/main.cu:102-152). Returns 0, or
  * -1 when a coordinate lies outside the image. */

@@ -1,0 +1,215 @@
+// lab5: sort of the binary arrays in the reference's lab5/data fixtures
+// (int10, float10, uchar10: int32 n, then n elements). The reference ships the
+// inputs only — no program consumes them — so the contract here is
+// ours: ascending order, in place on the device.
+//
+// MI355X design
+//   * int32 and float32 become order-preserving uint32 keys in place (sign
+//     flip; floats flip every bit when negative), so one network sorts both.
+//     Float order is the IEEE total order on the bit patterns: -NaN < -inf <
+//     ... < -0 < +0 < ... < +inf < +NaN.
+//   * The network is the all-ascending bitonic form: the first step of stage k
+//     compares i with i ^ (k - 1), later steps with i ^ j, and the lower index
+//     always keeps the minimum. Elements past n act as +inf and never move, so
+//     any n sorts without padding or scratch.
+//   * Stages up to kTile (4096 keys) run entirely in LDS, 16 keys per thread,
+//     in one launch. Larger stages issue one global compare-exchange pass per
+//     step with j >= kTile; the steps j < kTile of the same stage run in one
+//     LDS launch per tile. N = 2^26 takes 105 global passes + 15 LDS passes.
+//   * uint8 uses a counting sort instead: 256 LDS histogram bins per block
+//     (one global atomic per bin and block), then every block rebuilds the
+//     exclusive prefix in LDS and writes its output range by binary search.
+#include "internal.hpp"
+
+namespace mpx {
+namespace {
+
+constexpr int kSortThreads = 256;
+constexpr int kPerThread = 16;
+constexpr int kTile = kSortThreads * kPerThread;  // 4096 keys = 16 KiB of LDS
+
+__global__ void to_keys_kernel(uint32_t *__restrict__ x, int64_t n, int is_float) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t v = x[i];
+        x[i] = is_float ? (v ^ ((uint32_t)((int32_t)v >> 31) | 0x80000000u)) : (v ^ 0x80000000u);
+    }
+}
+
+__global__ void from_keys_kernel(uint32_t *__restrict__ x, int64_t n, int is_float) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = x[i];
+        x[i] = is_float ? (k ^ ((k >> 31) ? 0x80000000u : 0xffffffffu)) : (k ^ 0x80000000u);
+    }
+}
+
+__device__ __forceinline__ void cmpx(uint32_t *s, int i, int p) {
+    const uint32_t a = s[i], b = s[p];
+    if (b < a) {
+        s[i] = b;
+        s[p] = a;
+    }
+}
+
+// one LDS pass over a tile: either the whole network up to kTile (full = 1),
+// or the steps j = kTile/2 .. 1 of a larger stage (full = 0)
+__global__ __launch_bounds__(kSortThreads) void sort_tile_kernel(uint32_t *__restrict__ x, int64_t n, int full) {
+    __shared__ uint32_t s[kTile];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+        const int i = e * kSortThreads + t;
+        s[i] = base + i < n ? x[base + i] : 0xffffffffu;
+    }
+    __syncthreads();
+    // each of the kTile/2 compare pairs per step is owned by one (thread, e)
+    if (full) {
+        for (int k = 2; k <= kTile; k <<= 1) {
+            for (int e = 0; e < kPerThread / 2; ++e) {  // flip step of stage k
+                const int q = e * kSortThreads + t;
+                const int h = k >> 1;
+                const int i = (q / h) * k + (q % h);
+                cmpx(s, i, (i / k) * k + (k - 1) - (q % h));
+            }
+            __syncthreads();
+            for (int j = k >> 2; j >= 1; j >>= 1) {
+                for (int e = 0; e < kPerThread / 2; ++e) {
+                    const int q = e * kSortThreads + t;
+                    const int i = (q / j) * 2 * j + (q % j);
+                    cmpx(s, i, i + j);
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        for (int j = kTile >> 1; j >= 1; j >>= 1) {
+            for (int e = 0; e < kPerThread / 2; ++e) {
+                const int q = e * kSortThreads + t;
+                const int i = (q / j) * 2 * j + (q % j);
+                cmpx(s, i, i + j);
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+        const int i = e * kSortThreads + t;
+        if (base + i < n) x[base + i] = s[i];
+    }
+}
+
+// one global compare-exchange step of stage k: flip (j == k/2, first step) or half-cleaner
+__global__ void sort_step_kernel(uint32_t *__restrict__ x, int64_t n, int64_t npairs, int64_t k, int64_t j,
+                                 int flip) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs; q += stride) {
+        const int64_t i = (q / j) * 2 * j + (q % j);
+        const int64_t p = flip ? (i / k) * k + (k - 1) - (q % j) : i + j;
+        if (p >= n) continue;  // partner past the end is +inf: no exchange
+        const uint32_t a = x[i], b = x[p];
+        if (b < a) {
+            x[i] = b;
+            x[p] = a;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void hist_u8_kernel(const uint8_t *__restrict__ x, int64_t n,
+                                                      uint32_t *__restrict__ counts) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&h[x[i]], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, int64_t n,
+                                                      const uint32_t *__restrict__ counts) {
+    __shared__ int64_t start[257];
+    if (threadIdx.x == 0) {
+        int64_t acc = 0;
+        for (int v = 0; v < 256; ++v) {
+            start[v] = acc;
+            acc += counts[v];
+        }
+        start[256] = acc;
+    }
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += stride) {
+        int lo = 0, hi = 255;  // largest v with start[v] <= o
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (start[mid] <= o) lo = mid;
+            else hi = mid - 1;
+        }
+        x[o] = (uint8_t)lo;
+    }
+}
+
+int grid_for(int64_t work, int block) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((work + block - 1) / block, (int64_t)kNumCUs * 16));
+}
+
+int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
+    if (n < 2) return MPX_OK;
+    const int64_t tiles = (n + kTile - 1) / kTile;
+    MPX_CHECK_ARG(tiles <= INT32_MAX, "array too large");
+    hipLaunchKernelGGL(sort_tile_kernel, dim3((unsigned)tiles), dim3(kSortThreads), 0, s, x, n, 1);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    int64_t npow = kTile;
+    while (npow < n) npow <<= 1;
+    const int64_t npairs = npow / 2;
+    for (int64_t k = 2 * (int64_t)kTile; k <= npow; k <<= 1) {
+        for (int64_t j = k / 2; j >= kTile; j >>= 1) {
+            hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, j,
+                               j == k / 2 ? 1 : 0);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        }
+        hipLaunchKernelGGL(sort_tile_kernel, dim3((unsigned)tiles), dim3(kSortThreads), 0, s, x, n, 0);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    }
+    return MPX_OK;
+}
+
+}  // namespace
+
+int sort_impl(void *data, int64_t n, int dtype, void *stream) {
+    MPX_CHECK_ARG(n >= 0, "n must be >= 0");
+    MPX_CHECK_ARG(dtype == MPX_SORT_I32 || dtype == MPX_SORT_F32 || dtype == MPX_SORT_U8, "bad dtype");
+    if (n == 0) return MPX_OK;
+    MPX_CHECK_ARG(data, "null data");
+    hipStream_t s = as_stream(stream);
+    if (dtype == MPX_SORT_U8) {
+        uint32_t *counts = nullptr;
+        MPX_RETURN_IF_HIP_ERROR(hipMallocAsync(reinterpret_cast<void **>(&counts), 256 * sizeof(uint32_t), s));
+        MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(counts, 0, 256 * sizeof(uint32_t), s));
+        uint8_t *x = static_cast<uint8_t *>(data);
+        hipLaunchKernelGGL(hist_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, counts);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, counts);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        MPX_RETURN_IF_HIP_ERROR(hipFreeAsync(counts, s));
+        return MPX_OK;
+    }
+    MPX_CHECK_ARG((reinterpret_cast<uintptr_t>(data) & 3u) == 0, "int32/float32 data must be 4-byte aligned");
+    uint32_t *x = static_cast<uint32_t *>(data);
+    const int is_float = dtype == MPX_SORT_F32;
+    hipLaunchKernelGGL(to_keys_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, is_float);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    const int rc = sort_keys(x, n, s);
+    if (rc != MPX_OK) return rc;
+    hipLaunchKernelGGL(from_keys_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, is_float);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
+MPX_MODULE_ANCHOR(sort)
+
+}  // namespace mpx
+
+extern "C" int mpx_sort(void *data, int64_t n, int dtype, void *stream) { return mpx::sort_impl(data, n, dtype, stream); }

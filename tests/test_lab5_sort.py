@@ -1,0 +1,134 @@
+"""lab5: ascending sort of the reference's binary lab5/data fixtures.
+
+The reference ships only the inputs (int10, float10, uchar10) and no program,
+so parity is unpinned: the oracle is numpy's sort (and, for floats, the IEEE
+total order of the bit patterns, which numpy's sort does not define for NaN
+and -0.0). GPU results are compared byte for byte with the C reference.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from cuda_mpi_openmp_amd import ops
+from cuda_mpi_openmp_amd.ops.sort import read_fixture
+
+from .helpers import ROOT
+
+LAB5_DATA = os.path.join(ROOT, "labs", "lab5", "data")
+KINDS = {"int": (np.int32, torch.int32), "float": (np.float32, torch.float32), "uchar": (np.uint8, torch.uint8)}
+
+
+def total_order_sorted(a: np.ndarray) -> np.ndarray:
+    """Reference order: int/uint8 numerically; float32 by the IEEE total order."""
+    if a.dtype != np.float32:
+        return np.sort(a, kind="stable")
+    u = a.view(np.uint32)
+    key = np.where(u >> 31 == 1, ~u, u | np.uint32(0x80000000))
+    return a[np.argsort(key, kind="stable")]
+
+
+def random_array(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "int":
+        a = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+        if n > 4:
+            a[:4] = [-2**31, 2**31 - 1, 0, -1]
+        return a
+    if kind == "uchar":
+        return rng.integers(0, 256, n, dtype=np.int64).astype(np.uint8)
+    a = (rng.standard_normal(n) * 10.0 ** rng.integers(-30, 30, n)).astype(np.float32)
+    if n > 8:
+        a[:8] = [np.inf, -np.inf, 0.0, -0.0, np.nan, -np.nan, 1e-45, -1e-45]
+    return a
+
+
+def fixture_bytes(kind, a):
+    return np.int32(a.size).tobytes() + a.astype(KINDS[kind][0]).tobytes()
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_fixtures_parse(kind):
+    a = read_fixture(os.path.join(LAB5_DATA, kind + "10"), kind)
+    assert a.size == 10
+    expected = {"int": [0, 9, 8, 7, 6, 5, 4, 3, 2, 1], "float": [0, 9, 8, 7, 6, 5, 4, 3, 2, 1],
+                "uchar": [1, 2, 3, 1, 2, 3, 1, 2, 3, 4]}[kind]
+    assert a.tolist() == expected
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 1000, 4097])
+def test_cpu_sort_matches_total_order(kind, n):
+    a = random_array(kind, n, seed=n)
+    t = torch.from_numpy(a.copy())
+    ops.sort_(t)
+    assert t.numpy().tobytes() == total_order_sorted(a).tobytes()
+
+
+@pytest.mark.parametrize("exe", ["cpu_exe", "cpu_omp_exe"])
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_lab5_cpu_program_on_fixtures(exe, kind):
+    path = os.path.join(LAB5_DATA, kind + "10")
+    with open(path, "rb") as f:
+        r = subprocess.run([os.path.join(ROOT, "labs/lab5/src", exe), kind], stdin=f, capture_output=True,
+                           timeout=60)
+    assert r.returncode == 0, r.stderr
+    head, _, payload = r.stdout.partition(b"\n")
+    assert head.startswith(b"CPU execution time: <")
+    a = read_fixture(path, kind)
+    assert payload == np.sort(a).tobytes()
+
+
+def test_lab5_cpu_program_rejects_short_input():
+    r = subprocess.run([os.path.join(ROOT, "labs/lab5/src/cpu_exe"), "int"], input=np.int32(5).tobytes() + b"\0" * 8,
+                       capture_output=True, timeout=60)
+    assert r.returncode != 0 and b"expected 5 binary elements" in r.stderr
+
+
+def test_sort_rejects_bad_dtype():
+    with pytest.raises(ValueError):
+        ops.sort_(torch.zeros(4, dtype=torch.float64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", list(KINDS))
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 4095, 4096, 4097, 8192, 12289, 100_003, (1 << 20) + 7])
+def test_gpu_sort_matches_cpu(gpu, kind, n):
+    """Every tile / global-step boundary: sizes around the 4096-key LDS tile,
+    non-powers of two (virtual +inf padding) and a 2^20 + 7 array (9 stages
+    beyond the tile)."""
+    a = random_array(kind, n, seed=n + 1)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    ops.sort_(d)
+    assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_sort_matches_torch_and_handles_duplicates(gpu):
+    x = torch.randint(-50, 50, (300_001,), dtype=torch.int32, device=gpu)
+    ref = torch.sort(x).values
+    ops.sort_(x)
+    assert torch.equal(x, ref)
+    f = torch.randn(1 << 18, device=gpu)
+    ref = torch.sort(f).values
+    ops.sort_(f)
+    assert torch.equal(f, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exe", ["to_plot_hip_exe", "hip_exe"])
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_lab5_gpu_program(exe, kind):
+    a = random_array(kind, 50_000, seed=7)
+    for data in (fixture_bytes(kind, a), open(os.path.join(LAB5_DATA, kind + "10"), "rb").read()):
+        r = subprocess.run([os.path.join(ROOT, "labs/lab5/src", exe), kind], input=data, capture_output=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        src = np.frombuffer(data[4:], dtype=KINDS[kind][0])
+        payload = r.stdout
+        if exe == "to_plot_hip_exe":
+            head, _, payload = r.stdout.partition(b"\n")
+            assert head.startswith(b"HIP execution time: <")
+        assert payload == total_order_sorted(src).tobytes()
