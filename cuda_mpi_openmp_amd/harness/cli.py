@@ -71,7 +71,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     print(f"kwargs=<{json.dumps(kwargs, indent=2)}>")
     print(f"metadata_columns2plot=<{json.dumps(meta, indent=2)}>")
     print(f"n_gpus=<{args.n_gpus}>")
-    if lab_name in ("lab2", "lab3") and "dir_to_data" not in kwargs:
+    if lab_name in ("lab2", "lab3", "lab5") and "dir_to_data" not in kwargs:
         kwargs["lab_dir"] = lab_dir
     env = {}
     if args.timing:

@@ -92,22 +92,37 @@ def run_binary(binary_path: str, processor, k1=None, k2=None, return_inp: bool =
     try:
         stdin_text, verify_kwargs, debug = processor.pre_process(device_info=device_tag(binary_path, k1, k2))
         rec.debug_data = dict(debug or {})
-        stdin_text = geometry_prefix(k1, k2) + stdin_text
+        binary = getattr(processor, "binary_io", False)
+        if getattr(processor, "takes_geometry", True):
+            prefix = geometry_prefix(k1, k2)
+            stdin_text = (prefix.encode() + stdin_text) if binary else (prefix + stdin_text)
         if return_inp:
             rec.debug_data["input_str"] = stdin_text
         run_env = None
-        if env:
+        proc_env = dict(getattr(processor, "env", None) or {})
+        proc_env.update(env or {})
+        if proc_env:
             run_env = dict(os.environ)
-            run_env.update(env)
-        proc = subprocess.run([binary_path], input=stdin_text, text=True, capture_output=True, check=True,
+            run_env.update(proc_env)
+        proc = subprocess.run([binary_path], input=stdin_text, text=not binary, capture_output=True, check=True,
                               timeout=timeout, env=run_env)
-        head, payload = split_stdout(proc.stdout)
+        if binary:
+            # lab5: binary payload after a text timing line (benchmark personality only)
+            raw = proc.stdout
+            if raw.startswith(b"HIP execution time") or raw.startswith(b"CPU execution time"):
+                head_b, _, payload = raw.partition(b"\n")
+                head = head_b.decode(errors="replace")
+            else:
+                head, payload = "", raw
+        else:
+            head, payload = split_stdout(proc.stdout)
         rec.time_kernel_exe_ms = parse_timing(head)
         rec.task_result = processor.get_task_result(payload, **verify_kwargs)
         rec.test_verification_result = processor.verify_result(rec.task_result, **verify_kwargs)
         rec.status = True
     except subprocess.CalledProcessError as e:
-        rec.err = (e.stderr or "").strip()
+        err = e.stderr or ""
+        rec.err = (err.decode(errors="replace") if isinstance(err, bytes) else err).strip()
         print(f"[HIP ERROR] {rec.err}")
     except subprocess.TimeoutExpired:
         rec.err = f"timeout after {timeout} s"

@@ -239,4 +239,80 @@ class Lab3Processor(_ImageLabProcessor):
         return f"{item.data_path}\n{out}\n{len(cls)}\n{rows}", {"idx_data": item.idx, "out_path_res": out}, dbg
 
 
-PROCESSORS = {"lab1": Lab1Processor, "lab2": Lab2Processor, "lab3": Lab3Processor}
+LAB5_TYPES = {"int": np.int32, "float": np.float32, "uchar": np.uint8}
+
+
+def lab5_sorted(a: np.ndarray) -> np.ndarray:
+    """Expected lab5 order: numeric for int32/uint8, the IEEE total order for
+    float32 (-NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN), matching the
+    order-preserving uint32 keys of native/src/kernels/sort.hip."""
+    if a.dtype != np.float32:
+        return np.sort(a, kind="stable")
+    u = a.view(np.uint32)
+    key = np.where(u >> 31 == 1, ~u, u | np.uint32(0x80000000))
+    return a[np.argsort(key, kind="stable")]
+
+
+class Lab5Processor(LabProcessor):
+    """lab5 (sort). The reference ships only the binary fixtures
+    ``lab5/data/{int10,float10,uchar10}`` (int32 n + n elements) and no
+    processor, so this one is ours: it round-robins over the fixtures of the
+    chosen ``elem_type`` (plus ``n_random`` seeded random arrays of
+    ``min_size..max_size`` elements), feeds them as binary stdin, and verifies
+    the binary stdout byte-exactly against numpy's sort. The element type
+    reaches the program through ``MPX_LAB5_TYPE``; lab5 programs take no
+    launch geometry, so none is prepended."""
+
+    lab = "lab5"
+    binary_io = True
+    takes_geometry = False
+
+    def __init__(self, seed: int = 42, elem_type: str = "int", n_random: int = 2, min_size: int = 1024,
+                 max_size: int = 1 << 20, dir_to_data: Optional[str] = None, lab_dir: Optional[str] = None, **_):
+        super().__init__(seed)
+        if elem_type not in LAB5_TYPES:
+            raise ValueError(f"elem_type must be one of {sorted(LAB5_TYPES)}")
+        self.elem_type, self.dtype = elem_type, LAB5_TYPES[elem_type]
+        self.env = {"MPX_LAB5_TYPE": elem_type}
+        if dir_to_data is None:
+            dir_to_data = os.path.join(lab_dir, "data") if lab_dir else "./lab5/data"
+        self.items: List[Tuple[str, np.ndarray]] = []
+        fixture = os.path.join(dir_to_data, f"{elem_type}10")
+        if os.path.exists(fixture):
+            raw = open(fixture, "rb").read()
+            n = int(np.frombuffer(raw[:4], dtype="<i4")[0])
+            self.items.append((os.path.basename(fixture), np.frombuffer(raw[4:], dtype=self.dtype, count=n).copy()))
+        for i in range(int(n_random)):
+            n = int(self.rng.randint(int(min_size), int(max_size) + 1))
+            if elem_type == "float":
+                a = (self.rng.standard_normal(n) * 10.0 ** self.rng.randint(-30, 30, n)).astype(np.float32)
+            else:
+                info = np.iinfo(self.dtype)
+                a = self.rng.randint(int(info.min), int(info.max) + 1, n, dtype=np.int64).astype(self.dtype)
+            self.items.append((f"random_{i}_{n}", a))
+        if not self.items:
+            raise FileNotFoundError(f"no lab5 inputs for {elem_type}")
+        self.cursor = 0
+
+    def get_attr(self):
+        return {"elem_type": self.elem_type}
+
+    def pre_process(self, **kwargs):
+        name, a = self.items[self.cursor]
+        idx = self.cursor
+        self.cursor = (self.cursor + 1) % len(self.items)
+        stdin = np.int32(a.size).astype("<i4").tobytes() + a.astype(self.dtype).tobytes()
+        return stdin, {"idx_data": idx}, {"filename": name, "n": int(a.size)}
+
+    def get_task_result(self, payload: bytes, **kwargs):
+        return np.frombuffer(payload, dtype=self.dtype)
+
+    def verify_result(self, result, **kwargs) -> bool:
+        expect = lab5_sorted(self.items[kwargs["idx_data"]][1])
+        ok = result.size == expect.size and result.tobytes() == expect.tobytes()
+        if not ok:
+            print(f"[verify_result] lab5 {self.elem_type} mismatch: got {result.size} elements, want {expect.size}")
+        return ok
+
+
+PROCESSORS = {"lab1": Lab1Processor, "lab2": Lab2Processor, "lab3": Lab3Processor, "lab5": Lab5Processor}

@@ -17,8 +17,9 @@
 //     step with j >= kTile; the steps j < kTile of the same stage run in one
 //     LDS launch per tile. N = 2^26 takes 105 global passes + 15 LDS passes.
 //   * uint8 uses a counting sort instead: 256 LDS histogram bins per block
-//     (one global atomic per bin and block), then every block rebuilds the
-//     exclusive prefix in LDS and writes its output range by binary search.
+//     stored to a per-block row (no global atomics), one block reduces the
+//     rows and scans them into 257 bucket starts, and every block writes its
+//     output range by binary search over those starts staged in LDS.
 #include "internal.hpp"
 
 namespace mpx {
@@ -116,28 +117,42 @@ __global__ void sort_step_kernel(uint32_t *__restrict__ x, int64_t n, int64_t np
     }
 }
 
+// Per-block LDS histogram written to its own row of `partial` (no global
+// atomics), then one block reduces the rows column-wise (coalesced) and scans
+// them into the 257 bucket starts the fill kernel reads.
 __global__ __launch_bounds__(256) void hist_u8_kernel(const uint8_t *__restrict__ x, int64_t n,
-                                                      uint32_t *__restrict__ counts) {
+                                                      uint32_t *__restrict__ partial) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&h[x[i]], 1u);
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+    partial[(int64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void scan_u8_kernel(const uint32_t *__restrict__ partial, int nblocks,
+                                                      int64_t *__restrict__ start) {
+    __shared__ int64_t col[256];
+    int64_t acc = 0;
+    for (int b = 0; b < nblocks; ++b) acc += partial[(int64_t)b * 256 + threadIdx.x];
+    col[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int v = 0; v < 256; ++v) {
+            start[v] = run;
+            run += col[v];
+        }
+        start[256] = run;
+    }
 }
 
 __global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, int64_t n,
-                                                      const uint32_t *__restrict__ counts) {
+                                                      const int64_t *__restrict__ gstart) {
     __shared__ int64_t start[257];
-    if (threadIdx.x == 0) {
-        int64_t acc = 0;
-        for (int v = 0; v < 256; ++v) {
-            start[v] = acc;
-            acc += counts[v];
-        }
-        start[256] = acc;
-    }
+    start[threadIdx.x] = gstart[threadIdx.x];
+    if (threadIdx.x == 0) start[256] = gstart[256];
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += stride) {
@@ -185,15 +200,20 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
     MPX_CHECK_ARG(data, "null data");
     hipStream_t s = as_stream(stream);
     if (dtype == MPX_SORT_U8) {
-        uint32_t *counts = nullptr;
-        MPX_RETURN_IF_HIP_ERROR(hipMallocAsync(reinterpret_cast<void **>(&counts), 256 * sizeof(uint32_t), s));
-        MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(counts, 0, 256 * sizeof(uint32_t), s));
+        const int hblocks = std::min(grid_for(n, 256), 1024);
+        const size_t bytes = 257 * sizeof(int64_t) + (size_t)hblocks * 256 * sizeof(uint32_t);
+        void *scratch = nullptr;
+        MPX_RETURN_IF_HIP_ERROR(hipMallocAsync(&scratch, bytes, s));
+        int64_t *start = static_cast<int64_t *>(scratch);
+        uint32_t *partial = reinterpret_cast<uint32_t *>(start + 257);
         uint8_t *x = static_cast<uint8_t *>(data);
-        hipLaunchKernelGGL(hist_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, counts);
+        hipLaunchKernelGGL(hist_u8_kernel, dim3(hblocks), dim3(256), 0, s, x, n, partial);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, counts);
+        hipLaunchKernelGGL(scan_u8_kernel, dim3(1), dim3(256), 0, s, partial, hblocks, start);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        MPX_RETURN_IF_HIP_ERROR(hipFreeAsync(counts, s));
+        hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, start);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        MPX_RETURN_IF_HIP_ERROR(hipFreeAsync(scratch, s));
         return MPX_OK;
     }
     MPX_CHECK_ARG((reinterpret_cast<uintptr_t>(data) & 3u) == 0, "int32/float32 data must be 4-byte aligned");

@@ -159,3 +159,38 @@ def test_harness_lab2_gpu_n_gpus_warmup(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
     assert df["test_verification_result"].all() and (df["n_gpus"] == 2).all()
+
+
+@pytest.mark.parametrize("elem_type", ["int", "float", "uchar"])
+def test_harness_lab5_cpu(tmp_path, elem_type):
+    """lab5 through run_test.py: binary stdin/stdout, fixture + random arrays,
+    byte-exact verification; the default --kernel_sizes geometry is not sent."""
+    lab = _copy_lab(tmp_path, "lab5")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "3", "--elem_type", elem_type, "--max_size", "5000",
+                   "--metadata_columns2plot", '["filename"]'], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    df = pd.read_csv(lab / "src" / "stats_cpu_omp_exe.csv")
+    assert len(df) == 3 and df["test_verification_result"].all()
+    assert (df["elem_type"] == elem_type).all() and df["filename"].iloc[0] == f"{elem_type}10"
+
+
+def test_harness_lab5_detects_unsorted(tmp_path):
+    lab = _copy_lab(tmp_path, "lab5")
+    fake = lab / "src" / "fake_exe"  # echoes its input unsorted
+    fake.write_text("#!/bin/sh\necho 'CPU execution time: <1.0 ms>'\ntail -c +5\n")
+    fake.chmod(0o755)
+    r = _run_test(["--binary_path_cuda", str(fake), "--k_times", "2", "--n_random", "1"], tmp_path)
+    assert "FAILED" in r.stdout
+    assert os.path.exists(lab / "src" / "failed_fake_exe.csv")
+
+
+@pytest.mark.gpu
+def test_harness_lab5_gpu_vs_cpu(tmp_path):
+    lab = _copy_lab(tmp_path, "lab5")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "to_plot_hip_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "3", "--elem_type", "float", "--max_size", "200000"],
+                  tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
+    assert df["test_verification_result"].all() and (df["time_kernel_exe_ms"] >= 0).all()
