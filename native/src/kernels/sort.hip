@@ -20,6 +20,8 @@
 //     stored to a per-block row (no global atomics), one block reduces the
 //     rows and scans them into 257 bucket starts, and every block writes its
 //     output range by binary search over those starts staged in LDS.
+#include <mutex>
+
 #include "internal.hpp"
 
 namespace mpx {
@@ -170,6 +172,30 @@ int grid_for(int64_t work, int block) {
     return (int)std::max<int64_t>(1, std::min<int64_t>((work + block - 1) / block, (int64_t)kNumCUs * 16));
 }
 
+// The uint8 path's scratch (257 bucket starts + kHistBlocks histogram rows,
+// 1 MiB) is allocated once per device and kept: a stream-ordered
+// hipMallocAsync/hipFreeAsync pair per call returned corrupted output when a
+// plain HIP program (labs/lab5 CLI, null stream) sorted the same buffer twice
+// (tools/lab5_u8_diag.py), while the torch process did not. Sorts of uint8
+// data on one device therefore share the scratch and must run on one stream.
+constexpr int kHistBlocks = 1024;
+constexpr int kMaxDevices = 64;
+
+int u8_scratch(void **out) {
+    static std::mutex mu;
+    static void *bufs[kMaxDevices] = {};
+    int dev = 0;
+    MPX_RETURN_IF_HIP_ERROR(hipGetDevice(&dev));
+    MPX_CHECK_ARG(dev >= 0 && dev < kMaxDevices, "device index out of range");
+    std::lock_guard<std::mutex> lock(mu);
+    if (!bufs[dev]) {
+        const size_t bytes = 257 * sizeof(int64_t) + (size_t)kHistBlocks * 256 * sizeof(uint32_t);
+        MPX_RETURN_IF_HIP_ERROR(hipMalloc(&bufs[dev], bytes));
+    }
+    *out = bufs[dev];
+    return MPX_OK;
+}
+
 int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
     if (n < 2) return MPX_OK;
     const int64_t tiles = (n + kTile - 1) / kTile;
@@ -200,10 +226,9 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
     MPX_CHECK_ARG(data, "null data");
     hipStream_t s = as_stream(stream);
     if (dtype == MPX_SORT_U8) {
-        const int hblocks = std::min(grid_for(n, 256), 1024);
-        const size_t bytes = 257 * sizeof(int64_t) + (size_t)hblocks * 256 * sizeof(uint32_t);
+        const int hblocks = std::min(grid_for(n, 256), kHistBlocks);
         void *scratch = nullptr;
-        MPX_RETURN_IF_HIP_ERROR(hipMallocAsync(&scratch, bytes, s));
+        if (const int rc = u8_scratch(&scratch)) return rc;
         int64_t *start = static_cast<int64_t *>(scratch);
         uint32_t *partial = reinterpret_cast<uint32_t *>(start + 257);
         uint8_t *x = static_cast<uint8_t *>(data);
@@ -213,7 +238,6 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, start);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        MPX_RETURN_IF_HIP_ERROR(hipFreeAsync(scratch, s));
         return MPX_OK;
     }
     MPX_CHECK_ARG((reinterpret_cast<uintptr_t>(data) & 3u) == 0, "int32/float32 data must be 4-byte aligned");
