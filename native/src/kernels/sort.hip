@@ -120,51 +120,88 @@ __global__ void sort_step_kernel(uint32_t *__restrict__ x, int64_t n, int64_t np
 }
 
 // Per-block LDS histogram written to its own row of `partial` (no global
-// atomics), then one block reduces the rows column-wise (coalesced) and scans
-// them into the 257 bucket starts the fill kernel reads.
-__global__ __launch_bounds__(256) void hist_u8_kernel(const uint8_t *__restrict__ x, int64_t n,
-                                                      uint32_t *__restrict__ partial) {
+// atomics), then one block reduces the rows column-wise (coalesced, four row
+// groups in parallel) and scans them into the 257 bucket starts the fill
+// kernel reads. The body of the array moves as 16-B vectors (one uint4 per
+// thread and iteration); the unaligned head (< 16 B) and the tail go bytewise.
+__device__ inline int64_t u8_scalar_pos(int64_t i, int64_t head, int64_t tail0) {
+    return i < head ? i : tail0 + (i - head);
+}
+
+__global__ __launch_bounds__(256) void hist_u8_kernel(const uint8_t *__restrict__ x, int64_t n, int64_t head,
+                                                      int64_t nvec, uint32_t *__restrict__ partial) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&h[x[i]], 1u);
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4 *v = reinterpret_cast<const uint4 *>(x + head);
+    for (int64_t i = gid; i < nvec; i += stride) {
+        const uint4 q = v[i];
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) atomicAdd(&h[(w[k] >> (8 * b)) & 255u], 1u);
+    }
+    const int64_t tail0 = head + 16 * nvec;
+    for (int64_t i = gid; i < head + (n - tail0); i += stride) atomicAdd(&h[x[u8_scalar_pos(i, head, tail0)]], 1u);
     __syncthreads();
     partial[(int64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void scan_u8_kernel(const uint32_t *__restrict__ partial, int nblocks,
-                                                      int64_t *__restrict__ start) {
-    __shared__ int64_t col[256];
-    int64_t acc = 0;
-    for (int b = 0; b < nblocks; ++b) acc += partial[(int64_t)b * 256 + threadIdx.x];
-    col[threadIdx.x] = acc;
+__global__ __launch_bounds__(1024) void scan_u8_kernel(const uint32_t *__restrict__ partial, int nblocks,
+                                                       int64_t *__restrict__ start) {
+    __shared__ int64_t acc[4][256];
+    const int col = threadIdx.x & 255, grp = threadIdx.x >> 8;
+    int64_t sum = 0;
+    for (int b = grp; b < nblocks; b += 4) sum += partial[(int64_t)b * 256 + col];
+    acc[grp][col] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t run = 0;
         for (int v = 0; v < 256; ++v) {
             start[v] = run;
-            run += col[v];
+            run += acc[0][v] + acc[1][v] + acc[2][v] + acc[3][v];
         }
         start[256] = run;
     }
 }
 
-__global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, int64_t n,
-                                                      const int64_t *__restrict__ gstart) {
+__device__ inline int u8_value_at(const int64_t *start, int64_t o) {
+    int lo = 0, hi = 255;  // largest v with start[v] <= o
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (start[mid] <= o) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, int64_t n, int64_t head,
+                                                      int64_t nvec, const int64_t *__restrict__ gstart) {
     __shared__ int64_t start[257];
     start[threadIdx.x] = gstart[threadIdx.x];
     if (threadIdx.x == 0) start[256] = gstart[256];
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += stride) {
-        int lo = 0, hi = 255;  // largest v with start[v] <= o
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (start[mid] <= o) lo = mid;
-            else hi = mid - 1;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 *v = reinterpret_cast<uint4 *>(x + head);
+    for (int64_t i = gid; i < nvec; i += stride) {
+        const int64_t o = head + 16 * i;
+        int val = u8_value_at(start, o);
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            while (start[val + 1] <= o + k) ++val;  // start[256] = n > o + k: stops at 255
+            w[k >> 2] |= (uint32_t)val << (8 * (k & 3));
         }
-        x[o] = (uint8_t)lo;
+        v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    const int64_t tail0 = head + 16 * nvec;
+    for (int64_t i = gid; i < head + (n - tail0); i += stride) {
+        const int64_t o = u8_scalar_pos(i, head, tail0);
+        x[o] = (uint8_t)u8_value_at(start, o);
     }
 }
 
@@ -178,7 +215,7 @@ int grid_for(int64_t work, int block) {
 // plain HIP program (labs/lab5 CLI, null stream) sorted the same buffer twice
 // (tools/lab5_u8_diag.py), while the torch process did not. Sorts of uint8
 // data on one device therefore share the scratch and must run on one stream.
-constexpr int kHistBlocks = 1024;
+constexpr int kHistBlocks = 512;
 constexpr int kMaxDevices = 64;
 
 int u8_scratch(void **out) {
@@ -226,17 +263,20 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
     MPX_CHECK_ARG(data, "null data");
     hipStream_t s = as_stream(stream);
     if (dtype == MPX_SORT_U8) {
-        const int hblocks = std::min(grid_for(n, 256), kHistBlocks);
+        const int64_t head = std::min<int64_t>(n, (16 - (int64_t)(reinterpret_cast<uintptr_t>(data) & 15u)) & 15);
+        const int64_t nvec = (n - head) / 16;
+        const int hblocks = std::min(grid_for(std::max<int64_t>(nvec, 1), 256), kHistBlocks);
         void *scratch = nullptr;
         if (const int rc = u8_scratch(&scratch)) return rc;
         int64_t *start = static_cast<int64_t *>(scratch);
         uint32_t *partial = reinterpret_cast<uint32_t *>(start + 257);
         uint8_t *x = static_cast<uint8_t *>(data);
-        hipLaunchKernelGGL(hist_u8_kernel, dim3(hblocks), dim3(256), 0, s, x, n, partial);
+        hipLaunchKernelGGL(hist_u8_kernel, dim3(hblocks), dim3(256), 0, s, x, n, head, nvec, partial);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        hipLaunchKernelGGL(scan_u8_kernel, dim3(1), dim3(256), 0, s, partial, hblocks, start);
+        hipLaunchKernelGGL(scan_u8_kernel, dim3(1), dim3(1024), 0, s, partial, hblocks, start);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, start);
+        hipLaunchKernelGGL(fill_u8_kernel, dim3(grid_for(std::max<int64_t>(nvec, 1), 256)), dim3(256), 0, s, x, n, head,
+                           nvec, start);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;
     }

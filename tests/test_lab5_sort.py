@@ -145,3 +145,17 @@ def test_gpu_sort_twice_in_place(gpu, kind):
         ops.sort_(d)
         torch.cuda.synchronize()
         assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offset", [1, 3, 15, 16])
+@pytest.mark.parametrize("n", [5, 17, 40_000, 1 << 20])
+def test_gpu_sort_u8_unaligned(gpu, offset, n):
+    """uint8 views that start off a 16-B boundary: bytewise head, 16-B body,
+    bytewise tail; the bytes before the view stay untouched."""
+    a = random_array("uchar", n + offset, seed=n + offset)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    ops.sort_(d[offset:])
+    got = d.cpu().numpy()
+    assert got[:offset].tobytes() == a[:offset].tobytes()
+    assert got[offset:].tobytes() == np.sort(a[offset:]).tobytes()
