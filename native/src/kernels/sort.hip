@@ -155,16 +155,27 @@ __global__ __launch_bounds__(1024) void scan_u8_kernel(const uint32_t *__restric
     __shared__ int64_t acc[4][256];
     const int col = threadIdx.x & 255, grp = threadIdx.x >> 8;
     int64_t sum = 0;
+#pragma unroll 8
     for (int b = grp; b < nblocks; b += 4) sum += partial[(int64_t)b * 256 + col];
     acc[grp][col] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t run = 0;
-        for (int v = 0; v < 256; ++v) {
-            start[v] = run;
-            run += acc[0][v] + acc[1][v] + acc[2][v] + acc[3][v];
-        }
-        start[256] = run;
+    // inclusive Hillis-Steele scan of the 256 column totals (8 steps)
+    __shared__ int64_t scan[2][256];
+    int64_t tot = 0;
+    if (threadIdx.x < 256) {
+        tot = acc[0][col] + acc[1][col] + acc[2][col] + acc[3][col];
+        scan[0][col] = tot;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int off = 1; off < 256; off <<= 1) {
+        if (threadIdx.x < 256) scan[cur ^ 1][col] = scan[cur][col] + (col >= off ? scan[cur][col - off] : 0);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (threadIdx.x < 256) {
+        start[col] = scan[cur][col] - tot;
+        if (col == 255) start[256] = scan[cur][col];
     }
 }
 
@@ -215,7 +226,7 @@ int grid_for(int64_t work, int block) {
 // plain HIP program (labs/lab5 CLI, null stream) sorted the same buffer twice
 // (tools/lab5_u8_diag.py), while the torch process did not. Sorts of uint8
 // data on one device therefore share the scratch and must run on one stream.
-constexpr int kHistBlocks = 512;
+constexpr int kHistBlocks = 256;  // one per CU
 constexpr int kMaxDevices = 64;
 
 int u8_scratch(void **out) {
