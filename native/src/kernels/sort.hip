@@ -119,6 +119,32 @@ __global__ void sort_step_kernel(uint32_t *__restrict__ x, int64_t n, int64_t np
     }
 }
 
+// Two consecutive half-cleaner steps (j = 2h, then h) fused into one global
+// pass: each thread owns the quad i, i+h, i+2h, i+3h (i has bits h and 2h
+// clear), so the array is read and written once instead of twice. Power-of-two
+// index math with shifts. Slots past the end read as +inf and are never
+// stored (an ascending network never moves +inf down).
+__global__ void sort_step2_kernel(uint32_t *__restrict__ x, int64_t n, int64_t nquads, int lh) {
+    const int64_t h = (int64_t)1 << lh;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nquads; q += stride) {
+        const int64_t i = ((q >> lh) << (lh + 2)) | (q & (h - 1));
+        if (i + h >= n) continue;  // only slot 0 real (or slots 0 and 2, checked below): nothing moves
+        uint32_t v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = i + e * h < n ? x[i + e * h] : 0xffffffffu;
+        uint32_t a = min(v[0], v[2]), c = max(v[0], v[2]);
+        uint32_t b = min(v[1], v[3]), d = max(v[1], v[3]);
+        v[0] = min(a, b);
+        v[1] = max(a, b);
+        v[2] = min(c, d);
+        v[3] = max(c, d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (i + e * h < n) x[i + e * h] = v[e];
+    }
+}
+
 // Per-block LDS histogram written to its own row of `partial` (no global
 // atomics), then one block reduces the rows column-wise (coalesced, four row
 // groups in parallel) and scans them into the 257 bucket starts the fill
@@ -254,9 +280,17 @@ int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
     while (npow < n) npow <<= 1;
     const int64_t npairs = npow / 2;
     for (int64_t k = 2 * (int64_t)kTile; k <= npow; k <<= 1) {
-        for (int64_t j = k / 2; j >= kTile; j >>= 1) {
-            hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, j,
-                               j == k / 2 ? 1 : 0);
+        hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, k / 2, 1);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        int64_t j = k / 4;
+        for (; j >= 2 * (int64_t)kTile; j >>= 2) {  // steps j and j/2 in one pass
+            int lh = 0;
+            while (((int64_t)1 << lh) < j / 2) ++lh;
+            hipLaunchKernelGGL(sort_step2_kernel, dim3(grid_for(npow / 4, 256)), dim3(256), 0, s, x, n, npow / 4, lh);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        }
+        if (j == kTile) {
+            hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, j, 0);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         }
         hipLaunchKernelGGL(sort_tile_kernel, dim3((unsigned)tiles), dim3(kSortThreads), 0, s, x, n, 0);
