@@ -119,28 +119,33 @@ __global__ void sort_step_kernel(uint32_t *__restrict__ x, int64_t n, int64_t np
     }
 }
 
-// Two consecutive half-cleaner steps (j = 2h, then h) fused into one global
-// pass: each thread owns the quad i, i+h, i+2h, i+3h (i has bits h and 2h
-// clear), so the array is read and written once instead of twice. Power-of-two
-// index math with shifts. Slots past the end read as +inf and are never
-// stored (an ascending network never moves +inf down).
-__global__ void sort_step2_kernel(uint32_t *__restrict__ x, int64_t n, int64_t nquads, int lh) {
+// L consecutive half-cleaner steps (j = 2^(L-1) h, ..., 2h, h) fused into one
+// global pass: each thread owns the 2^L slots i + e*h (i has the L bits from h
+// up clear), so the array is read and written once instead of L times.
+// Power-of-two index math with shifts. Slots past the end read as +inf and are
+// never stored (an ascending network never moves +inf down).
+template <int L>
+__global__ void sort_stepn_kernel(uint32_t *__restrict__ x, int64_t n, int64_t ngroups, int lh) {
+    constexpr int G = 1 << L;
     const int64_t h = (int64_t)1 << lh;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nquads; q += stride) {
-        const int64_t i = ((q >> lh) << (lh + 2)) | (q & (h - 1));
-        if (i + h >= n) continue;  // only slot 0 real (or slots 0 and 2, checked below): nothing moves
-        uint32_t v[4];
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < ngroups; q += stride) {
+        const int64_t i = ((q >> lh) << (lh + L)) | (q & (h - 1));
+        if (i + h >= n) continue;  // only slot 0 is real: nothing moves
+        uint32_t v[G];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = i + e * h < n ? x[i + e * h] : 0xffffffffu;
-        uint32_t a = min(v[0], v[2]), c = max(v[0], v[2]);
-        uint32_t b = min(v[1], v[3]), d = max(v[1], v[3]);
-        v[0] = min(a, b);
-        v[1] = max(a, b);
-        v[2] = min(c, d);
-        v[3] = max(c, d);
+        for (int e = 0; e < G; ++e) v[e] = i + e * h < n ? x[i + e * h] : 0xffffffffu;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int d = G / 2; d >= 1; d >>= 1)
+#pragma unroll
+            for (int e = 0; e < G; ++e)
+                if ((e & d) == 0) {
+                    const uint32_t lo = min(v[e], v[e + d]), hi = max(v[e], v[e + d]);
+                    v[e] = lo;
+                    v[e + d] = hi;
+                }
+#pragma unroll
+        for (int e = 0; e < G; ++e)
             if (i + e * h < n) x[i + e * h] = v[e];
     }
 }
@@ -283,15 +288,20 @@ int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
         hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, k / 2, 1);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         int64_t j = k / 4;
-        for (; j >= 2 * (int64_t)kTile; j >>= 2) {  // steps j and j/2 in one pass
+        while (j >= kTile) {  // remaining half-cleaners j, j/2, ..., kTile: up to 3 per pass
+            int steps = 1;
+            while (steps < 3 && (j >> steps) >= kTile) ++steps;
             int lh = 0;
-            while (((int64_t)1 << lh) < j / 2) ++lh;
-            hipLaunchKernelGGL(sort_step2_kernel, dim3(grid_for(npow / 4, 256)), dim3(256), 0, s, x, n, npow / 4, lh);
+            while (((int64_t)1 << lh) < (j >> (steps - 1))) ++lh;
+            const int64_t groups = npow >> steps;
+            if (steps == 3)
+                hipLaunchKernelGGL(sort_stepn_kernel<3>, dim3(grid_for(groups, 256)), dim3(256), 0, s, x, n, groups, lh);
+            else if (steps == 2)
+                hipLaunchKernelGGL(sort_stepn_kernel<2>, dim3(grid_for(groups, 256)), dim3(256), 0, s, x, n, groups, lh);
+            else
+                hipLaunchKernelGGL(sort_stepn_kernel<1>, dim3(grid_for(groups, 256)), dim3(256), 0, s, x, n, groups, lh);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-        }
-        if (j == kTile) {
-            hipLaunchKernelGGL(sort_step_kernel, dim3(grid_for(npairs, 256)), dim3(256), 0, s, x, n, npairs, k, j, 0);
-            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            j >>= steps;
         }
         hipLaunchKernelGGL(sort_tile_kernel, dim3((unsigned)tiles), dim3(kSortThreads), 0, s, x, n, 0);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
