@@ -51,6 +51,26 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
     return float(t.item())
 
 
+def all_gather_floats(value: float, ctx: DistContext) -> List[float]:
+    """Every rank's host scalar, in rank order (e.g. per-rank step times)."""
+    if not ctx.is_distributed:
+        return [float(value)]
+    dev = ctx.device if ctx.backend == "nccl" else "cpu"
+    mine = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    every = [torch.empty_like(mine) for _ in range(ctx.world)]
+    dist.all_gather(every, mine)
+    return [float(t.item()) for t in every]
+
+
+def all_reduce_sum_host(value: float, ctx: DistContext) -> float:
+    """Sum of a host scalar over ranks."""
+    if not ctx.is_distributed:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def broadcast_object(obj: Any, ctx: DistContext, src: int = 0) -> Any:
     if not ctx.is_distributed:
         return obj

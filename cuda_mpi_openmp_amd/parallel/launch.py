@@ -1,0 +1,80 @@
+"""Self-launch of N ranks (one process per GPU) for scripts run as ``python X --gpus N``.
+
+A benchmark started without a torchrun environment but asked for N > 1 GPUs
+must not quietly measure one GPU: :func:`relaunch_if_needed` re-runs the same
+script under ``torch.distributed.run`` with N local ranks and returns the
+child's exit code, *before* anything in this process initialises HIP (the
+launcher only counts devices, which does not create a HIP context on this
+image). Inside a rank, :func:`check_world` refuses a WORLD_SIZE that differs
+from the requested N.
+
+One-GPU rehearsal: with ``MPX_DIST_BACKEND=gloo`` several ranks may share a
+device (control plane over gloo, halos over IPC-mapped peer memory); every
+other GPU run needs N visible devices or fails with exit code 2.
+
+The reference has no multi-process code at all; this is the
+north-star "1/2/4/8 MI355X" launch path.
+"""
+
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+from typing import List, Optional, Sequence
+
+EXIT_BAD_WORLD = 2
+
+
+def in_rank_env() -> bool:
+    """True when this process is already one rank of a launched job."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def visible_devices() -> int:
+    import torch
+
+    return int(torch.cuda.device_count())  # counts devices without creating a HIP context
+
+
+def launcher_cmd(script: str, argv: Sequence[str], nproc: int, port: Optional[int] = None) -> List[str]:
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()), script, *argv]
+
+
+def relaunch_if_needed(script: str, argv: Sequence[str], gpus: int, device: str) -> Optional[int]:
+    """None when this process should run the work itself (already a rank, or
+    N == 1); otherwise launch N ranks of ``script argv`` and return their exit
+    code (non-zero when N devices are not available)."""
+    if in_rank_env() or gpus <= 1:
+        return None
+    rehearsal = os.environ.get("MPX_DIST_BACKEND") == "gloo"
+    if device != "cpu" and not rehearsal:
+        ndev = visible_devices()
+        if device == "cuda" and ndev == 0:
+            print("[launch] --device cuda but no GPU is visible", file=sys.stderr)
+            return EXIT_BAD_WORLD
+        if ndev and ndev < gpus:
+            print(f"[launch] --gpus {gpus} requested but only {ndev} GPU(s) are visible; refusing to run fewer "
+                  f"ranks (set MPX_DIST_BACKEND=gloo to rehearse {gpus} ranks on shared devices)", file=sys.stderr)
+            return EXIT_BAD_WORLD
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // gpus)))
+    r = subprocess.run(launcher_cmd(script, argv, gpus), env=env)
+    return r.returncode
+
+
+def check_world(gpus: int, world: int) -> None:
+    """Inside a rank: the launched world must be exactly the requested one."""
+    if gpus != world:
+        print(f"[launch] --gpus {gpus} but WORLD_SIZE={world}; refusing to report a different GPU count",
+              file=sys.stderr)
+        raise SystemExit(EXIT_BAD_WORLD)

@@ -64,6 +64,10 @@ class NativeComm:
         self.device = device
         self._L = _native.lib()
 
+    def size(self) -> int:
+        """World size as the RCCL communicator itself reports it (ncclCommCount)."""
+        return int(self._L.mpx_comm_size(self.handle))
+
     # ------------------------------------------------------------ creation
     @classmethod
     def create(cls, ctx) -> Optional["NativeComm"]:

@@ -52,6 +52,7 @@ struct RcclApi {
     decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclAllReduce) AllReduce = nullptr;
     decltype(&ncclGetVersion) GetVersion = nullptr;
+    decltype(&ncclCommCount) CommCount = nullptr;  // optional: world size as RCCL reports it
     void *handle = nullptr;
     std::string path;
 };
@@ -106,6 +107,7 @@ extern "C" int mpx_comm_load(const char *path) {
               bind(h, "ncclGetErrorString", a.GetErrorString) && bind(h, "ncclGroupStart", a.GroupStart) &&
               bind(h, "ncclGroupEnd", a.GroupEnd) && bind(h, "ncclSend", a.Send) && bind(h, "ncclRecv", a.Recv) &&
               bind(h, "ncclAllReduce", a.AllReduce) && bind(h, "ncclGetVersion", a.GetVersion);
+    bind(h, "ncclCommCount", a.CommCount);
     if (!ok) {
         set_error("RCCL at %s lacks a required symbol", path ? path : "librccl.so.1");
         return MPX_ERR_ARG;
@@ -178,7 +180,13 @@ extern "C" int mpx_comm_destroy(void *h) {
 }
 
 extern "C" int mpx_comm_rank(void *h) { return h ? static_cast<Comm *>(h)->rank : -1; }
-extern "C" int mpx_comm_size(void *h) { return h ? static_cast<Comm *>(h)->nranks : -1; }
+extern "C" int mpx_comm_size(void *h) {
+    if (!h) return -1;
+    Comm *c = static_cast<Comm *>(h);
+    int n = -1;
+    if (g_api.CommCount && c->comm && g_api.CommCount(c->comm, &n) == ncclSuccess) return n;
+    return c->nranks;
+}
 
 namespace {
 int group_p2p(Comm *c, int n, const int *kind, void *const *ptr, const int64_t *bytes, const int *peer,

@@ -19,7 +19,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(args, nproc=None):
+def _run(args, nproc=None, rc=0):
     cmd = [sys.executable]
     if nproc:
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
@@ -27,6 +27,9 @@ def _run(args, nproc=None):
     cmd += [os.path.join(ROOT, "bench.py"), *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
+    if rc:  # torchrun reports a failed rank as 1 whatever the rank's own code
+        assert r.returncode != 0, r.stdout[-2000:]
+        return r
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -57,3 +60,17 @@ def test_bench_jacobi_two_ranks_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["scaling"] == "strong" and rec["residual"] is not None and rec["value"] > 0
+
+
+def test_bench_self_launches_ranks_cpu():
+    """--gpus N without a torchrun environment launches N ranks itself."""
+    rec = _run(["--gpus", "3", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2"])
+    assert rec["n_gpus"] == 3 and rec["world_size_seen"]["torch_distributed"] == 3
+    assert len(rec["per_rank_ms_per_step"]) == 3 and rec["verified_bit_exact"] is True
+    # every pixel of every rotated slab on every rank was compared
+    assert rec["verified_pixels"] == 3 * 2 * 64 * 64
+
+
+def test_bench_refuses_world_mismatch_cpu():
+    r = _run(["--gpus", "3", "--device", "cpu", "--size", "64", "--steps", "1", "--warmup", "0"], nproc=2, rc=2)
+    assert "WORLD_SIZE=2" in r.stderr

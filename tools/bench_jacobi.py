@@ -5,6 +5,7 @@ available), residual all-reduce every --check-every iterations.
 
   python tools/bench_jacobi.py [--size 16384] [--iters 100] [--warmup 10]
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_jacobi.py
+  python tools/bench_jacobi.py --gpus 8      (launches the 8 ranks itself)
 
 Prints one JSON line on rank 0 (max time over ranks).
 """
@@ -31,8 +32,18 @@ def main() -> int:
     p.add_argument("--overlap", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     p.add_argument("--graph", action="store_true", help="replay HIP graphs of whole residual cycles")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks to run (self-launched when no torchrun environment); default WORLD_SIZE or 1")
     a = p.parse_args()
+    from cuda_mpi_openmp_amd.parallel import launch
+
+    if a.gpus is not None:
+        rc = launch.relaunch_if_needed(os.path.abspath(__file__), sys.argv[1:], a.gpus, a.device)
+        if rc is not None:
+            return rc
     ctx = parallel.init(device=a.device)
+    if a.gpus is not None:
+        launch.check_world(a.gpus, ctx.world)
     dt = torch.float32 if a.fp32 else torch.float64
     sol = SlabJacobi(ctx, a.size, a.size, dtype=dt, check_every=a.check_every,
                      overlap={"auto": "auto", "on": True, "off": False}[a.overlap])
