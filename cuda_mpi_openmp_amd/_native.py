@@ -95,6 +95,9 @@ _SIGNATURES = {
     "mpx_cpu_classify": (None, [c_vp, c_i64, c_int, _dp, _dp]),
     "mpx_cpu_jacobi_f64": (ctypes.c_double, [c_vp, c_vp, c_int, c_int, c_int, c_int]),
     "mpx_sort": (c_int, [c_vp, c_i64, c_int, c_vp]),
+    "mpx_sort_workspace_bytes": (c_i64, [c_i64, c_int]),
+    "mpx_sort_ws": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
+    "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
     "mpx_cpu_sort": (None, [c_vp, c_i64, c_int]),
 }
 

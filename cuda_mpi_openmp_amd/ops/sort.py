@@ -17,14 +17,20 @@ def sort_(x: torch.Tensor) -> torch.Tensor:
     """Sort a contiguous int32 / float32 / uint8 tensor ascending, in place
     (flattened). Floats follow the IEEE total order of their bit patterns
     (-NaN < -inf < -0.0 < +0.0 < +inf < +NaN). GPU tensors run the gfx950
-    bitonic / counting-sort kernels, CPU tensors the C reference."""
+    radix (int32/float32, bitonic for n <= 4096) / counting-sort (uint8)
+    kernels with scratch from torch's caching allocator on the tensor's stream;
+    CPU tensors run the C reference."""
     if x.dtype not in DTYPES:
         raise ValueError("sort_ supports int32, float32 and uint8")
     if not x.is_contiguous():
         raise ValueError("input must be contiguous")
     L = _native.lib()
     if x.is_cuda:
-        _native.check(L.mpx_sort(x.data_ptr(), x.numel(), DTYPES[x.dtype], _native.stream_of(x)))
+        dt = DTYPES[x.dtype]
+        nbytes = int(L.mpx_sort_workspace_bytes(x.numel(), dt))
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=x.device) if nbytes else None
+        _native.check(L.mpx_sort_ws(x.data_ptr(), x.numel(), dt, ws.data_ptr() if ws is not None else None, nbytes,
+                                    _native.stream_of(x)))
     else:
         L.mpx_cpu_sort(x.data_ptr(), x.numel(), DTYPES[x.dtype])
     return x

@@ -175,8 +175,14 @@ int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r
                    void *stream);
 
 /* ---------------- lab5: ascending sort (no reference program) ---------------- */
-/* In place on the device; dtype is an mpx_sort_dtype. int32/float32: bitonic network
- * on order-preserving uint32 keys; uint8: counting sort. */
+/* In place on the device; dtype is an mpx_sort_dtype. int32/float32: LSD radix sort
+ * (onesweep, 8-bit digits) on order-preserving uint32 keys, bitonic network for
+ * n <= 4096 or n >= 2^30; uint8: counting sort.
+ * mpx_sort_ws takes the scratch from the caller (>= mpx_sort_workspace_bytes(n, dtype)
+ * bytes, 16-byte aligned, stream-ordered with `stream`; may be NULL when that size is 0).
+ * mpx_sort allocates and frees its own scratch and synchronises the stream. */
+int64_t mpx_sort_workspace_bytes(int64_t n, int dtype);
+int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, void *stream);
 int mpx_sort(void *data, int64_t n, int dtype, void *stream);
 
 /* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */

@@ -112,20 +112,28 @@ inline void init_stream_queue(hipStream_t stream) {
     HIP_CHECK(hipStreamSynchronize(stream));
 }
 
-// Runs `launch()` under the policy; returns kernel milliseconds.
-template <typename F>
-float time_kernel(F &&launch, hipStream_t stream = nullptr) {
+struct NoRestore {
+    void operator()() const {}
+};
+
+// Runs `launch()` under the policy; returns kernel milliseconds. `restore()`
+// runs before every launch, outside the event pair (in-place kernels whose
+// warm-up would otherwise hand the timed launch already-processed data).
+template <typename F, typename R = NoRestore>
+float time_kernel(F &&launch, hipStream_t stream = nullptr, R &&restore = R{}) {
     const TimingPolicy pol = TimingPolicy::from_env();
     init_stream_queue(stream);
     hipEvent_t a, b;
     HIP_CHECK(hipEventCreate(&a));
     HIP_CHECK(hipEventCreate(&b));
     for (int i = 0; i < pol.warmups; ++i) {
+        restore();
         launch();
         HIP_CHECK(hipStreamSynchronize(stream));
     }
     std::vector<float> ts;
     for (int i = 0; i < pol.reps; ++i) {
+        restore();
         HIP_CHECK(hipEventRecord(a, stream));
         launch();
         HIP_CHECK(hipEventRecord(b, stream));

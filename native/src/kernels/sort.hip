@@ -4,22 +4,36 @@
 // ours: ascending order, in place on the device.
 //
 // MI355X design
-//   * int32 and float32 become order-preserving uint32 keys in place (sign
-//     flip; floats flip every bit when negative), so one network sorts both.
-//     Float order is the IEEE total order on the bit patterns: -NaN < -inf <
-//     ... < -0 < +0 < ... < +inf < +NaN.
-//   * The network is the all-ascending bitonic form: the first step of stage k
-//     compares i with i ^ (k - 1), later steps with i ^ j, and the lower index
-//     always keeps the minimum. Elements past n act as +inf and never move, so
-//     any n sorts without padding or scratch.
-//   * Stages up to kTile (4096 keys) run entirely in LDS, 16 keys per thread,
-//     in one launch. Larger stages issue one global compare-exchange pass per
-//     step with j >= kTile; the steps j < kTile of the same stage run in one
-//     LDS launch per tile. N = 2^26 takes 105 global passes + 15 LDS passes.
-//   * uint8 uses a counting sort instead: 256 LDS histogram bins per block
-//     stored to a per-block row (no global atomics), one block reduces the
-//     rows and scans them into 257 bucket starts, and every block writes its
-//     output range by binary search over those starts staged in LDS.
+//   * int32 and float32 become order-preserving uint32 keys (sign flip; floats
+//     flip every bit when negative). Float order is the IEEE total order on the
+//     bit patterns: -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN.
+//   * n > kTile: LSD radix sort, 8-bit digits, 4 passes, onesweep style:
+//       - one histogram pass builds all four 256-bin digit histograms at once
+//         (LDS atomics per block, one global atomic per bin and block);
+//       - each digit pass is ONE kernel: a block takes the next 8192-key tile
+//         from an atomic tile counter, ranks its keys stably in LDS (per-wave
+//         8-ballot match of equal digits, mbcnt for the rank among lower
+//         lanes, per-wave digit counters), publishes its 256 digit counts and
+//         resolves its global digit offsets by decoupled look-back over the
+//         preceding tiles (flag + count packed in one 32-bit word, so a single
+//         relaxed agent-scope store publishes both), then stages the tile in
+//         LDS in digit order and writes it out in runs per digit;
+//       - the key transform rides on the first pass's loads and the inverse
+//         on the last pass's stores; 4 passes ping-pong data -> ws -> data.
+//     Traffic: 1 read (histogram) + 4 x (read + write) of the array, no
+//     compare network. Tile ids are taken in launch order, so a block only
+//     ever waits on tiles whose blocks are already resident.
+//   * n <= kTile (4096 keys): the whole bitonic network in LDS, one launch;
+//     n >= 2^30 (beyond the 30-bit look-back counts): the global bitonic
+//     network (stages > kTile as fused global half-cleaner passes).
+//   * uint8 uses a counting sort: 256 LDS histogram bins per block stored to a
+//     per-block row (no global atomics), one block reduces the rows and scans
+//     them into 257 bucket starts, and every block writes its output range by
+//     binary search over those starts staged in LDS.
+//   * Scratch comes from a caller-provided workspace (mpx_sort_workspace_bytes
+//     / mpx_sort_ws): the Python op takes it from torch's caching allocator on
+//     the tensor's stream, so concurrent sorts on different streams or devices
+//     never share scratch.
 #include <mutex>
 
 #include "internal.hpp"
@@ -247,33 +261,330 @@ __global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, i
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// LSD radix sort (onesweep)
+// ---------------------------------------------------------------------------
+constexpr int kRThreads = 512;                 // 8 waves
+constexpr int kRWaves = kRThreads / 64;
+constexpr int kRPer = 16;                      // keys per thread
+constexpr int kRTile = kRThreads * kRPer;      // 8192 keys per tile
+constexpr int kRWaveKeys = kRTile / kRWaves;   // 1024 contiguous keys per wave
+constexpr uint32_t kFlagA = 1u << 30;          // tile aggregate published
+constexpr uint32_t kFlagP = 2u << 30;          // inclusive prefix published
+constexpr uint32_t kCountMask = (1u << 30) - 1;
+constexpr int64_t kRadixMaxN = (int64_t)1 << 30;
+constexpr uint32_t kSpinLimit = 1u << 26;      // exit guarantee; never reached with resident predecessors
+
+enum { kRawKeys = 0, kRawI32 = 1, kRawF32 = 2 };
+
+__device__ __forceinline__ uint32_t to_key(uint32_t v, int mode) {
+    return mode == kRawF32 ? (v ^ ((uint32_t)((int32_t)v >> 31) | 0x80000000u))
+                           : mode == kRawI32 ? (v ^ 0x80000000u) : v;
+}
+__device__ __forceinline__ uint32_t from_key(uint32_t k, int mode) {
+    return mode == kRawF32 ? (k ^ ((k >> 31) ? 0x80000000u : 0xffffffffu))
+                           : mode == kRawI32 ? (k ^ 0x80000000u) : k;
+}
+
+// all four digit histograms of the (transformed) keys in one read
+__global__ __launch_bounds__(256) void radix_hist_kernel(const uint32_t *__restrict__ x, int64_t n, int mode,
+                                                         uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[4 * 256];
+    for (int i = threadIdx.x; i < 4 * 256; i += 256) h[i] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = to_key(x[i], mode);
+        atomicAdd(&h[k & 255u], 1u);
+        atomicAdd(&h[256 + ((k >> 8) & 255u)], 1u);
+        atomicAdd(&h[512 + ((k >> 16) & 255u)], 1u);
+        atomicAdd(&h[768 + (k >> 24)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * 256; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// exclusive scan of one value per thread over threads 0..255 (waves 0-3);
+// every thread of the block must call it (two barriers)
+__device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t *s_wsum) {
+    const int t = threadIdx.x, lane = t & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (t < 256 && lane == 63) s_wsum[t >> 6] = x;
+    __syncthreads();
+    uint32_t add = 0;
+    for (int w = 0; w < (t >> 6) && w < 4; ++w) add += s_wsum[w];
+    __syncthreads();  // s_wsum may be reused by the caller
+    return x - v + add;
+}
+
+// 8-ballot match: the lanes of `valid` keys whose digit equals this lane's
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint64_t bal = __ballot(valid && ((d >> b) & 1u));
+        m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Digit pass. LOOKBACK (onesweep): the tile id comes from an atomic counter
+// and the global digit offsets from decoupled look-back over `status`.
+// !LOOKBACK (reduce-then-scan): the tile id is the XCD-remapped block id and
+// the offsets were scanned beforehand (radix_count_kernel + radix_scan_kernel:
+// offs[d][tile] = keys of digit d in the tiles before this one, tot[d] = keys
+// of digit d in the array).
+template <bool LOOKBACK>
+__global__ __launch_bounds__(kRThreads) void radix_pass_kernel(const uint32_t *__restrict__ in,
+                                                               uint32_t *__restrict__ out, int64_t n, int shift,
+                                                               int in_mode, int out_mode,
+                                                               const uint32_t *__restrict__ hist,
+                                                               uint32_t *__restrict__ status,
+                                                               uint32_t *__restrict__ tile_ctr,
+                                                               uint32_t *__restrict__ err, int ntiles) {
+    __shared__ uint32_t s_keys[kRTile];
+    __shared__ uint32_t s_cnt[kRWaves][256];  // per-wave digit counts, then exclusive offsets
+    __shared__ uint32_t s_dstart[256];        // tile-local start of each digit
+    __shared__ uint32_t s_gbase[256];         // global position of digit d's run minus s_dstart[d]
+    __shared__ uint32_t s_wsum[4];
+    __shared__ uint32_t s_tile;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if constexpr (LOOKBACK) {
+        if (t == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    }
+    for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t tile = LOOKBACK ? s_tile : (uint32_t)xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t base = (int64_t)tile * kRTile + w * kRWaveKeys + lane;
+
+    uint32_t key[kRPer], rank[kRPer];
+#pragma unroll
+    for (int e = 0; e < kRPer; ++e) {
+        const int64_t i = base + e * 64;
+        key[e] = i < n ? to_key(in[i], in_mode) : 0xffffffffu;  // pads rank last and are never stored
+    }
+    // stable rank within the wave: slices in index order, lanes in order
+#pragma unroll
+    for (int e = 0; e < kRPer; ++e) {
+        const uint32_t d = (key[e] >> shift) & 255u;
+        const uint64_t m = match_digit(d, true);
+        const uint32_t pre = lanes_below(m);
+        const uint32_t old = s_cnt[w][d];
+        if (pre == 0) s_cnt[w][d] = old + (uint32_t)__popcll(m);
+        rank[e] = old + pre;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < 256) {
+#pragma unroll
+        for (int ww = 0; ww < kRWaves; ++ww) {
+            const uint32_t c = s_cnt[ww][t];
+            s_cnt[ww][t] = tot;
+            tot += c;
+        }
+        uint32_t excl = 0;
+        if constexpr (LOOKBACK) {
+            // publish this tile's count, then look back for the preceding tiles' sum
+            uint32_t *st = status + (size_t)tile * 256 + t;
+            if (tile == 0) {
+                __hip_atomic_store(st, kFlagP | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(st, kFlagA | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int64_t j = (int64_t)tile - 1;
+                uint32_t spins = 0;
+                while (true) {
+                    const uint32_t v = __hip_atomic_load(status + (size_t)j * 256 + t, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    if ((v & ~kCountMask) == 0) {
+                        if (++spins > kSpinLimit) {
+                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    excl += v & kCountMask;
+                    if (v & kFlagP) break;
+                    --j;
+                }
+                __hip_atomic_store(st, kFlagP | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            excl = status[(size_t)t * ntiles + tile];  // offs[d][tile]
+        }
+        s_gbase[t] = excl;  // + digit base - tile-local start, below
+    }
+    const uint32_t dstart = scan256_excl(tot, s_wsum);
+    const uint32_t dbase = scan256_excl(t < 256 ? hist[t] : 0u, s_wsum);
+    if (t < 256) {
+        s_dstart[t] = dstart;
+        s_gbase[t] += dbase - dstart;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kRPer; ++e) {
+        const uint32_t d = (key[e] >> shift) & 255u;
+        s_keys[s_dstart[d] + s_cnt[w][d] + rank[e]] = key[e];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int i = t; i < kRTile; i += kRThreads) {
+        const uint32_t k = s_keys[i];
+        const int64_t pos = (int64_t)s_gbase[(k >> shift) & 255u] + i;
+        if (pos < n) out[pos] = from_key(k, out_mode);
+    }
+}
+
+// reduce-then-scan, step 1: the tile's digit counts, digit-major
+// (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
+// 4-byte stores into whole lines
+constexpr int kCThreads = 256;
+constexpr int kCPer = kRTile / kCThreads;  // 32 keys per thread
+__global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *__restrict__ in, int64_t n, int shift,
+                                                                int mode, uint32_t *__restrict__ cnt, int ntiles) {
+    __shared__ uint32_t h[kCThreads / 64][256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int i = t; i < (kCThreads / 64) * 256; i += kCThreads) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t base = (int64_t)tile * kRTile + w * (kRTile / (kCThreads / 64)) + lane;
+    uint32_t key[kCPer];
+#pragma unroll
+    for (int e = 0; e < kCPer; ++e) {
+        const int64_t i = base + e * 64;
+        key[e] = i < n ? in[i] : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < kCPer; ++e) {
+        const bool valid = base + e * 64 < n;
+        const uint32_t d = (to_key(key[e], mode) >> shift) & 255u;
+        const uint64_t m = match_digit(d, valid);
+        if (valid && lanes_below(m) == 0) h[w][d] += (uint32_t)__popcll(m);  // one leader per digit
+    }
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int ww = 0; ww < kCThreads / 64; ++ww) c += h[ww][t];
+    cnt[(size_t)t * ntiles + tile] = c;
+}
+
+// reduce-then-scan, step 2: one block per digit turns its row of tile counts
+// into exclusive offsets in place and records the digit total
+__global__ __launch_bounds__(256) void radix_scan_kernel(uint32_t *__restrict__ cnt, int ntiles,
+                                                         uint32_t *__restrict__ tot) {
+    constexpr int kChunk = 256 * 16;
+    __shared__ uint32_t v[kChunk];
+    __shared__ uint32_t s_wsum[4];
+    const int t = threadIdx.x;
+    uint32_t *row = cnt + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < ntiles; c0 += kChunk) {
+        const int m = min(kChunk, ntiles - c0);
+        for (int i = t; i < kChunk; i += 256) v[i] = i < m ? row[c0 + i] : 0u;
+        __syncthreads();
+        uint32_t own = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) own += v[t * 16 + k];
+        uint32_t run = carry + scan256_excl(own, s_wsum);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t x = v[t * 16 + k];
+            v[t * 16 + k] = run;
+            run += x;
+        }
+        if (t == 255) s_wsum[0] = run;  // carry for the next chunk
+        __syncthreads();
+        for (int i = t; i < m; i += 256) row[c0 + i] = v[i];
+        carry = s_wsum[0];
+        __syncthreads();
+    }
+    if (t == 0) tot[blockIdx.x] = carry;
+}
+
+struct RadixWs {
+    uint32_t *tmp, *hist, *ctr, *err, *status;
+    int64_t tiles;
+    size_t zero_bytes;
+};
+
+int64_t radix_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
+
+size_t radix_ws_bytes(int64_t n) {
+    const size_t keys = ((size_t)n * 4 + 255) / 256 * 256;
+    return keys + (4 * 256 + 64) * 4 + (size_t)4 * radix_tiles(n) * 256 * 4;
+}
+
+RadixWs radix_layout(void *ws, int64_t n) {
+    RadixWs r;
+    char *p = static_cast<char *>(ws);
+    const size_t keys = ((size_t)n * 4 + 255) / 256 * 256;
+    r.tmp = reinterpret_cast<uint32_t *>(p);
+    r.hist = reinterpret_cast<uint32_t *>(p + keys);
+    r.ctr = r.hist + 4 * 256;
+    r.err = r.ctr + 4;
+    r.status = r.ctr + 64;
+    r.tiles = radix_tiles(n);
+    r.zero_bytes = (4 * 256 + 64) * 4 + (size_t)4 * r.tiles * 256 * 4;
+    return r;
+}
+
+// Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan.
+// Look-back resolves one predecessor tile per memory round trip and the
+// cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
+// L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
+// reduce-then-scan re-reads each tile once more but never waits.
+constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;
+
+int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
+    const RadixWs r = radix_layout(ws, n);
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 2;
+    const int ntiles = (int)r.tiles;
+    if (variant == 1) {
+        MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
+        hipLaunchKernelGGL(radix_hist_kernel,
+                           dim3(std::max<int64_t>(1, std::min<int64_t>((n + 4095) / 4096, kNumCUs * 8))), dim3(256), 0,
+                           s, x, n, mode, r.hist);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    }
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t *src = (p & 1) ? r.tmp : x;
+        uint32_t *dst = (p & 1) ? x : r.tmp;
+        const int in_mode = p == 0 ? mode : (int)kRawKeys, out_mode = p == 3 ? mode : (int)kRawKeys;
+        if (variant == 1) {
+            hipLaunchKernelGGL(radix_pass_kernel<true>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst, n,
+                               8 * p, in_mode, out_mode, r.hist + 256 * p, r.status + (size_t)p * ntiles * 256,
+                               r.ctr + p, r.err, ntiles);
+        } else {
+            // offsets in status[0 .. 256 * ntiles), digit totals in hist[0 .. 256)
+            hipLaunchKernelGGL(radix_count_kernel, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src, n, 8 * p,
+                               in_mode, r.status, ntiles);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            hipLaunchKernelGGL(radix_scan_kernel, dim3(256), dim3(256), 0, s, r.status, ntiles, r.hist);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst, n,
+                               8 * p, in_mode, out_mode, r.hist, r.status, r.ctr, r.err, ntiles);
+        }
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    }
+    return MPX_OK;
+}
+
 int grid_for(int64_t work, int block) {
     return (int)std::max<int64_t>(1, std::min<int64_t>((work + block - 1) / block, (int64_t)kNumCUs * 16));
 }
 
-// The uint8 path's scratch (257 bucket starts + kHistBlocks histogram rows,
-// 1 MiB) is allocated once per device and kept: a stream-ordered
-// hipMallocAsync/hipFreeAsync pair per call returned corrupted output when a
-// plain HIP program (labs/lab5 CLI, null stream) sorted the same buffer twice
-// (tools/lab5_u8_diag.py), while the torch process did not. Sorts of uint8
-// data on one device therefore share the scratch and must run on one stream.
-constexpr int kHistBlocks = 256;  // one per CU
-constexpr int kMaxDevices = 64;
-
-int u8_scratch(void **out) {
-    static std::mutex mu;
-    static void *bufs[kMaxDevices] = {};
-    int dev = 0;
-    MPX_RETURN_IF_HIP_ERROR(hipGetDevice(&dev));
-    MPX_CHECK_ARG(dev >= 0 && dev < kMaxDevices, "device index out of range");
-    std::lock_guard<std::mutex> lock(mu);
-    if (!bufs[dev]) {
-        const size_t bytes = 257 * sizeof(int64_t) + (size_t)kHistBlocks * 256 * sizeof(uint32_t);
-        MPX_RETURN_IF_HIP_ERROR(hipMalloc(&bufs[dev], bytes));
-    }
-    *out = bufs[dev];
-    return MPX_OK;
-}
+constexpr int kHistBlocks = 256;  // uint8 histogram rows: one per CU
 
 int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
     if (n < 2) return MPX_OK;
@@ -309,21 +620,32 @@ int sort_keys(uint32_t *x, int64_t n, hipStream_t s) {
     return MPX_OK;
 }
 
+size_t u8_ws_bytes() { return 257 * sizeof(int64_t) + (size_t)kHistBlocks * 256 * sizeof(uint32_t); }
+
+bool use_radix(int64_t n) { return n > kTile && n < kRadixMaxN; }
+
 }  // namespace
 
-int sort_impl(void *data, int64_t n, int dtype, void *stream) {
+int64_t sort_workspace_bytes(int64_t n, int dtype) {
+    if (n < 2) return 0;
+    if (dtype == MPX_SORT_U8) return (int64_t)u8_ws_bytes();
+    return use_radix(n) ? (int64_t)radix_ws_bytes(n) : 0;
+}
+
+int sort_impl(void *data, int64_t n, int dtype, void *ws, int64_t ws_bytes, void *stream, int variant = 0) {
     MPX_CHECK_ARG(n >= 0, "n must be >= 0");
     MPX_CHECK_ARG(dtype == MPX_SORT_I32 || dtype == MPX_SORT_F32 || dtype == MPX_SORT_U8, "bad dtype");
-    if (n == 0) return MPX_OK;
+    if (n < 2) return MPX_OK;
     MPX_CHECK_ARG(data, "null data");
+    MPX_CHECK_ARG(ws_bytes >= sort_workspace_bytes(n, dtype) && (ws || sort_workspace_bytes(n, dtype) == 0),
+                  "workspace smaller than mpx_sort_workspace_bytes(n, dtype)");
+    MPX_CHECK_ARG(!ws || aligned16(ws), "workspace must be 16-byte aligned");
     hipStream_t s = as_stream(stream);
     if (dtype == MPX_SORT_U8) {
         const int64_t head = std::min<int64_t>(n, (16 - (int64_t)(reinterpret_cast<uintptr_t>(data) & 15u)) & 15);
         const int64_t nvec = (n - head) / 16;
         const int hblocks = std::min(grid_for(std::max<int64_t>(nvec, 1), 256), kHistBlocks);
-        void *scratch = nullptr;
-        if (const int rc = u8_scratch(&scratch)) return rc;
-        int64_t *start = static_cast<int64_t *>(scratch);
+        int64_t *start = static_cast<int64_t *>(ws);
         uint32_t *partial = reinterpret_cast<uint32_t *>(start + 257);
         uint8_t *x = static_cast<uint8_t *>(data);
         hipLaunchKernelGGL(hist_u8_kernel, dim3(hblocks), dim3(256), 0, s, x, n, head, nvec, partial);
@@ -338,6 +660,7 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
     MPX_CHECK_ARG((reinterpret_cast<uintptr_t>(data) & 3u) == 0, "int32/float32 data must be 4-byte aligned");
     uint32_t *x = static_cast<uint32_t *>(data);
     const int is_float = dtype == MPX_SORT_F32;
+    if (use_radix(n)) return radix_sort32(x, n, is_float ? kRawF32 : kRawI32, ws, variant, s);
     hipLaunchKernelGGL(to_keys_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, n, is_float);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     const int rc = sort_keys(x, n, s);
@@ -347,8 +670,37 @@ int sort_impl(void *data, int64_t n, int dtype, void *stream) {
     return MPX_OK;
 }
 
+// Convenience form without a caller workspace (tools, one-off sorts): the
+// scratch is allocated for this call and freed after the stream drains.
+int sort_alloc(void *data, int64_t n, int dtype, void *stream) {
+    const int64_t bytes = sort_workspace_bytes(std::max<int64_t>(n, 0), dtype);
+    void *ws = nullptr;
+    if (bytes > 0) MPX_RETURN_IF_HIP_ERROR(hipMalloc(&ws, (size_t)bytes));
+    const int rc = sort_impl(data, n, dtype, ws, bytes, stream);
+    if (ws) {
+        const hipError_t e = hipStreamSynchronize(as_stream(stream));
+        (void)hipFree(ws);
+        MPX_RETURN_IF_HIP_ERROR(e);
+    }
+    return rc;
+}
+
 MPX_MODULE_ANCHOR(sort)
 
 }  // namespace mpx
 
-extern "C" int mpx_sort(void *data, int64_t n, int dtype, void *stream) { return mpx::sort_impl(data, n, dtype, stream); }
+extern "C" int mpx_sort(void *data, int64_t n, int dtype, void *stream) { return mpx::sort_alloc(data, n, dtype, stream); }
+
+extern "C" int64_t mpx_sort_workspace_bytes(int64_t n, int dtype) { return mpx::sort_workspace_bytes(n, dtype); }
+
+extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, void *stream) {
+    return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream);
+}
+
+// Tuning entry (tools/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
+// (decoupled look-back), 2 = reduce-then-scan.
+extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
+                                void *stream) {
+    if (variant < 0 || variant > 2) return MPX_ERR_ARG;
+    return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
+}

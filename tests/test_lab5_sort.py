@@ -94,11 +94,12 @@ def test_sort_rejects_bad_dtype():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 4095, 4096, 4097, 8192, 12289, 100_003, (1 << 20) + 7])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 4095, 4096, 4097, 8191, 8192, 8193, 12289, 100_003, (1 << 20) + 7,
+                               (1 << 22) + 3])
 def test_gpu_sort_matches_cpu(gpu, kind, n):
-    """Every tile / global-step boundary: sizes around the 4096-key LDS tile,
-    non-powers of two (virtual +inf padding) and a 2^20 + 7 array (9 stages
-    beyond the tile)."""
+    """Path and tile boundaries: the one-launch LDS bitonic network up to 4096
+    keys, the radix sort above (8192-key tiles: a partial last tile, exactly
+    one and just over one tile), and multi-thousand-tile look-back chains."""
     a = random_array(kind, n, seed=n + 1)
     d = torch.from_numpy(a.copy()).to(gpu)
     ops.sort_(d)
@@ -159,3 +160,95 @@ def test_gpu_sort_u8_unaligned(gpu, offset, n):
     got = d.cpu().numpy()
     assert got[:offset].tobytes() == a[:offset].tobytes()
     assert got[offset:].tobytes() == np.sort(a[offset:]).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["equal", "sorted", "reversed", "two_values", "high_byte_only"])
+def test_gpu_radix_sort_patterns(gpu, pattern):
+    """Radix-specific digit distributions: a single digit value in every pass
+    (all keys in one bucket: the look-back carries whole-tile counts), already
+    sorted / reversed input (stability of the per-wave ranking), keys that
+    differ only in the top byte (three passes are pure stable copies)."""
+    n = 300_007
+    rng = np.random.default_rng(5)
+    if pattern == "equal":
+        a = np.full(n, -7, dtype=np.int32)
+    elif pattern == "sorted":
+        a = np.sort(rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32))
+    elif pattern == "reversed":
+        a = np.sort(rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32))[::-1].copy()
+    elif pattern == "two_values":
+        a = rng.choice(np.array([3, -3], dtype=np.int32), n)
+    else:
+        a = (rng.integers(0, 256, n, dtype=np.int64) << 24).astype(np.uint32).view(np.int32)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    ops.sort_(d)
+    assert d.cpu().numpy().tobytes() == np.sort(a).tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_sort_is_stable_on_float_ties(gpu):
+    """-0.0 and +0.0 are distinct keys; equal bit patterns keep their order —
+    checked through the byte patterns of a tie-heavy float array."""
+    n = 200_003
+    rng = np.random.default_rng(9)
+    a = rng.choice(np.array([0.0, -0.0, 1.5, -1.5, np.inf], dtype=np.float32), n)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    ops.sort_(d)
+    assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_sorts_on_two_streams_do_not_share_scratch(gpu):
+    """Scratch comes from the caller (torch's caching allocator on each
+    tensor's stream): two sorts in flight on different streams stay
+    independent (round-1 advisor finding on the shared per-device scratch)."""
+    xs = [torch.randint(0, 256, (3_000_000,), dtype=torch.uint8, device=gpu),
+          torch.randint(-2**31, 2**31 - 1, (3_000_000,), dtype=torch.int32, device=gpu),
+          torch.randint(0, 256, (2_000_001,), dtype=torch.uint8, device=gpu),
+          torch.randint(-2**31, 2**31 - 1, (2_000_001,), dtype=torch.int32, device=gpu)]
+    refs = [torch.sort(x).values for x in xs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(gpu) for _ in xs]
+    for x, st in zip(xs, streams):
+        with torch.cuda.stream(st):
+            for _ in range(3):
+                ops.sort_(x)
+    torch.cuda.synchronize()
+    for x, r in zip(xs, refs):
+        assert torch.equal(x, r)
+
+
+@pytest.mark.gpu
+def test_gpu_sort_workspace_contract(gpu):
+    """mpx_sort_ws refuses a workspace smaller than mpx_sort_workspace_bytes."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    n = 100_000
+    need = int(L.mpx_sort_workspace_bytes(n, 0))
+    assert need >= 4 * n
+    assert int(L.mpx_sort_workspace_bytes(4096, 0)) == 0  # single-tile bitonic path needs none
+    x = torch.zeros(n, dtype=torch.int32, device=gpu)
+    ws = torch.empty(need - 16, dtype=torch.uint8, device=gpu)
+    rc = L.mpx_sort_ws(x.data_ptr(), n, 0, ws.data_ptr(), need - 16, _native.stream_of(x))
+    assert rc != 0 and b"workspace" in L.mpx_last_error()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("kind", ["int", "float"])
+@pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7])
+def test_gpu_radix_variants(gpu, variant, kind, n):
+    """Both radix schedules (1 onesweep look-back, 2 reduce-then-scan) against
+    the total order, independent of which one AUTO picks at this size."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    dt = {"int": 0, "float": 1}[kind]
+    a = random_array(kind, n, seed=n + variant)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    nb = int(L.mpx_sort_workspace_bytes(n, dt))
+    ws = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    _native.check(L.mpx_sort_variant(d.data_ptr(), n, dt, ws.data_ptr(), nb, variant, _native.stream_of(d)))
+    assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()

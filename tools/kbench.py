@@ -3,7 +3,7 @@
 interleaved rounds (cdna_hip_programming.md §5.4 rule 24) on random 4096^2
 RGBA8 data, and checks every variant bit-exact against the production kernel.
 
-  python tools/kbench.py [--size 4096] [--rounds 5] [--iters 20]
+  python tools/kbench.py [--size 4096] [--rounds 5] [--iters 20] [--rotate R]
 """
 
 import argparse
@@ -18,12 +18,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cuda_mpi_openmp_amd import _native, ops  # noqa: E402
 
 
-def time_launch(fn, iters):
+def time_launch(fn, iters, cyc):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
     torch.cuda.synchronize()
     s.record()
     for _ in range(iters):
+        cyc[0] += 1
         fn()
     e.record()
     e.synchronize()
@@ -35,13 +36,28 @@ def main():
     p.add_argument("--size", type=int, default=4096)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--rotate", type=int, default=1, help="input/output pairs cycled per launch (>= 3 at 4096^2 "
+                                                          "defeats the MALL)")
     p.add_argument("--only", default="", help="run only the variants whose name contains this string")
     args = p.parse_args()
     L = _native.lib()
     dev = torch.device("cuda:0")
     n = args.size
-    img = torch.randint(0, 256, (n, n, 4), dtype=torch.uint8, device=dev)
-    out = torch.empty_like(img)
+    # --rotate R: R independent (input, output) pairs cycled launch by launch,
+    # so the working set (R x 128 MiB at 4096^2) exceeds the 256 MB MALL and
+    # every launch streams from HBM (cache-assisted floors)
+    pairs = []
+    for r in range(max(1, args.rotate)):
+        a = torch.randint(0, 256, (n, n, 4), dtype=torch.uint8, device=dev)
+        pairs.append((a, torch.empty_like(a)))
+    img, out = pairs[0]
+    cyc = [0]
+
+    def I():  # noqa: E743
+        return pairs[cyc[0] % len(pairs)][0]
+
+    def O():  # noqa: E743
+        return pairs[cyc[0] % len(pairs)][1]
     bytes_moved = 2 * img.numel()
 
     # exhaustive fast-sqrt equivalence check
@@ -57,57 +73,57 @@ def main():
         ref = ops.conv(img, f)
 
         def mk(kind, p1, p2, fast, wx=wx, wy=wy, k=k):
-            return lambda: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, k, kind, p1, p2, fast,
+            return lambda: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, k, kind, p1, p2, fast,
                                                             wx, wy, 0))
 
         for seg in (8, 16, 32, 64):
             variants[f"{fname}/wave-rt/seg{seg}"] = (mk(1, seg, 0, 1), ref)
             variants[f"{fname}/wave-const/seg{seg}"] = (mk(2, seg, 0, 1), ref)
         variants[f"{fname}/lds-stream/rpt4"] = (mk(0, 4, 0, 1), ref)
-        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ref)
-        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ref)
+        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(I(), f, O())), ref)
+        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(I(), f, O(), direct=True)), ref)
     fs5 = ops.get_filter("sobel5")
     swx, swy = fs5.c_taps()
     sref = ops.conv(img, fs5)
     for seg in (0, 8, 20, 24):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
-                (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5,
+                (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5,
                                                                              kind, seg, 0, 1, swx, swy, 0))), sref)
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
-            (lambda seg=seg: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg, 1000, 1,
+            (lambda seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 1000, 1,
                                                               swx, swy, 0))), sref)
     for seg, per in ((0, 0), (0, 3), (0, 5), (0, 6), (8, 0), (12, 0), (16, 0), (24, 0), (32, 0)):
         variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
-            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 5, seg,
+            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 5, seg,
                                                                        per, 1, swx, swy, 0))), sref)
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
     for p2, nm in ((0, "buffer"), (1, "global"), (2, "global-nt")):  # row-load A/B
         variants[f"sobel5-sep/loads-{nm}"] = (
-            (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 6, 0, p2, 1,
+            (lambda p2=p2: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, p2, 1,
                                                             swx, swy, 0))), sref)
         variants[f"roberts/loads-{nm}"] = (
-            (lambda p2=p2: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 2, 7, 0, p2, 1,
+            (lambda p2=p2: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 2, 7, 0, p2, 1,
                                                             rwx, rwy, 0))), rref)
     for pf in (4, 8, 12):  # prefetch ring depth (D = 5 / 10 / 15 rows)
         for seg in (0, 16, 24, 32, 40):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
-                (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(img.data_ptr(), out.data_ptr(), n, n, 5, 3, seg,
+                (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg,
                                                                          pf, 1, swx, swy, 0))), sref)
     for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
         f = ops.get_filter(fname)
-        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(img, f, out)), ops.conv(img, f))
-        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(img, f, out, direct=True)), ops.conv(img, f))
-    variants["copy/torch"] = ((lambda: out.copy_(img)), img)
+        variants[f"{fname}/production"] = ((lambda f=f: ops.conv(I(), f, O())), ops.conv(img, f))
+        variants[f"{fname}/direct"] = ((lambda f=f: ops.conv(I(), f, O(), direct=True)), ops.conv(img, f))
+    variants["copy/torch"] = ((lambda: O().copy_(I())), img)
     for v, d, seg in ((2, 4, 8), (2, 4, 24), (2, 8, 24), (4, 4, 8), (4, 4, 24), (4, 8, 24), (4, 2, 24), (4, 4, 48)):
         variants[f"copy/strip-v{v}-d{d}-seg{seg}"] = (
-            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(img.data_ptr(), out.data_ptr(), n, n, v, d,
+            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
                                                                             seg, 0))), img)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
-        variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(img, out, geometry=g)), rob_ref)
+        variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
 
     if args.only:
         variants = {k: v for k, v in variants.items() if args.only in k}
@@ -118,6 +134,7 @@ def main():
         print(json.dumps({"production_vs_cpu": fname, "bit_exact": bool(torch.equal(ops.conv(img, fname).cpu(), cpu))}),
               flush=True)
     for name, (fn, ref) in variants.items():
+        cyc[0] = 0
         out.zero_()
         fn()
         torch.cuda.synchronize()
@@ -127,7 +144,7 @@ def main():
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
         for name, (fn, _) in variants.items():
-            times[name].append(time_launch(fn, args.iters))
+            times[name].append(time_launch(fn, args.iters, cyc))
     for name, ts in times.items():
         med = statistics.median(ts)
         print(json.dumps({"variant": name, "us_median": round(med, 2), "us_min": round(min(ts), 2),
