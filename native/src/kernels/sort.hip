@@ -12,8 +12,8 @@
 //         (LDS atomics per block, one global atomic per bin and block);
 //       - each digit pass is ONE kernel: a block takes the next 8192-key tile
 //         from an atomic tile counter, ranks its keys stably in LDS (per-wave
-//         8-ballot match of equal digits, mbcnt for the rank among lower
-//         lanes, per-wave digit counters), publishes its 256 digit counts and
+//         peer masks of equal digits from an LDS OR table, mbcnt for the rank
+//         among lower lanes, per-wave digit counters), publishes its 256 digit counts and
 //         resolves its global digit offsets by decoupled look-back over the
 //         preceding tiles (flag + count packed in one 32-bit word, so a single
 //         relaxed agent-scope store publishes both), then stages the tile in
@@ -324,14 +324,16 @@ __device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t *s_wsum) {
     return x - v + add;
 }
 
-// 8-ballot match: the lanes of `valid` keys whose digit equals this lane's
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
-    uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const uint64_t bal = __ballot(valid && ((d >> b) & 1u));
-        m &= ((d >> b) & 1u) ? bal : ~bal;
-    }
+// Peer mask of equal digits within a wave through a wave-private LDS table of
+// 256 lane masks: every lane ORs its bit into its digit's slot, reads the slot
+// back and clears it (LDS ops of one wave execute in order; OR commutes, so
+// the mask is deterministic whatever order the lanes land in). Three LDS ops
+// per 64 keys instead of an 8-ballot VALU match (~50 VALU per 64 keys), which
+// made the rank instruction-bound.
+__device__ __forceinline__ uint64_t match_digit_lds(uint32_t d, int lane, uint64_t *tbl) {
+    atomicOr(reinterpret_cast<unsigned long long *>(&tbl[d]), 1ull << lane);
+    const uint64_t m = tbl[d];
+    tbl[d] = 0;
     return m;
 }
 
@@ -346,24 +348,31 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // offs[d][tile] = keys of digit d in the tiles before this one, tot[d] = keys
 // of digit d in the array).
 template <bool LOOKBACK>
-__global__ __launch_bounds__(kRThreads) void radix_pass_kernel(const uint32_t *__restrict__ in,
+__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(6))) void radix_pass_kernel(const uint32_t *__restrict__ in,
                                                                uint32_t *__restrict__ out, int64_t n, int shift,
                                                                int in_mode, int out_mode,
                                                                const uint32_t *__restrict__ hist,
                                                                uint32_t *__restrict__ status,
                                                                uint32_t *__restrict__ tile_ctr,
                                                                uint32_t *__restrict__ err, int ntiles) {
+    // s_keys (scatter staging) doubles as the per-wave peer-mask tables
+    // (8 x 256 x 8 B) used only while ranking: 43 KB of LDS per block
     __shared__ uint32_t s_keys[kRTile];
     __shared__ uint32_t s_cnt[kRWaves][256];  // per-wave digit counts, then exclusive offsets
     __shared__ uint32_t s_dstart[256];        // tile-local start of each digit
     __shared__ uint32_t s_gbase[256];         // global position of digit d's run minus s_dstart[d]
     __shared__ uint32_t s_wsum[4];
     __shared__ uint32_t s_tile;
+    static_assert(kRWaves * 256 * 2 <= kRTile, "peer-mask tables must fit in the staging buffer");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t *tbl = reinterpret_cast<uint64_t *>(s_keys) + w * 256;
     if constexpr (LOOKBACK) {
         if (t == 0) s_tile = atomicAdd(tile_ctr, 1u);
     }
-    for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+    for (int i = t; i < kRWaves * 256; i += kRThreads) {
+        (&s_cnt[0][0])[i] = 0;
+        reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
+    }
     __syncthreads();
     const uint32_t tile = LOOKBACK ? s_tile : (uint32_t)xcd_remap(blockIdx.x, gridDim.x);
     const int64_t base = (int64_t)tile * kRTile + w * kRWaveKeys + lane;
@@ -374,15 +383,39 @@ __global__ __launch_bounds__(kRThreads) void radix_pass_kernel(const uint32_t *_
         const int64_t i = base + e * 64;
         key[e] = i < n ? to_key(in[i], in_mode) : 0xffffffffu;  // pads rank last and are never stored
     }
-    // stable rank within the wave: slices in index order, lanes in order
+    // reduce-then-scan: this tile's offsets and the digit totals are known
+    // up front — issue their loads now, under the ranking
+    uint32_t pre_excl = 0, pre_tot = 0;
+    if constexpr (!LOOKBACK) {
+        if (t < 256) {
+            pre_excl = status[(size_t)t * ntiles + tile];  // offs[d][tile]
+            pre_tot = hist[t];
+        }
+    }
+    // Stable rank within the wave (slices in index order, lanes in order),
+    // batched so the LDS round trips overlap: (1) every slice's peer mask,
+    // (2) one leader per digit and slice adds the slice's count to the wave
+    // counter (ds_add_rtn; same-wave LDS ops land in program order, so slice
+    // e sees exactly slices < e), (3) peers take the leader's old count.
+    // groups of kRG slices bound the live peer masks (VGPR pressure)
+    constexpr int kRG = 4;
 #pragma unroll
-    for (int e = 0; e < kRPer; ++e) {
-        const uint32_t d = (key[e] >> shift) & 255u;
-        const uint64_t m = match_digit(d, true);
-        const uint32_t pre = lanes_below(m);
-        const uint32_t old = s_cnt[w][d];
-        if (pre == 0) s_cnt[w][d] = old + (uint32_t)__popcll(m);
-        rank[e] = old + pre;
+    for (int g = 0; g < kRPer; g += kRG) {
+        uint64_t m[kRG];
+#pragma unroll
+        for (int e = 0; e < kRG; ++e) m[e] = match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
+        uint32_t old[kRG], pre[kRG];
+#pragma unroll
+        for (int e = 0; e < kRG; ++e) {
+            pre[e] = lanes_below(m[e]);
+            old[e] = 0;
+            if (pre[e] == 0) old[e] = atomicAdd(&s_cnt[w][(key[g + e] >> shift) & 255u], (uint32_t)__popcll(m[e]));
+        }
+#pragma unroll
+        for (int e = 0; e < kRG; ++e) {
+            const int leader = (int)__builtin_ctzll(m[e]);
+            rank[g + e] = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old[e]) + pre[e];
+        }
     }
     __syncthreads();
     uint32_t tot = 0;
@@ -421,12 +454,12 @@ __global__ __launch_bounds__(kRThreads) void radix_pass_kernel(const uint32_t *_
                 __hip_atomic_store(st, kFlagP | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else {
-            excl = status[(size_t)t * ntiles + tile];  // offs[d][tile]
+            excl = pre_excl;
         }
         s_gbase[t] = excl;  // + digit base - tile-local start, below
     }
     const uint32_t dstart = scan256_excl(tot, s_wsum);
-    const uint32_t dbase = scan256_excl(t < 256 ? hist[t] : 0u, s_wsum);
+    const uint32_t dbase = scan256_excl(t < 256 ? (LOOKBACK ? hist[t] : pre_tot) : 0u, s_wsum);
     if (t < 256) {
         s_dstart[t] = dstart;
         s_gbase[t] += dbase - dstart;
@@ -446,7 +479,8 @@ __global__ __launch_bounds__(kRThreads) void radix_pass_kernel(const uint32_t *_
     }
 }
 
-// reduce-then-scan, step 1: the tile's digit counts, digit-major
+// reduce-then-scan, step 1: the tile's digit counts (per-wave LDS atomics,
+// order irrelevant), digit-major
 // (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
 // 4-byte stores into whole lines
 constexpr int kCThreads = 256;
@@ -466,12 +500,8 @@ __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *
         key[e] = i < n ? in[i] : 0u;
     }
 #pragma unroll
-    for (int e = 0; e < kCPer; ++e) {
-        const bool valid = base + e * 64 < n;
-        const uint32_t d = (to_key(key[e], mode) >> shift) & 255u;
-        const uint64_t m = match_digit(d, valid);
-        if (valid && lanes_below(m) == 0) h[w][d] += (uint32_t)__popcll(m);  // one leader per digit
-    }
+    for (int e = 0; e < kCPer; ++e)
+        if (base + e * 64 < n) atomicAdd(&h[w][(to_key(key[e], mode) >> shift) & 255u], 1u);
     __syncthreads();
     uint32_t c = 0;
 #pragma unroll
@@ -544,7 +574,7 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
 // reduce-then-scan re-reads each tile once more but never waits.
-constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;
+constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
