@@ -285,24 +285,91 @@ static int cmp_u32(const void *a, const void *b) {
     return (x > y) - (x < y);
 }
 
+#ifdef _OPENMP
+/* OpenMP build: T sorted runs (qsort per thread), then log2(T) rounds of
+ * pairwise merges, each round's merges in parallel. */
+static void merge_u32(const uint32_t *a, int64_t na, const uint32_t *b, int64_t nb, uint32_t *out) {
+    int64_t i = 0, j = 0, o = 0;
+    while (i < na && j < nb) out[o++] = b[j] < a[i] ? b[j++] : a[i++];
+    while (i < na) out[o++] = a[i++];
+    while (j < nb) out[o++] = b[j++];
+}
+
+static int sort_u32_parallel(uint32_t *x, int64_t n) {
+    int runs = omp_get_max_threads();
+    if (runs < 2 || n < (1 << 16)) return 0;
+    uint32_t *tmp = (uint32_t *)malloc((size_t)n * sizeof(uint32_t));
+    int64_t *bound = (int64_t *)malloc((size_t)(runs + 1) * sizeof(int64_t));
+    if (!tmp || !bound) {
+        free(tmp);
+        free(bound);
+        return 0;
+    }
+    for (int r = 0; r <= runs; ++r) bound[r] = n * r / runs;
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < runs; ++r) qsort(x + bound[r], (size_t)(bound[r + 1] - bound[r]), sizeof(uint32_t), cmp_u32);
+    uint32_t *src = x, *dst = tmp;
+    for (int width = 1; width < runs; width *= 2) {
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int r = 0; r < runs; r += 2 * width) {
+            const int mid = r + width < runs ? r + width : runs;
+            const int end = r + 2 * width < runs ? r + 2 * width : runs;
+            merge_u32(src + bound[r], bound[mid] - bound[r], src + bound[mid], bound[end] - bound[mid], dst + bound[r]);
+        }
+        uint32_t *t = src;
+        src = dst;
+        dst = t;
+    }
+    if (src != x) memcpy(x, src, (size_t)n * sizeof(uint32_t));
+    free(tmp);
+    free(bound);
+    return 1;
+}
+#endif
+
 void mpx_cpu_sort(void *data, int64_t n, int dtype) {
     if (n < 2) return;
-    if (dtype == MPX_SORT_U8) { /* counting sort */
+    if (dtype == MPX_SORT_U8) { /* counting sort (per-thread histograms in the OpenMP build) */
         uint8_t *x = (uint8_t *)data;
         int64_t cnt[256] = {0};
+#ifdef _OPENMP
+#pragma omp parallel
+        {
+            int64_t local[256] = {0};
+#pragma omp for schedule(static) nowait
+            for (int64_t i = 0; i < n; ++i) local[x[i]]++;
+#pragma omp critical
+            for (int v = 0; v < 256; ++v) cnt[v] += local[v];
+        }
+        int64_t start[257];
+        start[0] = 0;
+        for (int v = 0; v < 256; ++v) start[v + 1] = start[v] + cnt[v];
+#pragma omp parallel for schedule(dynamic, 8)
+        for (int v = 0; v < 256; ++v) memset(x + start[v], v, (size_t)cnt[v]);
+#else
         for (int64_t i = 0; i < n; ++i) cnt[x[i]]++;
         int64_t o = 0;
         for (int v = 0; v < 256; ++v)
             for (int64_t c = 0; c < cnt[v]; ++c) x[o++] = (uint8_t)v;
+#endif
         return;
     }
     uint32_t *x = (uint32_t *)data;
     const int is_float = dtype == MPX_SORT_F32;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
     for (int64_t i = 0; i < n; ++i) {
         const uint32_t v = x[i];
         x[i] = is_float ? (v ^ ((uint32_t)((int32_t)v >> 31) | 0x80000000u)) : (v ^ 0x80000000u);
     }
-    qsort(x, (size_t)n, sizeof(uint32_t), cmp_u32);
+#ifdef _OPENMP
+    if (!sort_u32_parallel(x, n))
+#endif
+        qsort(x, (size_t)n, sizeof(uint32_t), cmp_u32);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
     for (int64_t i = 0; i < n; ++i) {
         const uint32_t k = x[i];
         x[i] = is_float ? (k ^ ((k >> 31) ? 0x80000000u : 0xffffffffu)) : (k ^ 0x80000000u);

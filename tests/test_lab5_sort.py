@@ -59,8 +59,10 @@ def test_fixtures_parse(kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 1000, 4097])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 10, 1000, 4097, 200_003])
 def test_cpu_sort_matches_total_order(kind, n):
+    """libmpx's CPU path is the OpenMP build: n >= 2^16 takes the parallel
+    run-sort + pairwise-merge path (uint8: per-thread histograms)."""
     a = random_array(kind, n, seed=n)
     t = torch.from_numpy(a.copy())
     ops.sort_(t)
@@ -79,6 +81,18 @@ def test_lab5_cpu_program_on_fixtures(exe, kind):
     assert head.startswith(b"CPU execution time: <")
     a = read_fixture(path, kind)
     assert payload == np.sort(a).tobytes()
+
+
+@pytest.mark.parametrize("exe", ["cpu_exe", "cpu_omp_exe"])
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_lab5_cpu_program_large(exe, kind):
+    """Serial -O0 and OpenMP builds agree with the total order on an array
+    large enough for the parallel merge path."""
+    a = random_array(kind, 300_007, seed=11)
+    r = subprocess.run([os.path.join(ROOT, "labs/lab5/src", exe), kind], input=fixture_bytes(kind, a),
+                       capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.partition(b"\n")[2] == total_order_sorted(a).tobytes()
 
 
 def test_lab5_cpu_program_rejects_short_input():
