@@ -4,7 +4,17 @@ stencil, 16384^2 grid domain-decomposed across 8 MI355X, halo exchange over
 xGMI"). The reference has no such solver; this is its MI355X-native
 form.
 
-Per iteration and rank:
+Halo transports (``halo=``):
+
+* ``"peer"`` (GPU, default when available): one-sided and device-signalled.
+  Each rank IPC-maps its neighbours' u/u_new buffers and completed-iteration
+  words once; every iteration is ONE sweep kernel whose slab-edge waves wait
+  on the neighbours' counters, read their boundary rows over xGMI and publish
+  this rank's counter (native/src/kernels/jacobi.hip, ``parallel.peer.
+  JacobiPeerLink``). No exchange kernel, no host round trip per iteration.
+* ``"rccl"``: two-sided send/recv of the edge rows (below).
+
+RCCL transport, per iteration and rank:
   1. sweep the two slab-edge rows (the only rows a neighbour needs);
   2. post the halo exchange of those freshly computed rows over RCCL
      (point-to-point on the xGMI link between neighbouring GPUs);
@@ -21,6 +31,7 @@ fixed. A decomposed run is bit-identical to a one-rank run.
 
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Optional
 
 import torch
@@ -35,7 +46,7 @@ from ..parallel.slab import Slab
 
 class SlabJacobi:
     def __init__(self, ctx: DistContext, global_rows: int, cols: int, dtype=torch.float64, check_every: int = 10,
-                 overlap: bool | str = "auto"):
+                 overlap: bool | str = "auto", halo: str = "auto"):
         if cols < 3:
             raise ValueError("need at least 3 columns")
         self.ctx = ctx
@@ -50,8 +61,41 @@ class SlabJacobi:
         self.halo = HaloExchange(self.slab, ctx)
         shape = (self.slab.buffer_rows, cols)
         dev = ctx.device
-        self.u = torch.zeros(shape, dtype=dtype, device=dev)
-        self.un = torch.zeros(shape, dtype=dtype, device=dev)
+        if halo not in ("auto", "peer", "rccl", "none"):
+            raise ValueError(f"unknown halo transport {halo!r}")
+        # "none": benchmarking ablation only — ranks sweep their slabs with no
+        # halo exchange at all (wrong answer, same per-rank work): the
+        # difference to "peer" is the cost of the device-side ordering and the
+        # xGMI halo reads
+        self.no_halo = halo == "none"
+        if self.no_halo:
+            self.overlap = False
+        self.peer = None
+        if halo not in ("rccl", "none") and ctx.is_distributed and dev.type == "cuda":
+            # two allocations (buffer 0 + the sync block, buffer 1), each shared by IPC
+            from .. import _native
+            from ..parallel.peer import try_jacobi_peer
+
+            nel = shape[0] * shape[1]
+            es = torch.empty(0, dtype=dtype).element_size()
+            sync_el = max(1, 512 // es)
+            self._storages = [torch.zeros(nel + sync_el, dtype=dtype, device=dev),
+                              torch.zeros(nel, dtype=dtype, device=dev)]
+            self.u = self._storages[0][:nel].view(shape)
+            self.un = self._storages[1].view(shape)
+            sync = self._storages[0][nel:nel + sync_el].view(torch.int32)
+            assert sync.numel() * 4 >= _native.lib().mpx_jacobi_sync_bytes()
+            nv = 16 // es
+            layout_ok = cols % nv == 0 and self.u.data_ptr() % 16 == 0 and self.un.data_ptr() % 16 == 0
+            self.peer = try_jacobi_peer(ctx, self.slab, self._storages, [self.u, self.un], sync, layout_ok)
+            if self.peer is None and halo == "peer":
+                raise RuntimeError("peer halo transport unavailable (IPC mapping failed or cols not a multiple of "
+                                   f"{nv})")
+        else:
+            if halo == "peer":
+                raise RuntimeError("peer halos need a distributed GPU run")
+            self.u = torch.zeros(shape, dtype=dtype, device=dev)
+            self.un = torch.zeros(shape, dtype=dtype, device=dev)
         self.resid = torch.zeros(1, dtype=dtype, device=dev)
         self.iteration = 0
         self.last_residual: Optional[float] = None
@@ -82,12 +126,34 @@ class SlabJacobi:
         self.un.copy_(self.u)
         self._halos_valid = False
 
+    @property
+    def transport(self) -> Optional[str]:
+        if not self.ctx.is_distributed:
+            return None
+        if self.no_halo:
+            return "none (ablation: no halo exchange)"
+        if self.peer is not None:
+            return "xgmi-peer-signalled"
+        return "native-rccl" if self.ctx.native is not None else "torch.distributed"
+
     def sync_halos(self) -> None:
         """Exchange u's slab-edge rows (needed once after (re)initialisation;
-        afterwards every step refreshes the halos of the rows it computes)."""
+        afterwards every step refreshes the halos of the rows it computes).
+        Peer mode: publish the buffers and reset every rank's iteration word."""
+        if self.peer is not None or self.no_halo:
+            self.un.copy_(self.u)
+            if self.peer is not None:
+                self.peer.publish(self.u, self.iteration)
+            self._halos_valid = True
+            return
         self.halo.exchange(self.u)
         self.un.copy_(self.u)
         self._halos_valid = True
+
+    def check_peer(self) -> None:
+        """Raise when a device-side halo wait gave up (a neighbour stalled)."""
+        if self.peer is not None and self.peer.timed_out():
+            raise RuntimeError(f"rank {self.ctx.rank}: peer halo wait timed out at iteration ~{self.iteration}")
 
     @property
     def owned(self) -> torch.Tensor:
@@ -112,6 +178,7 @@ class SlabJacobi:
         self._advance(track)
         if track:
             self.last_residual = float(self.resid.item())
+            self.check_peer()
             return self.last_residual
         return None
 
@@ -123,7 +190,13 @@ class SlabJacobi:
         n = s.rows
         if track:
             self.resid.zero_()
-        if self.ctx.is_distributed and self.overlap:
+        if self.peer is not None:
+            from .. import _native
+
+            _native.check(_native.lib().mpx_jacobi_peer_sweep(
+                int(self.dtype == torch.float64), self.u.data_ptr(), self.un.data_ptr(), self.cols, self.cols, n,
+                self.resid.data_ptr() if track else None, ctypes.byref(self.peer.desc), _native.stream_of(self.u)))
+        elif self.ctx.is_distributed and self.overlap:
             edge = [1] if n == 1 else [1, n]
             for r in edge:
                 self._sweep(r, r + 1, track)
@@ -132,7 +205,8 @@ class SlabJacobi:
             self.halo.wait()
         else:
             self._sweep(1, n + 1, track)
-            self.halo.exchange(self.un)
+            if not self.no_halo:
+                self.halo.exchange(self.un)
         self.u, self.un = self.un, self.u
         self.iteration += 1
         if track:
@@ -201,6 +275,7 @@ class SlabJacobi:
             self.iteration += self.check_every
             done += self.check_every
             self.last_residual = float(self.resid.item())
+            self.check_peer()
             if tol is not None and self.last_residual < tol:
                 return -1
         return done
@@ -215,6 +290,13 @@ class SlabJacobi:
         torch.save({"u": self.u.cpu(), "iteration": self.iteration, "residual": self.last_residual,
                     "global_rows": self.slab.global_rows, "world": self.ctx.world, "cols": self.cols}, path)
         return path
+
+    def close(self) -> None:
+        """Unmap the neighbours' buffers (peer mode)."""
+        if self.peer is not None:
+            torch.cuda.synchronize(self.u.device)
+            self.peer.close()
+            self.peer = None
 
     def load_checkpoint(self, prefix: str) -> None:
         ck = torch.load(f"{prefix}.rank{self.ctx.rank}.pt", weights_only=True)

@@ -22,24 +22,32 @@ def _native_ok(x: torch.Tensor, ctx: DistContext) -> bool:
         torch.float64, torch.float32, torch.int32)
 
 
+def _host_staged(x: torch.Tensor, ctx: DistContext) -> bool:
+    """A GPU tensor on a gloo control plane (one-GPU rehearsal): reduce a host copy."""
+    return x.is_cuda and ctx.backend != "nccl"
+
+
+def _all_reduce(x: torch.Tensor, ctx: DistContext, op, native_op: str) -> torch.Tensor:
+    if ctx.is_distributed:
+        if _native_ok(x, ctx):
+            ctx.native.all_reduce_(x, native_op)
+        elif _host_staged(x, ctx):
+            h = x.cpu()
+            dist.all_reduce(h, op=op)
+            x.copy_(h)
+        else:
+            dist.all_reduce(x, op=op)
+    return x
+
+
 def all_reduce_max(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     """In-place MAX over ranks, ordered on the current stream (native RCCL tier
     when available, torch.distributed otherwise)."""
-    if ctx.is_distributed:
-        if _native_ok(x, ctx):
-            ctx.native.all_reduce_(x, "max")
-        else:
-            dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    return x
+    return _all_reduce(x, ctx, dist.ReduceOp.MAX, "max")
 
 
 def all_reduce_sum(x: torch.Tensor, ctx: DistContext) -> torch.Tensor:
-    if ctx.is_distributed:
-        if _native_ok(x, ctx):
-            ctx.native.all_reduce_(x, "sum")
-        else:
-            dist.all_reduce(x, op=dist.ReduceOp.SUM)
-    return x
+    return _all_reduce(x, ctx, dist.ReduceOp.SUM, "sum")
 
 
 def max_over_ranks(value: float, ctx: DistContext) -> float:
@@ -87,6 +95,8 @@ def gather_slabs(own: torch.Tensor, slab: Slab, ctx: DistContext, dst: int = 0) 
     """
     if not ctx.is_distributed:
         return own
+    if _host_staged(own, ctx):
+        own = own.cpu()  # gloo control plane: the assembled array comes back on the host
     maxr = max(slab.rows_of(r) for r in range(slab.world))
     pad = torch.zeros((maxr,) + tuple(own.shape[1:]), dtype=own.dtype, device=own.device)
     pad[: own.shape[0]] = own

@@ -19,6 +19,7 @@ the BASELINE north star.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import torch
@@ -160,3 +161,154 @@ def try_peer_halo(ctx: DistContext, slab: Slab, own: torch.Tensor) -> Optional[P
         ph.close()
         return None
     return ph
+
+
+# --------------------------------------------------------------------------
+# Jacobi: one-sided halos with device-side ordering
+# --------------------------------------------------------------------------
+def _dbg(ctx: DistContext, msg: str) -> None:
+    if os.environ.get("MPX_DEBUG_PEER"):
+        import sys
+        import time
+
+        print(f"[peer r{ctx.rank} {time.monotonic():.3f}] {msg}", file=sys.stderr, flush=True)
+
+
+class _JacobiPeerDesc(ctypes.Structure):
+    """ctypes mirror of ``mpx_jacobi_peer`` (native/include/mpx/capi.h)."""
+
+    _fields_ = [("up_row", ctypes.c_void_p * 2), ("dn_row", ctypes.c_void_p * 2), ("up_flag", ctypes.c_void_p),
+                ("dn_flag", ctypes.c_void_p), ("sync", ctypes.c_void_p), ("spin_limit", ctypes.c_uint)]
+
+
+# hipIpcOpenMemHandle of one allocation above 2 GiB never returned on the
+# MI355X box (ROCm 7 dmabuf path; 2048.5 MiB hung, 1152 MiB mapped in ~1 ms),
+# so every IPC-shared allocation stays below this and larger slabs fall back
+# to RCCL with a message instead of hanging.
+IPC_MAX_BYTES = (2 << 30) - (64 << 20)
+
+
+class JacobiPeerLink:
+    """IPC links of one Jacobi rank to its neighbours' u/u_new buffers and
+    completed-iteration words (``mpx_jacobi_peer_sweep``).
+
+    ``storages`` are this rank's two allocations: the first holds ``bufs[0]``
+    and the sync block, the second ``bufs[1]`` (each (rows + 2) x cols), each
+    below IPC_MAX_BYTES. Each sweep's edge waves read the neighbours' boundary
+    rows over xGMI and wait on / publish the iteration counters on the device —
+    the host only launches one kernel per iteration (reference: none; SURVEY
+    §2.6 / §7.2 step 7 north star).
+    """
+
+    def __init__(self, ctx: DistContext, slab: Slab, storages: List[torch.Tensor], bufs: List[torch.Tensor],
+                 sync: torch.Tensor):
+        self.ctx = ctx
+        self.slab = slab
+        self.bufs = bufs
+        self.sync = sync
+        self.row_bytes = bufs[0][0].numel() * bufs[0].element_size()
+        self._bases: List[int] = []
+        for st in storages:
+            nb = st.numel() * st.element_size()
+            if nb > IPC_MAX_BYTES:
+                raise ValueError(f"slab allocation of {nb / 2**20:.0f} MiB exceeds the {IPC_MAX_BYTES >> 20} MiB IPC "
+                                 "mapping limit")
+        L = _native.lib()
+        mine = []
+        for st, parts in ((storages[0], (bufs[0], sync)), (storages[1], (bufs[1],))):
+            h = (ctypes.c_char * L.mpx_ipc_handle_size())()
+            off = ctypes.c_int64()
+            _native.check(L.mpx_ipc_get_handle(st.data_ptr(), h, ctypes.byref(off)))
+            mine.append((bytes(h), int(off.value) + (parts[0].data_ptr() - st.data_ptr()),
+                         (parts[1].data_ptr() - parts[0].data_ptr()) if len(parts) > 1 else None))
+        mine = (mine, slab.rows, self.row_bytes)
+        _dbg(ctx, "link: handles taken")
+        every: List[Optional[tuple]] = [None] * ctx.world
+        dist.all_gather_object(every, mine)
+        _dbg(ctx, "link: handles exchanged")
+        self._nb = {}
+        try:
+            for side, r in (("up", ctx.rank - 1), ("dn", ctx.rank + 1)):
+                if 0 <= r < ctx.world:
+                    (h0, b0, sy_rel), (h1, b1, _), rows, rb = every[r][0][0], every[r][0][1], every[r][1], every[r][2]
+                    if rb != self.row_bytes:
+                        raise ValueError("neighbour row pitch differs")
+                    p0 = self._open(h0) + b0
+                    p1 = self._open(h1) + b1
+                    _dbg(ctx, f"link: opened {side} neighbour")
+                    self._nb[side] = (p0, p1, p0 + sy_rel, rows)
+        except Exception:
+            self.close()
+            raise
+        self.desc = _JacobiPeerDesc()
+
+    def _open(self, handle: bytes) -> int:
+        L = _native.lib()
+        base = ctypes.c_void_p()
+        _native.check(L.mpx_ipc_open(handle, ctypes.byref(base)))
+        self._bases.append(int(base.value))
+        return int(base.value)
+
+    def publish(self, u: torch.Tensor, iteration: int) -> None:
+        """Collective, between sweeps: make this rank's buffers visible, set its
+        completed-iteration word to ``iteration`` (every rank passes the same
+        value) and rebuild the descriptor for the current u/u_new roles."""
+        torch.cuda.synchronize(u.device)
+        self.sync.zero_()
+        self.sync[0] = iteration
+        torch.cuda.synchronize(u.device)
+        # which buffer is u at even iterations, per rank
+        even = 0 if (u.data_ptr() == self.bufs[0].data_ptr()) == (iteration % 2 == 0) else 1
+        every: List[Optional[int]] = [None] * self.ctx.world
+        dist.all_gather_object(every, even)
+        d = _JacobiPeerDesc()
+        for side, r in (("up", self.ctx.rank - 1), ("dn", self.ctx.rank + 1)):
+            if side not in self._nb:
+                continue
+            b0, b1, sy, rows = self._nb[side]
+            bufs = (b0, b1) if every[r] == 0 else (b1, b0)
+            row = rows if side == "up" else 1  # its last / first owned row
+            ptrs = [b + row * self.row_bytes for b in bufs]
+            if side == "up":
+                d.up_row[0], d.up_row[1], d.up_flag = ptrs[0], ptrs[1], sy
+            else:
+                d.dn_row[0], d.dn_row[1], d.dn_flag = ptrs[0], ptrs[1], sy
+        d.sync = self.sync.data_ptr()
+        d.spin_limit = int(os.environ.get("MPX_PEER_SPIN_LIMIT", "0"))  # diagnostics: give up sooner
+        self.desc = d
+        self.ctx.barrier()
+
+    def timed_out(self) -> bool:
+        return bool(self.sync[64].item())
+
+    def close(self) -> None:
+        L = _native.lib()
+        for b in self._bases:
+            L.mpx_ipc_close(ctypes.c_void_p(b))
+        self._bases = []
+
+
+def try_jacobi_peer(ctx: DistContext, slab: Slab, storages: List[torch.Tensor], bufs: List[torch.Tensor],
+                    sync: torch.Tensor, layout_ok: bool) -> Optional[JacobiPeerLink]:
+    """Collective: a JacobiPeerLink on every rank, or None on every rank."""
+    if ctx.world < 2 or not storages[0].is_cuda or not dist.is_initialized():
+        return None
+    link, err = None, None
+    if not layout_ok:
+        err = "columns are not a multiple of the 16-byte vector width"
+    else:
+        try:
+            link = JacobiPeerLink(ctx, slab, storages, bufs, sync)
+        except Exception as e:  # noqa: BLE001 - reported below, then everyone falls back
+            err = f"{type(e).__name__}: {e}"
+    votes: List[Optional[bool]] = [None] * ctx.world
+    dist.all_gather_object(votes, link is not None)
+    if not all(votes):
+        if link is not None:
+            link.close()
+        if err is not None:
+            import sys
+
+            print(f"[peer-halo] rank {ctx.rank}: Jacobi IPC links unavailable ({err}); using RCCL", file=sys.stderr)
+        return None
+    return link

@@ -3,6 +3,7 @@
 //
 //   mpx_mgpu conv   [--gpus N] [--size S] [--filter sobel5] [--steps K] [--warmup W]
 //   mpx_mgpu jacobi [--gpus N] [--size S] [--iters K] [--warmup W] [--check-every C] [--fp32]
+//                   [--halo rccl|peer] [--shared]
 //   mpx_mgpu vsub   [--gpus N] [--n ELEMS_PER_GPU] [--steps K] [--warmup W] [--fp64]
 //
 // Each prints one JSON line (whole-job throughput, ms per step, verification).
@@ -19,6 +20,14 @@
 //   * global residual = ncclAllReduce(max) every --check-every iterations (the
 //     small-message latency over xGMI is paid once per check, not per sweep);
 //   * weak scaling: the per-GPU slab is fixed, the global problem grows with N.
+//   * jacobi --halo peer: one-sided, device-signalled halos instead of RCCL —
+//     each rank's sweep kernel reads the neighbours' edge rows straight from
+//     their buffers (P2P over xGMI) and orders itself on the neighbours'
+//     completed-iteration words (mpx_jacobi_peer_sweep); one launch per
+//     iteration, the residual max over ranks on the host every --check-every.
+//     --shared maps ranks r -> device r % ndev, so up to 4 ranks rehearse on
+//     one GPU (one HIP stream each; more would share hardware queues, and a
+//     waiting kernel would block a neighbour queued behind it).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -73,12 +82,15 @@ struct Args {
     std::string mode;
     int gpus = 0;  // 0: every visible device
     int size = 0;
+    int rows = 0;  // jacobi --halo peer: global rows (default --size)
     int steps = 0;
     int warmup = 5;
     int check_every = 10;
     long long n = 0;
     bool fp32 = false, fp64 = false;
+    bool shared = false;
     std::string filter = "sobel5";
+    std::string halo = "rccl";
 };
 
 Args parse(int argc, char **argv) {
@@ -100,6 +112,7 @@ Args parse(int argc, char **argv) {
         };
         if (k == "--gpus") a.gpus = atoi(val());
         else if (k == "--size") a.size = atoi(val());
+        else if (k == "--rows") a.rows = atoi(val());
         else if (k == "--steps" || k == "--iters") a.steps = atoi(val());
         else if (k == "--warmup") a.warmup = atoi(val());
         else if (k == "--check-every") a.check_every = std::max(1, atoi(val()));
@@ -107,6 +120,8 @@ Args parse(int argc, char **argv) {
         else if (k == "--filter") a.filter = val();
         else if (k == "--fp32") a.fp32 = true;
         else if (k == "--fp64") a.fp64 = true;
+        else if (k == "--shared") a.shared = true;
+        else if (k == "--halo") a.halo = val();
         else {
             fprintf(stderr, "unknown option %s\n", k.c_str());
             exit(2);
@@ -180,7 +195,11 @@ void cpu_sweep_f32(const float *u, float *un, int cols, int r0, int r1) {
 
 struct Shared {
     int world = 1;
+    int ndev = 1;
     ncclUniqueId id;
+    std::vector<void *> peer_u, peer_un;   // jacobi --halo peer: every rank's buffers
+    std::vector<unsigned *> peer_sync;     // and completed-iteration blocks
+    std::vector<double> res;               // per-rank residual at a check
     Barrier *bar = nullptr;
     std::vector<double> elapsed;  // seconds per rank
     std::vector<int> verified;    // 1 ok, 0 mismatch, -1 not checked
@@ -263,6 +282,114 @@ void conv_worker(const Args &a, Shared &sh, int rank) {
     HIP_OK(hipFree(out));
     HIP_OK(hipStreamDestroy(s));
     NCCL_CHECK(ncclCommDestroy(comm));
+}
+
+// ---------------------------------------------------------------- jacobi, peer halos
+template <typename T>
+void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
+    const int dev = rank % sh.ndev;
+    HIP_OK(hipSetDevice(dev));
+    hipStream_t s;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const int cols = a.size;
+    const int grows = a.rows > 0 ? a.rows : a.size;
+    const Slab sl(grows, sh.world, rank);
+    const long long rows = sl.rows;
+    const size_t row_bytes = (size_t)cols * sizeof(T);
+    const size_t bytes = (rows + 2) * row_bytes;
+    T *u, *un, *res;
+    unsigned *sync;
+    HIP_OK(hipMalloc(&u, bytes));
+    HIP_OK(hipMalloc(&un, bytes));
+    HIP_OK(hipMalloc(&res, sizeof(T)));
+    HIP_OK(hipMalloc(&sync, mpx_jacobi_sync_bytes()));
+    fill_unit<T><<<1024, 256, 0, s>>>(u, (rows + 2) * cols, 77 + rank);
+    HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
+    HIP_OK(hipMemsetAsync(sync, 0, mpx_jacobi_sync_bytes(), s));
+    HIP_OK(hipStreamSynchronize(s));
+    sh.peer_u[rank] = u;
+    sh.peer_un[rank] = un;
+    sh.peer_sync[rank] = sync;
+    sh.bar->wait();
+    mpx_jacobi_peer pr{};
+    pr.sync = sync;
+    for (int nb : {rank - 1, rank + 1}) {
+        if (nb < 0 || nb >= sh.world || a.halo == "none") continue;
+        const int nd = nb % sh.ndev;
+        if (nd != dev) {
+            const hipError_t e = hipDeviceEnablePeerAccess(nd, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
+            (void)hipGetLastError();
+        }
+        const Slab ns(grows, sh.world, nb);
+        const long long row = nb < rank ? ns.rows : 1;  // its last / first owned row
+        const void *even = static_cast<const T *>(sh.peer_u[nb]) + row * cols;  // every rank starts with u
+        const void *odd = static_cast<const T *>(sh.peer_un[nb]) + row * cols;
+        if (nb < rank) {
+            pr.up_row[0] = even, pr.up_row[1] = odd, pr.up_flag = sh.peer_sync[nb];
+        } else {
+            pr.dn_row[0] = even, pr.dn_row[1] = odd, pr.dn_flag = sh.peer_sync[nb];
+        }
+    }
+    int it = 0;
+    double last_res = -1;
+    auto iterate = [&]() {
+        const bool check = (it + 1) % a.check_every == 0;
+        MPX_OK_OR_DIE(mpx_jacobi_peer_sweep(sizeof(T) == 8, u, un, cols, cols, (int)rows, check ? res : nullptr, &pr, s));
+        std::swap(u, un);
+        if (check) {  // residual max over ranks on the host (no RCCL in this mode)
+            T h;
+            HIP_OK(hipMemcpyAsync(&h, res, sizeof(T), hipMemcpyDeviceToHost, s));
+            HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
+            HIP_OK(hipStreamSynchronize(s));
+            sh.res[rank] = (double)h;
+            sh.bar->wait();
+            last_res = *std::max_element(sh.res.begin(), sh.res.end());
+            sh.bar->wait();
+        }
+        ++it;
+    };
+    for (int i = 0; i < a.warmup; ++i) iterate();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    const auto t0 = Clock::now();
+    for (int i = 0; i < a.steps; ++i) iterate();
+    HIP_OK(hipStreamSynchronize(s));
+    sh.bar->wait();
+    sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
+    sh.extra[rank] = last_res;
+    unsigned err = 0;
+    HIP_OK(hipMemcpy(&err, sync + 64, sizeof(err), hipMemcpyDeviceToHost));
+    // verify: pull the neighbours' current edge rows into the local halo rows,
+    // then one sweep of the first owned rows against the CPU reference
+    if (rank > 0 && a.halo != "none") {  // the upper neighbour's current u: swapped `it` times like ours
+        const T *nb_u = static_cast<const T *>(it % 2 ? sh.peer_un[rank - 1] : sh.peer_u[rank - 1]);
+        HIP_OK(hipMemcpy(u, nb_u + Slab(grows, sh.world, rank - 1).rows * cols, row_bytes, hipMemcpyDefault));
+    }
+    // rows 1..vr need row vr + 1: stay clear of the lower halo row (not pulled)
+    const long long vr = std::max<long long>(
+        1, std::min<long long>(rank + 1 < sh.world && a.halo != "none" ? rows - 1 : rows, 8));
+    std::vector<T> hu_((vr + 2) * cols), hun((vr + 2) * cols), gun((vr + 2) * cols);
+    HIP_OK(hipMemcpy(hu_.data(), u, (vr + 2) * row_bytes, hipMemcpyDeviceToHost));
+    hun = hu_;
+    if constexpr (sizeof(T) == 8) {
+        MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, 1, (int)vr + 1, nullptr, s));
+        mpx_cpu_jacobi_f64(hu_.data(), hun.data(), cols, cols, 1, (int)vr + 1);
+    } else {
+        MPX_OK_OR_DIE(mpx_jacobi_f32(u, un, cols, cols, 1, (int)vr + 1, nullptr, s));
+        cpu_sweep_f32(hu_.data(), hun.data(), cols, 1, (int)vr + 1);
+    }
+    HIP_OK(hipMemcpyAsync(gun.data(), un, (vr + 2) * row_bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    sh.verified[rank] = err == 0 && std::memcmp(gun.data() + cols, hun.data() + cols, (size_t)vr * row_bytes) == 0;
+    if (err) fprintf(stderr, "[ERROR MPX] rank %d: a device-side halo wait timed out\n", rank);
+    sh.bar->wait();  // nobody frees buffers a neighbour may still read
+    HIP_OK(hipFree(u));
+    HIP_OK(hipFree(un));
+    HIP_OK(hipFree(res));
+    HIP_OK(hipFree(sync));
+    HIP_OK(hipStreamDestroy(s));
 }
 
 // ---------------------------------------------------------------- jacobi
@@ -416,18 +543,34 @@ int main(int argc, char **argv) {
         return 1;
     }
     const int N = a.gpus > 0 ? a.gpus : ndev;
-    if (N > ndev) {
+    // --halo none: ablation of the peer mode (same kernels and launches, no
+    // neighbour reads or waits; wrong answer) to isolate the ordering cost
+    const bool peer = a.mode == "jacobi" && (a.halo == "peer" || a.halo == "none");
+    if (a.halo != "rccl" && a.halo != "peer" && a.halo != "none") {
+        fprintf(stderr, "[ERROR] --halo must be rccl, peer or none\n");
+        return 2;
+    }
+    if (a.shared && (!peer || N > 4 * ndev)) {
+        fprintf(stderr, "[ERROR] --shared needs jacobi --halo peer and at most 4 ranks per device\n");
+        return 2;
+    }
+    if (N > ndev && !a.shared) {
         fprintf(stderr, "[ERROR] --gpus %d but only %d device(s) visible\n", N, ndev);
         return 1;
     }
     Shared sh;
     sh.world = N;
+    sh.ndev = ndev;
+    sh.peer_u.assign(N, nullptr);
+    sh.peer_un.assign(N, nullptr);
+    sh.peer_sync.assign(N, nullptr);
+    sh.res.assign(N, 0.0);
     Barrier bar(N);
     sh.bar = &bar;
     sh.elapsed.assign(N, 0.0);
     sh.verified.assign(N, -1);
     sh.extra.assign(N, 0.0);
-    if (a.mode != "vsub") NCCL_CHECK(ncclGetUniqueId(&sh.id));
+    if (a.mode != "vsub" && !peer) NCCL_CHECK(ncclGetUniqueId(&sh.id));
 
     std::vector<std::thread> th;
     if (a.mode == "conv") {
@@ -438,7 +581,10 @@ int main(int argc, char **argv) {
         if (a.size <= 0) a.size = 16384;
         if (a.steps <= 0) a.steps = 50;
         for (int r = 0; r < N; ++r)
-            th.emplace_back([&, r] { a.fp32 ? jacobi_worker<float>(a, sh, r) : jacobi_worker<double>(a, sh, r); });
+            th.emplace_back([&, r] {
+                if (peer) a.fp32 ? jacobi_peer_worker<float>(a, sh, r) : jacobi_peer_worker<double>(a, sh, r);
+                else a.fp32 ? jacobi_worker<float>(a, sh, r) : jacobi_worker<double>(a, sh, r);
+            });
     } else if (a.mode == "vsub") {
         if (a.n <= 0) a.n = 1LL << 26;
         if (a.steps <= 0) a.steps = 50;
@@ -460,12 +606,15 @@ int main(int argc, char **argv) {
                "\"verified_bit_exact\": %s}\n",
                a.filter.c_str(), N, a.size, a.size, a.steps, ms, gpix, ok ? "true" : "false");
     } else if (a.mode == "jacobi") {
-        const double pts = (double)a.size * a.size * a.steps / el / 1e9;
-        const double tbs = (double)a.size * a.size * (a.fp32 ? 4 : 8) * 2 * a.steps / el / 1e12;
+        const int grows = peer && a.rows > 0 ? a.rows : a.size;
+        const double pts = (double)grows * a.size * a.steps / el / 1e9;
+        const double tbs = (double)grows * a.size * (a.fp32 ? 4 : 8) * 2 * a.steps / el / 1e12;
         printf("{\"workload\": \"jacobi\", \"dtype\": \"%s\", \"n_gpus\": %d, \"grid\": [%d, %d], \"iters\": %d, "
                "\"check_every\": %d, \"ms_per_iter\": %.5f, \"value\": %.3f, \"unit\": \"Gpoint/s\", "
-               "\"TBps_aggregate\": %.3f, \"scaling\": \"strong\", \"residual\": %.6e, \"verified\": %s}\n",
-               a.fp32 ? "fp32" : "fp64", N, a.size, a.size, a.steps, a.check_every, ms, pts, tbs, sh.extra[0],
+               "\"TBps_aggregate\": %.3f, \"scaling\": \"strong\", \"residual\": %.6e, \"halo\": \"%s\", "
+               "\"devices\": %d, \"verified\": %s}\n",
+               a.fp32 ? "fp32" : "fp64", N, grows, a.size, a.steps, a.check_every, ms, pts, tbs, sh.extra[0],
+               !peer ? "rccl" : a.halo == "none" ? "none (ablation)" : "peer-signalled", std::min(N, ndev),
                ok ? "true" : "false");
     } else {
         const int es = a.fp64 ? 8 : 4;

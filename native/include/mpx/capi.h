@@ -169,6 +169,26 @@ int mpx_memcpy_d2d(void *dst, const void *src, int64_t bytes, void *stream);
  * kernel folds max|un-u| over the swept points into *resid (atomic max, bit
  * pattern of a non-negative double), so callers zero it first.
  */
+/* One-sided, device-signalled halo sweep of a whole slab (rows 1..rows of a
+ * (rows + 2) x pitch buffer): the halo rows are read from the neighbours'
+ * IPC-mapped buffers, ordered by completed-iteration counters (see jacobi.hip).
+ * up_row[k] / dn_row[k]: the neighbour's last / first owned row in the buffer
+ * that is its u at even (k = 0) / odd (k = 1) iterations; NULL (with a NULL
+ * flag) at the global boundary, where the local halo row is the boundary row.
+ * sync: this rank's mpx_jacobi_sync_bytes() block; word 0 = completed
+ * iterations (the neighbours' *_flag points at theirs), word 64 != 0 after a
+ * bounded wait gave up. */
+typedef struct mpx_jacobi_peer {
+    const void *up_row[2];
+    const void *dn_row[2];
+    const unsigned int *up_flag;
+    const unsigned int *dn_flag;
+    unsigned int *sync;
+    unsigned int spin_limit; /* polls before a wait gives up (0 = default, ~seconds) */
+} mpx_jacobi_peer;
+int mpx_jacobi_sync_bytes(void);
+int mpx_jacobi_peer_sweep(int fp64, void *u, void *un, int cols, int pitch, int rows, void *resid,
+                          const mpx_jacobi_peer *p, void *stream);
 int mpx_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1,
                    double *resid, void *stream);
 int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r1, float *resid,

@@ -166,10 +166,46 @@ __device__ __forceinline__ T dpp_shift(T v, int ctrl) {
     }
 }
 
-template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true>
+// ---------------------------------------------------------------------------
+// one-sided, device-signalled halos (PEER): the neighbours' slab rows are read
+// straight from their IPC-mapped buffers over xGMI, and per-iteration order
+// comes from completed-iteration counters in device memory — no host round
+// trip, no exchange kernel, no RCCL: one launch per iteration, as on one GPU.
+//
+// Only the slab-edge waves (row block 0: reads halo row 0, writes row 1; the
+// last row block: writes row n, reads halo row n+1) take part. At iteration t
+// an edge wave waits until the neighbour's counter is >= t — the neighbour has
+// finished iteration t-1, so (a) its edge row of u^(t) is written and (b) it
+// is done reading this rank's edge row of u^(t-1), the buffer this sweep
+// overwrites. After its stores, an edge wave releases them at system scope and
+// bumps this rank's edge-wave counter; the last one publishes counter value
+// t+1. Coherence without cache-maintenance fences (an L2 write-back or
+// invalidate per edge wave cost ~40 us per sweep): the rows a neighbour reads
+// are stored at system scope (write-through) and acknowledged before the
+// count goes up, and halo rows are loaded at system scope (never a stale
+// cached line). Interior waves never wait. Edge waves are dispatched first so the
+// counter is published early in the sweep. Waits are bounded (pr.spin_limit):
+// a wave that gives up sets sync[kSyncErr] and the host raises.
+// ---------------------------------------------------------------------------
+constexpr int kSyncIter = 0, kSyncCtr = 32, kSyncErr = 64;  // uint32 slots, 128 B apart
+constexpr int kCpolSystem = 1 | 16;                          // gfx950 cache policy SC0 | SC1: system scope
+constexpr uint32_t kPeerSpinDefault = 1u << 22;             // ~seconds of s_sleep
+
+__device__ __forceinline__ void peer_wait(const uint32_t *flag, uint32_t target, uint32_t *err, uint32_t limit) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+        if (++spins > limit) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true, bool PEER = false>
 __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
-                                                          int nwaves, T *__restrict__ resid) {
+                                                          int nwaves, T *__restrict__ resid, mpx_jacobi_peer pr) {
     using V = typename JWide<T>::type;
     constexpr int NV = JVec<T>::n;
     const int lane = threadIdx.x & 63;
@@ -177,7 +213,9 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
     T rmax = (T)0;
     if (wave < nwaves) {
         const int strip = wave % strips;  // consecutive waves: adjacent strips of the same rows
-        const int rb = wave / strips;
+        int rb = wave / strips;
+        const int nrb = nwaves / strips;
+        if (PEER && nrb > 1) rb = rb == 0 ? 0 : rb == 1 ? nrb - 1 : rb - 1;  // both edge blocks first
         const int nvec = cols / NV;
         const int cv = strip * kStripVec - 1 + lane;  // this lane's column vector
         const bool out_lane = lane >= 1 && lane <= kStripVec && cv < nvec;
@@ -185,8 +223,37 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
         const int i0 = r0 + rb * rows_per_wave;
         const int i1 = min(i0 + rows_per_wave, r1);
         const T *base = u + (int64_t)cvc * NV;
+        const bool edge = PEER && (rb == 0 || i1 == r1);
+        const T *up_row = nullptr, *dn_row = nullptr;
+        uint32_t it = 0;
+        if constexpr (PEER) {
+            if (edge) {
+                // this rank's completed iterations = the index of this sweep (bumped only
+                // after every edge wave of the sweep has finished)
+                it = __hip_atomic_load(pr.sync + kSyncIter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (rb == 0 && pr.up_flag) {
+                    peer_wait(pr.up_flag, it, pr.sync + kSyncErr, pr.spin_limit ? pr.spin_limit : kPeerSpinDefault);
+                    up_row = static_cast<const T *>(pr.up_row[it & 1u]) + (int64_t)cvc * NV;
+                }
+                if (i1 == r1 && pr.dn_flag) {
+                    peer_wait(pr.dn_flag, it, pr.sync + kSyncErr, pr.spin_limit ? pr.spin_limit : kPeerSpinDefault);
+                    dn_row = static_cast<const T *>(pr.dn_row[it & 1u]) + (int64_t)cvc * NV;
+                }
+            }
+        }
         auto ld = [&](int i) {
             const V *p = reinterpret_cast<const V *>(base + (int64_t)i * pitch);
+            if constexpr (PEER) {  // wave-uniform row select: halo rows come from the neighbours,
+                const T *q = nullptr;  // loaded at system scope (sc0 sc1): never a stale cached line
+                if (i == r0 - 1 && up_row) q = up_row;
+                if (i == r1 && dn_row) q = dn_row;
+                if (q) {
+                    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(q), 0, 16,
+                                                                                       0x00020000);
+                    return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kCpolSystem));
+                }
+            }
             if constexpr (LNT) return __builtin_nontemporal_load(p);  // tuning variant
             else return *p;
         };
@@ -225,7 +292,11 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
             const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
                 un + (int64_t)min(r, i1 - 1) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
             typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, AUX);
+            if (PEER && edge && (r == r0 || r == r1 - 1))  // a row the neighbours read: write through
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0,
+                                                       kCpolSystem);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, AUX);
             // keep each step's prefetch at its start: the scheduler otherwise sinks
             // loads past the next step's use and the wait counts collapse to 0
             __builtin_amdgcn_sched_barrier(0);
@@ -257,6 +328,22 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
                 if (i + 2 < i1) {
                     step(I2{}, i);
                     if (i + 3 < i1) step(I3{}, i);
+                }
+            }
+        }
+        if constexpr (PEER) {
+            if (edge) {
+                // the write-through edge-row stores are acknowledged at system scope
+                // before the count goes up: no L2 write-back fence needed
+                __builtin_amdgcn_s_waitcnt(0);
+                if (lane == 0) {
+                    const int n_edge = nrb > 1 ? 2 * strips : strips;
+                    const uint32_t c = __hip_atomic_fetch_add(pr.sync + kSyncCtr, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                    if (c + 1 == (uint32_t)n_edge) {  // last edge wave of this sweep
+                        __hip_atomic_store(pr.sync + kSyncCtr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(pr.sync + kSyncIter, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 }
             }
         }
@@ -292,7 +379,7 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
         while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
         hipLaunchKernelGGL((jacobi_wave_kernel<T, 2>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
-                           cols, pitch, r0, r1, strips, R, nwaves, resid);
+                           cols, pitch, r0, r1, strips, R, nwaves, resid, mpx_jacobi_peer{});
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;
     }
@@ -305,6 +392,28 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
     else
         hipLaunchKernelGGL((jacobi_kernel<T, false>), grd, blk, 0, as_stream(stream), u, un, cols, pitch, r0, r1,
                            resid);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
+template <typename T>
+int launch_jacobi_peer(const T *u, T *un, int cols, int pitch, int rows, T *resid, const mpx_jacobi_peer &pr,
+                       void *stream) {
+    MPX_CHECK_ARG(u && un && pr.sync, "null pointer");
+    MPX_CHECK_ARG(cols >= 1 && pitch >= cols && rows >= 1, "bad slab geometry");
+    MPX_CHECK_ARG(!pr.up_flag == !pr.up_row[0] && !pr.up_row[0] == !pr.up_row[1], "up neighbour: rows and flag together");
+    MPX_CHECK_ARG(!pr.dn_flag == !pr.dn_row[0] && !pr.dn_row[0] == !pr.dn_row[1], "down neighbour: rows and flag together");
+    constexpr int NV = JVec<T>::n;
+    MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un),
+                  "peer halos need the 16-byte vector layout (cols and pitch multiples of the vector width)");
+    for (const void *q : {pr.up_row[0], pr.up_row[1], pr.dn_row[0], pr.dn_row[1]})
+        MPX_CHECK_ARG(!q || aligned16(q), "neighbour rows must be 16-byte aligned");
+    const int strips = (cols / NV + kStripVec - 1) / kStripVec;
+    int R = 5;
+    while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
+    const int nwaves = strips * ((rows + R - 1) / R);
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
+                       as_stream(stream), u, un, cols, pitch, 1, rows + 1, strips, R, nwaves, resid, pr);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }
@@ -324,6 +433,18 @@ extern "C" int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, in
     return mpx::launch_jacobi<float>(u, un, cols, pitch, r0, r1, resid, stream);
 }
 
+extern "C" int mpx_jacobi_peer_sweep(int fp64, void *u, void *un, int cols, int pitch, int rows, void *resid,
+                                     const mpx_jacobi_peer *p, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(p, "null peer descriptor");
+    if (fp64)
+        return launch_jacobi_peer<double>((const double *)u, (double *)un, cols, pitch, rows, (double *)resid, *p,
+                                          stream);
+    return launch_jacobi_peer<float>((const float *)u, (float *)un, cols, pitch, rows, (float *)resid, *p, stream);
+}
+
+extern "C" int mpx_jacobi_sync_bytes(void) { return 4 * 128; }
+
 // Tuning entry point (tools/jbench.py): wave kernel with an explicit rows-per-
 // wave R and buffer-store cache policy aux (0 default, 2 = nontemporal).
 extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0, int r1, void *resid, int fp64,
@@ -340,13 +461,13 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
     hipStream_t s = as_stream(stream);
 #define MPX_JV(T, A)                                                                                          \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, A>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, \
-                       R, nwaves, (T *)resid)
+                       R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVN(T)                                                                                             \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, true>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
-                       strips, R, nwaves, (T *)resid)
+                       strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVX(T)                                                                                             \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, false>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, \
-                       r1, strips, R, nwaves, (T *)resid)
+                       r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
     if (fp64) {
         if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
     } else {

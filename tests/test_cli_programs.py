@@ -174,9 +174,26 @@ def test_mpx_mgpu_single_gpu(args):
     assert rec.get("verified_bit_exact", rec.get("verified")) is True
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,extra", [(1, []), (2, []), (3, ["--fp32"]), (4, ["--rows", "805"])])
+def test_mpx_mgpu_jacobi_peer_shared(ranks, extra):
+    """Native runtime, one-sided device-signalled halos: up to 4 ranks (one
+    stream each) rehearse on the one GPU; per-rank self-verification plus no
+    device-side wait may time out."""
+    import json
+
+    r = run("bin/mpx_mgpu", "", args=["jacobi", "--halo", "peer", "--shared", "--gpus", str(ranks), "--size", "1024",
+                                      "--iters", "40", "--warmup", "3", "--check-every", "10", *extra])
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == ranks and rec["halo"] == "peer-signalled" and rec["verified"] is True
+
+
 def test_mpx_mgpu_usage_errors():
     assert run("bin/mpx_mgpu", "").returncode == 2
     assert run("bin/mpx_mgpu", "", args=["conv", "--bogus"]).returncode == 2
+    assert run("bin/mpx_mgpu", "", args=["jacobi", "--halo", "carrier-pigeon"]).returncode == 2
+    assert run("bin/mpx_mgpu", "", args=["conv", "--shared", "--gpus", "2"]).returncode == 2
 
 
 def _png_to_data(png, dst):

@@ -1,10 +1,13 @@
-"""One-sided halo transport (parallel/peer.py): neighbour slabs IPC-mapped and
-read by the conv kernel over xGMI.
+"""One-sided halo transports (parallel/peer.py): neighbour slabs IPC-mapped
+and read by the kernels over xGMI — the conv (static inputs) and the Jacobi
+sweep (device-signalled: per-iteration order from completed-iteration words,
+no host round trip).
 
-The GPU tests run 2 and 3 ranks as separate processes on ONE MI355X (IPC works
-between processes on the same device; RCCL would refuse two ranks on one GPU,
-so the control plane is gloo). The decomposed result must be bit-identical to
-the single-process convolution of the whole image.
+The GPU tests run 2, 3, 4 and 8 ranks as separate processes on ONE MI355X
+(IPC works between processes on the same device; RCCL would refuse two ranks
+on one GPU, so the control plane is gloo): interior ranks map both
+neighbours, as at N = 8 on a node. Global row counts 8k+5 leave uneven slabs.
+Decomposed results must be bit-identical to the single-process run.
 """
 
 import os
@@ -61,18 +64,58 @@ def _peer_worker(rank, world, port, h, w, filt, errq):
         errq.put(f"rank {rank}: {traceback.format_exc()}")
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (3, "sobel5_dense")])
-def test_peer_halo_ranks_share_one_gpu(gpu, world, filt):
+def _jacobi_peer_worker(rank, world, port, rows, cols, iters, fp64, errq):
+    try:
+        from cuda_mpi_openmp_amd.models import SlabJacobi
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        ctx = parallel.init(device="cuda", backend="gloo")
+        dt = torch.float64 if fp64 else torch.float32
+        g = torch.Generator().manual_seed(3)
+        field = torch.rand((rows, cols - 2), generator=g, dtype=torch.float64).to(dt)
+
+        def setup(sol):
+            sol.set_boundary(top=1.0, left=0.5, right=0.25)
+            s = sol.slab
+            sol.u[1:1 + s.rows, 1:-1] = field[s.row0:s.row0 + s.rows].to(sol.u.device)
+            sol.un.copy_(sol.u)
+            sol._halos_valid = False
+
+        sol = SlabJacobi(ctx, rows, cols, dtype=dt, check_every=10, halo="peer")
+        assert sol.transport == "xgmi-peer-signalled", sol.transport
+        setup(sol)
+        sol.run(iters)
+        torch.cuda.synchronize()
+        sol.check_peer()
+        got = sol.gather()
+        res = sol.last_residual
+        # a restart from the gathered state must continue seamlessly (re-publish)
+        sol.run(10)
+        got2 = sol.gather()
+        sol.close()
+        if ctx.rank == 0:
+            ref = SlabJacobi(parallel.DistContext(device=ctx.device), rows, cols, dtype=dt, check_every=10)
+            setup(ref)
+            ref.run(iters)
+            assert torch.equal(got.cpu(), ref.owned.cpu()), "peer-signalled Jacobi differs from one rank"
+            assert res == ref.last_residual
+            ref.run(10)
+            assert torch.equal(got2.cpu(), ref.owned.cpu())
+        parallel.shutdown()
+    except Exception:  # noqa: BLE001
+        errq.put(f"rank {rank}: {traceback.format_exc()}")
+
+
+def _run_ranks(target, world, *args, timeout=240):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    h, w = 301, 258
-    procs = [ctx.Process(target=_peer_worker, args=(r, world, port, h, w, filt, errq)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, errq)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=240)
+        p.join(timeout=timeout)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
@@ -81,6 +124,23 @@ def test_peer_halo_ranks_share_one_gpu(gpu, world, filt):
             p.kill()
     assert not errs, "\n".join(errs)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (3, "sobel5_dense"), (4, "sobel5"),
+                                        (8, "sobel5")])
+def test_peer_halo_ranks_share_one_gpu(gpu, world, filt):
+    h = 301 if world <= 3 else 8 * 37 + 5  # 8k+5: uneven slabs at 4 and 8 ranks
+    _run_ranks(_peer_worker, world, h, 258, filt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,fp64", [(2, True), (3, False), (4, True), (8, True)])
+def test_jacobi_peer_signalled_equals_one_rank(gpu, world, fp64):
+    """100 iterations of the device-signalled one-sided halo sweep (plus a
+    10-iteration restart) are bit-identical to a single-rank run, residual
+    included; 8k+5 global rows."""
+    _run_ranks(_jacobi_peer_worker, world, 8 * 9 + 5, 132 if fp64 else 136, 100, fp64)
 
 
 def test_peer_halo_not_for_single_rank_or_cpu():

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """BASELINE north star 5: 2-D Jacobi on a 16384^2 fp64 grid, row-slab
-decomposed over N GPUs (strong scaling), halos over RCCL (native tier when
-available), residual all-reduce every --check-every iterations.
+decomposed over N GPUs (strong scaling), residual all-reduce every
+--check-every iterations. Halos (--halo): one-sided device-signalled xGMI
+reads of the neighbours' buffers (peer, default when the IPC links map) or
+RCCL send/recv (native tier when available).
+
+One-GPU rehearsal of N ranks (peer halos, gloo control plane):
+  MPX_DIST_BACKEND=gloo python tools/bench_jacobi.py --gpus 4
 
   python tools/bench_jacobi.py [--size 16384] [--iters 100] [--warmup 10]
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_jacobi.py
@@ -25,13 +30,17 @@ from cuda_mpi_openmp_amd.models import SlabJacobi  # noqa: E402
 def main() -> int:
     p = argparse.ArgumentParser()
     p.add_argument("--size", type=int, default=16384)
+    p.add_argument("--rows", type=int, default=None, help="global rows (default --size: a square grid)")
     p.add_argument("--iters", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--check-every", type=int, default=10)
     p.add_argument("--fp32", action="store_true")
     p.add_argument("--overlap", choices=["auto", "on", "off"], default="auto")
+    p.add_argument("--halo", choices=["auto", "peer", "rccl", "none"], default="auto",
+                   help="none = ablation without any halo exchange (wrong answer; isolates the exchange cost)")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     p.add_argument("--graph", action="store_true", help="replay HIP graphs of whole residual cycles")
+    p.add_argument("--progress", action="store_true", help="per-phase and per-check timing on stderr")
     p.add_argument("--gpus", type=int, default=None,
                    help="ranks to run (self-launched when no torchrun environment); default WORLD_SIZE or 1")
     a = p.parse_args()
@@ -45,33 +54,53 @@ def main() -> int:
     if a.gpus is not None:
         launch.check_world(a.gpus, ctx.world)
     dt = torch.float32 if a.fp32 else torch.float64
-    sol = SlabJacobi(ctx, a.size, a.size, dtype=dt, check_every=a.check_every,
-                     overlap={"auto": "auto", "on": True, "off": False}[a.overlap])
+    rows = a.rows or a.size
+    sol = SlabJacobi(ctx, rows, a.size, dtype=dt, check_every=a.check_every,
+                     overlap={"auto": "auto", "on": True, "off": False}[a.overlap], halo=a.halo)
+    def say(msg):
+        if a.progress:
+            print(f"[jacobi r{ctx.rank} {time.perf_counter() - t_start:8.3f}s] {msg}", file=sys.stderr, flush=True)
+
+    t_start = time.perf_counter()
+    say(f"solver ready, transport {sol.transport}")
     sol.set_boundary(top=1.0)
     sol.fill(seed=0)
+    say("filled")
     sync = (lambda: torch.cuda.synchronize(ctx.device)) if ctx.device.type == "cuda" else (lambda: None)
-    sol.run(a.warmup, graph=a.graph)
+    if a.progress:
+        for k in range(a.warmup):
+            r = sol.step()
+            sync()
+            say(f"warmup step {k} residual {r}")
+    else:
+        sol.run(a.warmup, graph=a.graph)
     sync()
     ctx.barrier()
     t0 = time.perf_counter()
     sol.run(a.iters, graph=a.graph)
     sync()
     ctx.barrier()
-    el = parallel.max_over_ranks(time.perf_counter() - t0, ctx)
+    mine = time.perf_counter() - t0
+    sol.check_peer()
+    el = parallel.max_over_ranks(mine, ctx)
+    per_rank = parallel.all_gather_floats(mine, ctx)  # collective: every rank
     if ctx.rank == 0:
         ms = el * 1e3 / a.iters
         es = 4 if a.fp32 else 8
         print(json.dumps({
             "metric": "2-D Jacobi iteration time, 16384^2 grid domain-decomposed over N MI355X",
             "value": round(ms, 5), "unit": "ms/iteration", "higher_is_better": False, "scaling": "strong",
-            "n_gpus": ctx.world, "iters": a.iters, "warmup": a.warmup, "grid": [a.size, a.size],
+            "n_gpus": ctx.world, "iters": a.iters, "warmup": a.warmup, "grid": [rows, a.size],
             "dtype": "fp32" if a.fp32 else "fp64", "check_every": a.check_every,
-            "gpoints_per_s": round(a.size * a.size / (ms * 1e-3) / 1e9, 3),
-            "TBps_aggregate": round(2 * a.size * a.size * es / (ms * 1e-3) / 1e12, 3),
+            "gpoints_per_s": round(rows * a.size / (ms * 1e-3) / 1e9, 3),
+            "TBps_aggregate": round(2 * rows * a.size * es / (ms * 1e-3) / 1e12, 3),
             "residual": sol.last_residual,
-            "transport": ("native-rccl" if ctx.native is not None else "torch.distributed") if ctx.world > 1 else None,
-            "halo": ("overlap" if sol.overlap else "inorder") if ctx.world > 1 else None,
+            "transport": sol.transport,
+            "halo": ("one-launch" if sol.peer is not None else "overlap" if sol.overlap else "inorder")
+            if ctx.world > 1 else None,
+            "per_rank_ms": [round(t * 1e3 / a.iters, 5) for t in per_rank],
             "hip_graph": bool(a.graph and ctx.device.type == "cuda")}), flush=True)
+    sol.close()
     parallel.shutdown()
     return 0
 
