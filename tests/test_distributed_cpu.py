@@ -1,5 +1,7 @@
-"""Multi-process decomposition tests on CPU (gloo backend, world sizes 2 and 3):
-every distributed workload must reproduce the single-process result exactly."""
+"""Multi-process decomposition tests on CPU (gloo backend, world sizes 2, 3, 4
+and 8): every distributed workload must reproduce the single-process result
+exactly. At 8 ranks every interior rank has both neighbours (the N = 8 node
+topology); global row counts of 8k+5 leave uneven slabs."""
 
 import os
 import socket
@@ -137,7 +139,61 @@ def collectives_worker(ctx):
     assert torch.equal(mine, torch.arange(40, dtype=torch.float32).reshape(10, 4)[s.row0:s.row0 + s.rows])
 
 
+def all_workloads_worker(ctx, k):
+    """conv (sobel5 overlapped + roberts in order), classifier, vsub and Jacobi
+    on 8k+5-row problems, each compared bit-exactly with one process."""
+    h, w = 8 * k + 5, 29
+    full = _img(h, w, 17)
+    for filt, overlap in (("sobel5", True), ("roberts", False)):
+        det = SlabEdgeDetector(ctx, h, w, filt, overlap=overlap)
+        s = det.slab
+        det.load(full[s.row0:s.row0 + s.rows])
+        got = parallel.gather_slabs(det.step(), s, ctx)
+        if ctx.rank == 0:
+            assert torch.equal(got, ops.conv(full, filt)), f"{filt} at world {ctx.world}"
+    # classifier
+    pts = class_points_for(h, w, 5, 20, seed=4)
+    clf = SlabPixelClassifier(ctx, h, w, path="direct")
+    clf.img.copy_(split_rows(full, clf.slab))
+    clf.fit(pts)
+    clf.classify()
+    got = parallel.gather_slabs(clf.img, clf.slab, ctx)
+    if ctx.rank == 0:
+        ref = full.clone()
+        mu, inv = ops.class_stats(full, pts)
+        ops.classify_(ref, mu, inv)
+        assert torch.equal(got, ref), f"classifier at world {ctx.world}"
+    # vsub
+    m = ShardedVectorSub(ctx, 8 * 1000 + 5)
+    m.fill_random(seed=6)
+    m.step()
+    assert torch.equal(m.c, m.a - m.b)
+    # Jacobi: 25 iterations, residual every 5
+    rows, cols = 8 * k + 5, 19
+    g = torch.Generator().manual_seed(8)
+    field = torch.rand((rows, cols - 2), generator=g, dtype=torch.float64)
+
+    def setup(sol):
+        sol.set_boundary(top=1.0, left=0.5)
+        sol.u[1:1 + sol.slab.rows, 1:-1] = field[sol.slab.row0:sol.slab.row0 + sol.slab.rows]
+        sol._halos_valid = False
+
+    sol = SlabJacobi(ctx, rows, cols, check_every=5)
+    setup(sol)
+    sol.run(25)
+    got = sol.gather()
+    if ctx.rank == 0:
+        ref = SlabJacobi(parallel.DistContext(), rows, cols, check_every=5)
+        setup(ref)
+        ref.run(25)
+        assert torch.equal(got, ref.owned) and sol.last_residual == ref.last_residual, f"jacobi at {ctx.world}"
+
+
 # ---------------------------------------------------------------- tests
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_all_workloads_decomposed_uneven(world):
+    run_world(world, "all_workloads_worker", 3)
+
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("filt", ["sobel5", "roberts", "sobel3"])
 def test_slab_conv_equals_single(world, filt, tmp_path):
