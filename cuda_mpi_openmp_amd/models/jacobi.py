@@ -92,8 +92,8 @@ class SlabJacobi:
                 raise RuntimeError("peer halo transport unavailable (IPC mapping failed or cols not a multiple of "
                                    f"{nv})")
         else:
-            if halo == "peer":
-                raise RuntimeError("peer halos need a distributed GPU run")
+            if halo == "peer" and ctx.is_distributed:
+                raise RuntimeError("peer halos need GPU ranks (IPC-mapped device memory)")
             self.u = torch.zeros(shape, dtype=dtype, device=dev)
             self.un = torch.zeros(shape, dtype=dtype, device=dev)
         self.resid = torch.zeros(1, dtype=dtype, device=dev)

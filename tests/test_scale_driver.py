@@ -1,0 +1,21 @@
+"""tools/scale.py: the 1/2/4/8 scaling driver, dry-run on the CPU (gloo)."""
+import json
+import os
+import subprocess
+import sys
+
+from .helpers import ROOT
+
+
+def test_scale_driver_cpu_dry_run(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale.py"), "--device", "cpu", "--gpus", "1,2",
+                        "--only", "conv", "--out", str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    data = json.load(open(tmp_path / "scaling.json"))
+    runs = {(x["name"], x["n"]): x for x in data["runs"]}
+    one, two = runs[("conv/peer", 1)], runs[("conv/rccl", 2)]
+    assert one["status"] == "ok" and one["efficiency"] == 1.0
+    assert two["status"] == "ok" and two["n_reported"] == 2 and two["verified"] is True
+    assert two["efficiency"] is not None and two["world_size_seen"]["torch_distributed"] == 2
+    assert runs[("conv/peer", 2)]["status"] == "skipped" and runs[("conv/peer", 2)]["reason"]
+    assert (tmp_path / "scaling.csv").exists() and (tmp_path / "scaling.png").exists()

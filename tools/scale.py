@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Scaling driver: 1/2/4/8-GPU curves of every multi-GPU workload, one command.
+
+  python tools/scale.py [--gpus 1,2,4,8] [--out scaling] [--rehearse] [--device cpu] [--quick]
+
+For each N it runs, each as its own launched job (one process per GPU, the
+same commands a user would type):
+
+  * conv (weak scaling, the flagship): ``bench.py --gpus N`` with one-sided
+    peer halos and with RCCL halos — every rank owns a 4096^2 slab;
+  * Jacobi 16384^2 fp64 (strong scaling): ``tools/bench_jacobi.py --gpus N``
+    with device-signalled peer halos and with RCCL halos;
+  * the native one-process runtime: ``bin/mpx_mgpu conv|jacobi --gpus N``.
+
+and writes ``<out>/scaling.json`` (one record per run: N, value, ms/step,
+efficiency vs N = 1, transport, world size the job saw), ``scaling.csv`` and
+``scaling.png`` (weak-scaling throughput and strong-scaling speedup against
+the ideal lines). Efficiency: weak = value_N / (N * value_1); strong =
+t_1 / (N * t_N). Runs that cannot execute here (fewer devices than N, RCCL
+with several ranks on one GPU) are recorded as skipped with the reason.
+
+``--rehearse``: several ranks share the GPUs (gloo control plane, peer halos
+only; the native runtime in ``--shared`` mode up to 4 ranks) — the N = 8
+code paths on a one-GPU box. ``--device cpu``: gloo on the CPU with small
+problems (CI dry run). The reference has no multi-GPU code and no scaling
+plot (its only plot: /root/reference/tester.py:325-407, the per-run median
+bar chart); SURVEY §5 and §7.2 step 7 ask for this one.
+"""
+
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def visible_gpus() -> int:
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())  # counts devices without creating a HIP context
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def last_json(text: str) -> Optional[dict]:
+    for line in reversed(text.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except json.JSONDecodeError:
+                continue
+    return None
+
+
+def run_job(cmd: List[str], env: Dict[str, str], timeout: float, log) -> dict:
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"status": "timeout", "wall_s": round(time.perf_counter() - t0, 1)}
+    log.write(f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr[-4000:]}\n")
+    log.flush()
+    rec = last_json(r.stdout)
+    if r.returncode != 0 or rec is None:
+        return {"status": f"failed rc={r.returncode}", "stderr_tail": r.stderr[-800:],
+                "wall_s": round(time.perf_counter() - t0, 1)}
+    return {"status": "ok", "record": rec, "wall_s": round(time.perf_counter() - t0, 1)}
+
+
+def plan(n: int, a, ndev: int) -> List[dict]:
+    """The jobs of one rank count: name, kind (weak/strong), command, skip reason."""
+    py = sys.executable
+    cpu = a.device == "cpu"
+    shared = a.rehearse or cpu
+    conv_sz = ["--size", "128", "--steps", "3", "--warmup", "1", "--rotate", "2"] if cpu else (
+        ["--steps", "20", "--warmup", "5"] if a.quick else ["--steps", "50", "--warmup", "10"])
+    jac_sz = ["--size", "256", "--iters", "10", "--warmup", "2"] if cpu else (
+        ["--iters", "50", "--warmup", "10"] if a.quick else ["--iters", "200", "--warmup", "20"])
+    dev = ["--device", "cpu"] if cpu else []
+    jobs = []
+    lacks = None if shared or n <= ndev else f"needs {n} GPUs, {ndev} visible"
+    for halo in ("peer", "rccl"):
+        skip = lacks
+        if n > 1 and halo == "rccl" and a.rehearse and not cpu:
+            skip = "RCCL refuses several ranks on one GPU (rehearsal uses peer halos)"
+        if n == 1 and halo == "rccl":
+            skip = "single rank: no halo transport"
+        if cpu and halo == "peer" and n > 1:
+            skip = "peer halos need GPUs (IPC); the CPU run uses gloo send/recv"
+        jobs.append({"name": f"conv/{halo}", "kind": "weak", "skip": skip,
+                     "cmd": [py, "bench.py", "--gpus", str(n), "--halo", halo, "--no-cpu-baseline", *dev, *conv_sz]})
+        jobs.append({"name": f"jacobi/{halo}", "kind": "strong",
+                     "skip": skip,
+                     "cmd": [py, "tools/bench_jacobi.py", "--gpus", str(n), "--halo", halo, *dev, *jac_sz]})
+    mg = os.path.join(ROOT, "bin", "mpx_mgpu")
+    if cpu:
+        jobs.append({"name": "mgpu/conv", "kind": "weak", "skip": "native runtime needs GPUs", "cmd": []})
+        jobs.append({"name": "mgpu/jacobi-peer", "kind": "strong", "skip": "native runtime needs GPUs", "cmd": []})
+    else:
+        steps = ["--steps", "20", "--warmup", "5"] if a.quick else ["--steps", "50", "--warmup", "10"]
+        jobs.append({"name": "mgpu/conv", "kind": "weak",
+                     "skip": (f"needs {n} GPUs, {ndev} visible (RCCL: one rank per GPU)" if n > ndev else None),
+                     "cmd": [mg, "conv", "--gpus", str(n), *steps]})
+        sh = n > ndev
+        jobs.append({"name": "mgpu/jacobi-peer", "kind": "strong",
+                     "skip": ("the one-process rehearsal shares at most 4 ranks per GPU" if sh and n > 4 * ndev
+                              else None),
+                     "cmd": [mg, "jacobi", "--halo", "peer", *(["--shared"] if sh else []), "--gpus", str(n),
+                             "--iters", steps[1], "--warmup", steps[3]]})
+    return jobs
+
+
+def value_of(rec: dict) -> Optional[float]:
+    for k in ("value",):
+        if k in rec:
+            return float(rec[k])
+    return None
+
+
+def ms_of(rec: dict) -> Optional[float]:
+    for k in ("ms_per_step", "ms_per_iter"):
+        if k in rec:
+            return float(rec[k])
+    if rec.get("unit") == "ms/iteration":
+        return float(rec["value"])
+    return None
+
+
+def efficiencies(rows: List[dict]) -> None:
+    base: Dict[str, dict] = {}
+    for r in rows:
+        if r["n"] == 1 and r["status"] == "ok":
+            base[r["name"]] = r
+    for r in rows:
+        b = base.get(r["name"]) or base.get(r["name"].replace("/rccl", "/peer"))
+        r["efficiency"] = None
+        if r["status"] != "ok" or b is None:
+            continue
+        if r["kind"] == "weak" and r.get("value") and b.get("value"):
+            r["efficiency"] = round(r["value"] / (r["n"] * b["value"]), 4)
+        elif r["kind"] == "strong" and r.get("ms") and b.get("ms"):
+            r["efficiency"] = round(b["ms"] / (r["n"] * r["ms"]), 4)
+            r["speedup"] = round(b["ms"] / r["ms"], 3)
+
+
+def plot(rows: List[dict], path: str, title: str) -> Optional[str]:
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except Exception:  # noqa: BLE001
+        return None
+    fig, (ax1, ax2) = plt.subplots(1, 2, figsize=(13, 5))
+    ns = sorted({r["n"] for r in rows})
+    for name in sorted({r["name"] for r in rows if r["kind"] == "weak"}):
+        pts = [(r["n"], r["value"]) for r in rows if r["name"] == name and r["status"] == "ok" and r.get("value")]
+        if pts:
+            ax1.plot(*zip(*pts), marker="o", label=name)
+            b = [v for n, v in pts if n == 1]
+            if b:
+                ax1.plot(ns, [b[0] * n for n in ns], ls=":", color="gray")
+    ax1.set_xlabel("GPUs")
+    ax1.set_ylabel("Gpixel/s (whole job)")
+    ax1.set_title("weak scaling (dotted: ideal)")
+    ax1.set_xticks(ns)
+    ax1.legend(fontsize=8)
+    for name in sorted({r["name"] for r in rows if r["kind"] == "strong"}):
+        pts = [(r["n"], r["speedup"]) for r in rows if r["name"] == name and r.get("speedup")]
+        if pts:
+            ax2.plot(*zip(*pts), marker="o", label=name)
+    ax2.plot(ns, ns, ls=":", color="gray", label="ideal")
+    ax2.set_xlabel("GPUs")
+    ax2.set_ylabel("speedup vs 1 GPU")
+    ax2.set_title("strong scaling: Jacobi 16384^2 fp64")
+    ax2.set_xticks(ns)
+    ax2.legend(fontsize=8)
+    fig.suptitle(title)
+    fig.tight_layout()
+    fig.savefig(path, dpi=150)
+    plt.close(fig)
+    return path
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", default="1,2,4,8")
+    p.add_argument("--out", default="scaling")
+    p.add_argument("--device", choices=["auto", "cpu"], default="auto")
+    p.add_argument("--rehearse", action="store_true", help="ranks share the visible GPUs (gloo control plane)")
+    p.add_argument("--quick", action="store_true", help="fewer steps per run")
+    p.add_argument("--only", default="", help="run only jobs whose name contains this string")
+    p.add_argument("--timeout", type=float, default=600.0, help="seconds per job")
+    a = p.parse_args(argv)
+    ns = [int(x) for x in a.gpus.split(",") if x.strip()]
+    out = a.out if os.path.isabs(a.out) else os.path.join(ROOT, a.out)
+    os.makedirs(out, exist_ok=True)
+    ndev = 0 if a.device == "cpu" else visible_gpus()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if a.device == "cpu" or a.rehearse:
+        env["MPX_DIST_BACKEND"] = "gloo"
+    rows: List[dict] = []
+    with open(os.path.join(out, "scaling.log"), "w") as log:
+        for n in ns:
+            for job in plan(n, a, ndev):
+                if a.only and a.only not in job["name"]:
+                    continue
+                row = {"name": job["name"], "kind": job["kind"], "n": n, "cmd": " ".join(job["cmd"])}
+                if job["skip"]:
+                    row["status"] = "skipped"
+                    row["reason"] = job["skip"]
+                else:
+                    res = run_job(job["cmd"], env, a.timeout, log)
+                    row["status"] = res["status"]
+                    row["wall_s"] = res["wall_s"]
+                    if res["status"] == "ok":
+                        rec = res["record"]
+                        row["value"] = value_of(rec)
+                        row["unit"] = rec.get("unit")
+                        row["ms"] = ms_of(rec)
+                        row["n_reported"] = rec.get("n_gpus")
+                        row["transport"] = (rec.get("config") or {}).get("transport") or rec.get("transport") or \
+                            rec.get("halo")
+                        row["world_size_seen"] = rec.get("world_size_seen")
+                        row["verified"] = rec.get("verified_bit_exact", rec.get("verified"))
+                    else:
+                        row["stderr_tail"] = res.get("stderr_tail")
+                rows.append(row)
+                print(json.dumps({k: row.get(k) for k in ("name", "n", "status", "value", "unit", "ms", "transport",
+                                                           "reason")}), flush=True)
+    efficiencies(rows)
+    meta = {"devices_visible": ndev, "device": a.device, "rehearse": a.rehearse, "gpus": ns,
+            "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    with open(os.path.join(out, "scaling.json"), "w") as f:
+        json.dump({"meta": meta, "runs": rows}, f, indent=1)
+    cols = ["name", "kind", "n", "status", "value", "unit", "ms", "efficiency", "speedup", "transport", "verified",
+            "reason"]
+    with open(os.path.join(out, "scaling.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=cols, extrasaction="ignore")
+        w.writeheader()
+        for r in rows:
+            w.writerow(r)
+    title = f"mpx scaling ({'CPU/gloo dry run' if a.device == 'cpu' else 'rehearsal: ranks share GPUs' if a.rehearse else 'one rank per MI355X'})"
+    png = plot(rows, os.path.join(out, "scaling.png"), title)
+    print(json.dumps({"scaling_json": os.path.join(out, "scaling.json"), "plot": png,
+                      "ok": sum(r["status"] == "ok" for r in rows), "skipped": sum(r["status"] == "skipped" for r in rows),
+                      "failed": sum(r["status"] not in ("ok", "skipped") for r in rows)}), flush=True)
+    return 0 if all(r["status"] in ("ok", "skipped") for r in rows) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
