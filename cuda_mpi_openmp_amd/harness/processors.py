@@ -19,11 +19,14 @@ from __future__ import annotations
 
 import os
 import shutil
+import subprocess
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from ..utils.imgdata import ImgData, encode_data, hex_groups, normalize_hex
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 LAB_IMAGE_FILES = [
     "stalker2.png", "98.data", "AoE.png", "doom.png", "hf2.png", "starcraft.png", "warcraft.png",
@@ -108,9 +111,21 @@ class _ImageLabProcessor(LabProcessor):
     def __init__(self, seed: int = 42, atol: float = 1e-10, precision_array: int = 10,
                  extra_links_to_png: Optional[List[str]] = None, dir_to_data: Optional[str] = None,
                  dir_to_data_out: Optional[str] = None, dir_to_data_out_gt: Optional[str] = None,
-                 lab_dir: Optional[str] = None, synthetic: Optional[str] = None, **_):
+                 lab_dir: Optional[str] = None, synthetic: Optional[str] = None, verify: str = "auto", **_):
         super().__init__(seed)
         self.atol, self.precision_array = atol, precision_array
+        # verify: "gt" = ground truth where it exists, other images pass (the
+        # reference, lab2_processor.py:139-144); "cpu" = every image without GT
+        # is compared byte for byte with the OpenMP CPU reference program's
+        # output (labs/<lab>/src/cpu_omp_exe, run once per image); "auto" =
+        # "cpu" when that program is built, else "gt" with a warning.
+        if verify not in ("auto", "gt", "cpu"):
+            raise ValueError("verify must be auto, gt or cpu")
+        self.cpu_oracle = os.path.join(REPO_ROOT, "labs", self.lab, "src", "cpu_omp_exe")
+        if verify == "cpu" and not os.path.exists(self.cpu_oracle):
+            raise FileNotFoundError(f"--verify cpu needs {self.cpu_oracle} (make apps)")
+        self.verify = "cpu" if verify == "cpu" or (verify == "auto" and os.path.exists(self.cpu_oracle)) else "gt"
+        self._expected: Dict[int, bytes] = {}
         if dir_to_data is None:
             dir_to_data = os.path.join(lab_dir, "data") if lab_dir else f"./{self.lab}/data"
         dir_to_data = os.path.normpath(dir_to_data)
@@ -176,12 +191,45 @@ class _ImageLabProcessor(LabProcessor):
     def get_task_result(self, payload: str, **kwargs):
         return ImgData(kwargs["out_path_res"])
 
+    def task_stdin(self, item: ImgData, out_path: str) -> str:
+        """The CPU program's stdin for ``item`` (the task without launch geometry)."""
+        return f"{item.data_path}\n{out_path}"
+
+    def cpu_expected(self, idx: int) -> bytes:
+        """The OpenMP CPU reference program's output bytes for input ``idx``
+        (computed once, kept under the output directory)."""
+        if idx not in self._expected:
+            item = self.inputs[idx]
+            d = os.path.join(self.dir_to_data_out, "_cpu_reference")
+            os.makedirs(d, exist_ok=True)
+            out = os.path.join(d, f"{item.data_name}.data")
+            r = subprocess.run([self.cpu_oracle], input=self.task_stdin(item, out), capture_output=True, text=True,
+                               timeout=600)
+            if r.returncode != 0:
+                raise RuntimeError(f"CPU reference failed on {item.data_name}: {r.stderr[-500:]}")
+            with open(out, "rb") as f:
+                self._expected[idx] = f.read()
+        return self._expected[idx]
+
     def verify_result(self, result: ImgData, **kwargs) -> bool:
         idx = kwargs["idx_data"]
         result.idx = idx
         gt = self.ground_truth.get(idx)
         if gt is None:
-            return True
+            if self.verify != "cpu":
+                return True  # reference behaviour (lab2_processor.py:139-144): no GT, no check
+            want = self.cpu_expected(idx)
+            ok = result.raw == want
+            if not ok:
+                a = np.frombuffer(result.raw, dtype=np.uint8)
+                b = np.frombuffer(want, dtype=np.uint8)
+                n = min(a.size, b.size)
+                bad = np.flatnonzero(a[:n] != b[:n])
+                first = int(bad[0]) if bad.size else n
+                print(f"[verify_result] FAILED `verify_result` vs CPU reference: `{result.data_name}`: "
+                      f"{bad.size + abs(a.size - b.size)} bytes differ, first at byte {first} "
+                      f"(pixel {(first - 8) // 4 if first >= 8 else 'header'})")
+            return ok
         ok = normalize_hex(result.hex) == normalize_hex(gt.hex)
         if not ok:
             src = self.inputs[idx]
@@ -198,7 +246,7 @@ class Lab2Processor(_ImageLabProcessor):
     def pre_process(self, **kwargs):
         item = self.next_item()
         out = self._out_path(kwargs["device_info"], item)
-        return f"{item.data_path}\n{out}", {"idx_data": item.idx, "out_path_res": out}, self._debug(item)
+        return self.task_stdin(item, out), {"idx_data": item.idx, "out_path_res": out}, self._debug(item)
 
 
 def random_class_points(w: int, h: int, count_pts: Optional[int], rng: np.random.RandomState) -> np.ndarray:
@@ -229,14 +277,18 @@ class Lab3Processor(_ImageLabProcessor):
             if not 0 < len(self.classes[i]) <= MAX_CLASSES:
                 raise ValueError(f"need 0 < classes <= {MAX_CLASSES}")
 
+    def task_stdin(self, item: ImgData, out_path: str) -> str:
+        cls = self.classes[item.idx]
+        rows = "\n".join(f"{len(c)} " + " ".join(str(int(v)) for v in np.asarray(c).reshape(-1)) for c in cls)
+        return f"{item.data_path}\n{out_path}\n{len(cls)}\n{rows}"
+
     def pre_process(self, **kwargs):
         item = self.next_item()
         out = self._out_path(kwargs["device_info"], item)
         cls = self.classes[item.idx]
-        rows = "\n".join(f"{len(c)} " + " ".join(str(int(v)) for v in np.asarray(c).reshape(-1)) for c in cls)
         dbg = self._debug(item)
         dbg["stat_init_pts"] = f"Count Classes: {len(cls)}, Count Points: {set(len(c) for c in cls)}"
-        return f"{item.data_path}\n{out}\n{len(cls)}\n{rows}", {"idx_data": item.idx, "out_path_res": out}, dbg
+        return self.task_stdin(item, out), {"idx_data": item.idx, "out_path_res": out}, dbg
 
 
 LAB5_TYPES = {"int": np.int32, "float": np.float32, "uchar": np.uint8}

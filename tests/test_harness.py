@@ -112,6 +112,35 @@ def test_harness_lab2_detects_wrong_output(tmp_path):
     assert os.path.exists(lab / "src" / "failed_fake_exe.csv")
 
 
+def test_harness_verify_cpu_catches_one_lsb(tmp_path):
+    """Images without GT are checked against the OpenMP CPU reference program
+    (--verify cpu), not passed unconditionally: a 1-LSB corruption of one
+    pixel of the metric_calc/large images fails; the honest program passes."""
+    lab = _copy_lab(tmp_path, "lab2")
+    shutil.copytree(os.path.join(ROOT, "labs", "lab2", "metric_calc"), lab / "metric_calc")
+    real = os.path.join(ROOT, "labs", "lab2", "src", "cpu_omp_exe")
+    fake = lab / "src" / "lsb_exe"
+    fake.write_text(f"""#!{sys.executable}
+import subprocess, sys
+stdin = sys.stdin.read()
+r = subprocess.run([{real!r}], input=stdin, capture_output=True, text=True)
+out = stdin.split()[1]
+b = bytearray(open(out, "rb").read())
+b[8 + 4 * (len(b) // 8)] ^= 1  # one LSB of one pixel's R channel
+open(out, "wb").write(bytes(b))
+sys.stdout.write(r.stdout)
+""")
+    fake.chmod(0o755)
+    large = str(lab / "metric_calc" / "large")
+    r = _run_test(["--binary_path_cuda", str(fake), "--k_times", "3", "--kernel_sizes", "[[null, null]]",
+                   "--dir_to_data", large, "--verify", "cpu"], tmp_path)
+    assert "FAILED" in r.stdout and "vs CPU reference" in r.stdout, r.stdout[-2000:]
+    assert os.path.exists(lab / "src" / "failed_lsb_exe.csv")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--k_times", "3", "--kernel_sizes",
+                   "[[null, null]]", "--dir_to_data", large, "--verify", "cpu"], tmp_path)
+    assert r.returncode == 0 and "SUCCESS" in r.stdout and "FAILED" not in r.stdout, r.stdout[-2000:]
+
+
 def test_harness_lab1_cpu(tmp_path):
     lab = _copy_lab(tmp_path, "lab1")
     r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--k_times", "2", "--kernel_sizes",
@@ -194,3 +223,12 @@ def test_harness_lab5_gpu_vs_cpu(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
     assert df["test_verification_result"].all() and (df["time_kernel_exe_ms"] >= 0).all()
+
+
+def test_metric_calc_ground_truth_matches_cpu_reference():
+    """The committed metric_calc GT (tools/make_metric_gt.py) is exactly the C
+    reference's output on every bucket image."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "make_metric_gt.py"), "--check"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("ok ") == 13

@@ -135,7 +135,11 @@ def ms_of(rec: dict) -> Optional[float]:
     return None
 
 
-def efficiencies(rows: List[dict]) -> None:
+def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
+    """Scaling efficiency vs N = 1. In a rehearsal all ranks share the same
+    GPUs, so the meaningful number is ``retained``: the fraction of the
+    single-rank throughput the N-rank decomposition keeps on that hardware
+    (1.0 = the halos and the ordering cost nothing)."""
     base: Dict[str, dict] = {}
     for r in rows:
         if r["n"] == 1 and r["status"] == "ok":
@@ -147,9 +151,13 @@ def efficiencies(rows: List[dict]) -> None:
             continue
         if r["kind"] == "weak" and r.get("value") and b.get("value"):
             r["efficiency"] = round(r["value"] / (r["n"] * b["value"]), 4)
+            if rehearse:
+                r["retained"] = round(r["value"] / b["value"], 4)
         elif r["kind"] == "strong" and r.get("ms") and b.get("ms"):
             r["efficiency"] = round(b["ms"] / (r["n"] * r["ms"]), 4)
             r["speedup"] = round(b["ms"] / r["ms"], 3)
+            if rehearse:
+                r["retained"] = r["speedup"]
 
 
 def plot(rows: List[dict], path: str, title: str) -> Optional[str]:
@@ -238,13 +246,13 @@ def main(argv=None) -> int:
                 rows.append(row)
                 print(json.dumps({k: row.get(k) for k in ("name", "n", "status", "value", "unit", "ms", "transport",
                                                            "reason")}), flush=True)
-    efficiencies(rows)
+    efficiencies(rows, a.rehearse)
     meta = {"devices_visible": ndev, "device": a.device, "rehearse": a.rehearse, "gpus": ns,
             "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
     with open(os.path.join(out, "scaling.json"), "w") as f:
         json.dump({"meta": meta, "runs": rows}, f, indent=1)
-    cols = ["name", "kind", "n", "status", "value", "unit", "ms", "efficiency", "speedup", "transport", "verified",
-            "reason"]
+    cols = ["name", "kind", "n", "status", "value", "unit", "ms", "efficiency", "speedup", "retained", "transport",
+            "verified", "reason"]
     with open(os.path.join(out, "scaling.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=cols, extrasaction="ignore")
         w.writeheader()
