@@ -22,6 +22,42 @@ static double now_ms(void) {
 #endif
 }
 
+#ifdef _OPENMP
+/* OpenMP build: the rest of stdin read once, both vectors parsed in parallel
+ * (mpx_parse_doubles: one strtod per token, the values scanf("%lf") yields) */
+static char *g_in = NULL;
+static size_t g_len = 0, g_pos = 0;
+
+static int slurp_stdin(void) {
+    size_t cap = 1 << 20;
+    g_in = (char *)malloc(cap + 1);
+    if (!g_in) return 1;
+    size_t got;
+    while ((got = fread(g_in + g_len, 1, cap - g_len, stdin)) > 0) {
+        g_len += got;
+        if (g_len == cap) {
+            char *p = (char *)realloc(g_in, 2 * cap + 1);
+            if (!p) return 1;
+            g_in = p;
+            cap *= 2;
+        }
+    }
+    g_in[g_len] = 0;
+    return 0;
+}
+
+static int read_vec(double *v, int n, const char *what) {
+    size_t end = g_pos;
+    const int64_t got = mpx_parse_doubles(g_in, g_len, g_pos, n, v, &end);
+    if (got != n) {
+        fprintf(stderr, "[ERROR CPU] %s: expected %d values, got %lld\n", what, n, (long long)got);
+        return 1;
+    }
+    g_pos = end;
+    return 0;
+}
+#else
+/* serial build: scanf per value, the reference's host loop (lab1/src/main.c) */
 static int read_vec(double *v, int n, const char *what) {
     for (int i = 0; i < n; ++i)
         if (scanf("%lf", &v[i]) != 1) {
@@ -30,6 +66,7 @@ static int read_vec(double *v, int n, const char *what) {
         }
     return 0;
 }
+#endif
 
 int main(void) {
     int n;
@@ -45,14 +82,37 @@ int main(void) {
         fprintf(stderr, "[ERROR CPU] allocation failed\n");
         goto done;
     }
+#ifdef _OPENMP
+    if (slurp_stdin()) {
+        fprintf(stderr, "[ERROR CPU] out of memory reading stdin\n");
+        goto done;
+    }
+#endif
     if (read_vec(a, n, "first vector") || read_vec(b, n, "second vector")) goto done;
     const double t0 = now_ms();
     mpx_cpu_vsub_f64(a, b, c, n);
     const double t1 = now_ms();
     printf("CPU execution time: <%f ms>\n", t1 - t0);
+#ifdef _OPENMP
+    {
+        size_t len = 0;
+        char *txt = mpx_format_e10(c, n, &len);
+        if (!txt && n) {
+            fprintf(stderr, "[ERROR CPU] out of memory formatting the result\n");
+            goto done;
+        }
+        fflush(stdout);
+        if (len) fwrite(txt, 1, len, stdout);
+        free(txt);
+    }
+#else
     for (int i = 0; i < n; ++i) printf("%.10e ", c[i]);
+#endif
     rc = 0;
 done:  /* one exit path: the host sanitizer build checks for leaks */
+#ifdef _OPENMP
+    free(g_in);
+#endif
     free(a);
     free(b);
     free(c);

@@ -31,16 +31,15 @@ int main() {
         return 1;
     }
     std::vector<double> a(n), b(n), c(n);
-    for (int i = 0; i < n; ++i)
-        if (!in.next_double(a[i])) {
-            std::fprintf(stderr, "[ERROR CPU] first vector: expected %d values, got %d\n", n, i);
-            return 1;
-        }
-    for (int i = 0; i < n; ++i)
-        if (!in.next_double(b[i])) {
-            std::fprintf(stderr, "[ERROR CPU] second vector: expected %d values, got %d\n", n, i);
-            return 1;
-        }
+    // both vectors parsed in parallel (host.hpp Scanner::next_doubles)
+    if (const int64_t got = in.next_doubles(a.data(), n); got != n) {
+        std::fprintf(stderr, "[ERROR CPU] first vector: expected %d values, got %lld\n", n, (long long)got);
+        return 1;
+    }
+    if (const int64_t got = in.next_doubles(b.data(), n); got != n) {
+        std::fprintf(stderr, "[ERROR CPU] second vector: expected %d values, got %lld\n", n, (long long)got);
+        return 1;
+    }
 
     const int nparts = parts_from_env();
     float ms = 0.0f;

@@ -536,13 +536,6 @@ void vsub_worker(const Args &a, Shared &sh, int rank) {
 
 int main(int argc, char **argv) {
     Args a = parse(argc, argv);
-    int ndev = 0;
-    HIP_OK(hipGetDeviceCount(&ndev));
-    if (ndev < 1) {
-        fprintf(stderr, "[ERROR HIP] no GPU visible\n");
-        return 1;
-    }
-    const int N = a.gpus > 0 ? a.gpus : ndev;
     // --halo none: ablation of the peer mode (same kernels and launches, no
     // neighbour reads or waits; wrong answer) to isolate the ordering cost
     const bool peer = a.mode == "jacobi" && (a.halo == "peer" || a.halo == "none");
@@ -550,7 +543,18 @@ int main(int argc, char **argv) {
         fprintf(stderr, "[ERROR] --halo must be rccl, peer or none\n");
         return 2;
     }
-    if (a.shared && (!peer || N > 4 * ndev)) {
+    if (a.shared && !peer) {
+        fprintf(stderr, "[ERROR] --shared needs jacobi --halo peer\n");
+        return 2;
+    }
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (ndev < 1) {
+        fprintf(stderr, "[ERROR HIP] no GPU visible\n");
+        return 1;
+    }
+    const int N = a.gpus > 0 ? a.gpus : ndev;
+    if (a.shared && N > 4 * ndev) {
         fprintf(stderr, "[ERROR] --shared needs jacobi --halo peer and at most 4 ranks per device\n");
         return 2;
     }

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "mpx/capi.h"
+#include "../../src/cpu/cpu_kernels.h"
 
 // Same stderr format as the reference's CSC macro (lab1/src/main.cu:5-13),
 // naming HIP; the process exits with status 1.
@@ -286,6 +287,14 @@ class Scanner {
         v = (int)x;
         return true;
     }
+    // the next `count` numbers in parallel (libmpx's OpenMP mpx_parse_doubles:
+    // one strtod per token, so the values are those of next_double)
+    int64_t next_doubles(double *out, int64_t count) {
+        size_t end = pos_;
+        const int64_t got = mpx_parse_doubles(buf_.c_str(), buf_.size(), pos_, count, out, &end);
+        if (got == count) pos_ = end;
+        return got;
+    }
     bool next_double(double &v) {
         skip_ws();
         if (pos_ >= buf_.size()) return false;
@@ -306,21 +315,18 @@ class Scanner {
 };
 
 // ---- stdout ----
-// Buffered "%.10e " writer (reference lab1/src/to_plot.cu:86-88 prints one
-// printf per element).
+// "%.10e " writer (reference lab1/src/to_plot.cu:86-88 prints one printf per
+// element): formatted in parallel per thread range (mpx_format_e10), written
+// in order with one fwrite.
 inline void print_e10(const double *v, int64_t n) {
-    std::vector<char> out;
-    out.reserve(64 * 1024);
-    char tmp[64];
-    for (int64_t i = 0; i < n; ++i) {
-        const int k = std::snprintf(tmp, sizeof(tmp), "%.10e ", v[i]);
-        out.insert(out.end(), tmp, tmp + k);
-        if (out.size() > 60 * 1024) {
-            std::fwrite(out.data(), 1, out.size(), stdout);
-            out.clear();
-        }
+    size_t len = 0;
+    char *buf = mpx_format_e10(v, n, &len);
+    if (!buf && n) {
+        std::fprintf(stderr, "[ERROR CPU] out of memory formatting %lld values\n", (long long)n);
+        std::exit(1);
     }
-    if (!out.empty()) std::fwrite(out.data(), 1, out.size(), stdout);
+    if (len) std::fwrite(buf, 1, len, stdout);
+    std::free(buf);
 }
 
 }  // namespace host

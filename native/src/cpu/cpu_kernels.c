@@ -7,6 +7,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -31,6 +32,131 @@ int mpx_cpu_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* ---- lab1 text I/O ---- */
+static int is_ws(char c) { return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\f' || c == '\v'; }
+
+int64_t mpx_parse_doubles(const char *buf, size_t len, size_t pos, int64_t count, double *out, size_t *end) {
+    *end = pos;
+    if (count <= 0) return 0;
+    while (pos < len && is_ws(buf[pos])) ++pos;
+    int T = 1;
+#ifdef _OPENMP
+    T = omp_get_max_threads();
+    if ((int64_t)(len - pos) < ((int64_t)1 << 16)) T = 1;
+#endif
+    /* chunk k starts at a token start (or len): cut evenly, then move each cut
+     * past the token it lands in and the whitespace after it */
+    size_t *start = (size_t *)malloc(sizeof(size_t) * (size_t)(T + 1));
+    int64_t *ntok = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
+    if (!start || !ntok) {
+        free(start);
+        free(ntok);
+        return 0;
+    }
+    start[0] = pos;
+    start[T] = len;
+    for (int k = 1; k < T; ++k) {
+        size_t c = pos + (len - pos) / (size_t)T * (size_t)k;
+        if (c < start[k - 1]) c = start[k - 1];
+        if (c > pos && !is_ws(buf[c - 1]))
+            while (c < len && !is_ws(buf[c])) ++c;
+        while (c < len && is_ws(buf[c])) ++c;
+        start[k] = c;
+    }
+    /* pass 1: tokens per chunk */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+#endif
+    for (int k = 0; k < T; ++k) {
+        int64_t c = 0;
+        int in_tok = 0;
+        for (size_t i = start[k]; i < start[k + 1]; ++i) {
+            const int w = is_ws(buf[i]);
+            if (!w && !in_tok) ++c;
+            in_tok = !w;
+        }
+        ntok[k + 1] = c;
+    }
+    for (int k = 0; k < T; ++k) ntok[k + 1] += ntok[k];
+    /* pass 2: strtod each token whose index is < count */
+    int64_t bad = count;  /* first malformed token index */
+    size_t last_end = pos;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 1) num_threads(T) reduction(min : bad)
+#endif
+    for (int k = 0; k < T; ++k) {
+        int64_t idx = ntok[k];
+        size_t i = start[k];
+        while (idx < count && i < start[k + 1]) {
+            while (i < start[k + 1] && is_ws(buf[i])) ++i;
+            if (i >= start[k + 1]) break;
+            char *e = NULL;
+            out[idx] = strtod(buf + i, &e);
+            if (e == buf + i) {  /* not a number */
+                if (idx < bad) bad = idx;
+                break;
+            }
+            size_t j = i;
+            while (j < start[k + 1] && !is_ws(buf[j])) ++j;
+            if ((size_t)(e - buf) != j) {  /* trailing junk in the token */
+                if (idx < bad) bad = idx;
+                break;
+            }
+            if (idx == count - 1) last_end = j;
+            i = j;
+            ++idx;
+        }
+    }
+    const int64_t got = ntok[T] < count ? ntok[T] : count;
+    free(start);
+    free(ntok);
+    const int64_t n = bad < got ? bad : got;
+    if (n == count) *end = last_end;
+    return n;
+}
+
+char *mpx_format_e10(const double *v, int64_t n, size_t *len) {
+    int T = 1;
+#ifdef _OPENMP
+    T = omp_get_max_threads();
+    if (n < 4096) T = 1;
+#endif
+    char **part = (char **)calloc((size_t)T, sizeof(char *));
+    size_t *plen = (size_t *)calloc((size_t)T, sizeof(size_t));
+    int fail = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 1) num_threads(T) reduction(| : fail)
+#endif
+    for (int k = 0; k < T; ++k) {
+        const int64_t a = n * k / T, b = n * (k + 1) / T;
+        char *buf = (char *)malloc((size_t)(b - a) * 32 + 1);
+        if (!buf) {
+            fail |= 1;
+            continue;
+        }
+        size_t o = 0;
+        for (int64_t i = a; i < b; ++i) o += (size_t)snprintf(buf + o, 32, "%.10e ", v[i]);
+        part[k] = buf;
+        plen[k] = o;
+    }
+    size_t total = 0;
+    for (int k = 0; k < T; ++k) total += plen[k];
+    char *outb = fail ? NULL : (char *)malloc(total + 1);
+    if (outb) {
+        size_t o = 0;
+        for (int k = 0; k < T; ++k) {
+            memcpy(outb + o, part[k], plen[k]);
+            o += plen[k];
+        }
+        outb[total] = 0;
+    }
+    for (int k = 0; k < T; ++k) free(part[k]);
+    free(part);
+    free(plen);
+    *len = outb ? total : 0;
+    return outb;
 }
 
 void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n) {

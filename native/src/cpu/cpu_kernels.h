@@ -11,6 +11,7 @@
 #ifndef MPX_CPU_KERNELS_H
 #define MPX_CPU_KERNELS_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -27,6 +28,18 @@ void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, con
 double mpx_cpu_jacobi_f64(const double *u, double *un, int cols, int pitch, int r0, int r1);
 /* lab5: ascending sort in place, same order as mpx_sort (dtype: enum mpx_sort_dtype). */
 void mpx_cpu_sort(void *data, int64_t n, int dtype);
+
+/* lab1 host text I/O (reference lab1/src/main.cu:46-52 scanf per value,
+ * :82-84 printf per value), parallel over OpenMP threads in the -fopenmp builds
+ * and serial otherwise; byte-identical to the serial strtod / "%.10e " path.
+ * mpx_parse_doubles: the next `count` whitespace-separated numbers of
+ * buf[pos, len) (buf NUL-terminated at len) into out[]; returns how many were
+ * parsed (< count: missing or malformed token at that index) and sets *end to
+ * the offset just past the last parsed token.
+ * mpx_format_e10: "%.10e " for each of n values, as one malloc'd buffer of
+ * *len bytes (caller frees). */
+int64_t mpx_parse_doubles(const char *buf, size_t len, size_t pos, int64_t count, double *out, size_t *end);
+char *mpx_format_e10(const double *v, int64_t n, size_t *len);
 
 /* lab3 host statistics H1 (reference lab3/src/main.cu:102-152). Returns 0, or
  * -1 when a coordinate lies outside the image. */

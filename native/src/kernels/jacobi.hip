@@ -248,7 +248,6 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
                 if (i == r0 - 1 && up_row) q = up_row;
                 if (i == r1 && dn_row) q = dn_row;
                 if (q) {
-                    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(q), 0, 16,
                                                                                        0x00020000);
                     return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kCpolSystem));
