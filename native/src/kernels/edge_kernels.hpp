@@ -2,6 +2,8 @@
 // tools/kbench variant harness). See edge.hip for the design notes.
 #pragma once
 
+#include <type_traits>
+
 #include "internal.hpp"
 
 namespace mpx {
@@ -544,16 +546,25 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // branches are scalar and hipcc keeps counted vmcnt waits across them
     const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gw >= nwaves) return;  // wave-uniform
-    // strip_minor: consecutive waves take horizontally adjacent strips of the
-    // same rows, so the waves running together stream contiguous row pieces
+    // strip_minor bit 0: consecutive waves take horizontally adjacent strips of
+    // the same rows, so the waves running together stream contiguous row pieces
     // (DRAM-page friendly, like a copy); otherwise they walk one strip downwards.
-    const int strip = strip_minor ? gw % strips : gw / segs_per_strip;
-    const int sg0 = strip_minor ? gw / strips : gw - strip * segs_per_strip;
+    // Bit 1 (alternate): odd segments walk their rows upwards. The segments of
+    // one resident round all start together, so with every segment walking
+    // down, the K-1 input rows two vertical neighbours share are read at the
+    // START of the lower segment and at the END of the upper one, a whole
+    // segment apart — long gone from L2. Walking alternate segments up, each
+    // shared band is read by both neighbours at the same moment (both ends or
+    // both starts), and the second read hits L2.
+    const bool minor = strip_minor & 1;
+    const int strip = minor ? gw % strips : gw / segs_per_strip;
+    const int sg0 = minor ? gw / strips : gw - strip * segs_per_strip;
     // both boundary segments first (strip-minor order): in a slab their halo
     // rows may come from a neighbour's HBM over xGMI (RowSrc), the slowest
     // loads of the launch, so their waves start in the first round
-    const int sg = (!strip_minor || segs_per_strip < 3 || sg0 == 0) ? sg0
+    const int sg = (!minor || segs_per_strip < 3 || sg0 == 0) ? sg0
                    : (sg0 == 1 ? segs_per_strip - 1 : sg0 - 1);
+    const bool up = (strip_minor & 2) && (sg & 1);  // wave-uniform
     const int ys = oy0 + sg * seg;
     const int ye = min(ys + seg, oy1);
     const int x0 = strip * G::OW;
@@ -573,8 +584,9 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // The sched_barrier pins every load at its program position: left alone the
     // scheduler sinks prefetches towards their first use (lower register
     // pressure), which turns the ring back into load-then-wait.
+    const int iy_last = ye - 1 + (K - 1 - A);  // last input row (upward walk: input row 0)
     auto load_row = [&](int i) -> uint2 {
-        const int gy = mpx_clampi(iy0 + i, y_lo, y_hi);
+        const int gy = mpx_clampi(up ? iy_last - i : iy0 + i, y_lo, y_hi);
         // wave-uniform row source select (scalar): own slab or a neighbour's
         const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
         const uint32_t *row = src + (int64_t)gy * pitch;
@@ -662,22 +674,27 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // in whole groups of D (ring slots are then compile-time constants) with no
     // branch around any memory operation; output rows past the segment end are
     // computed and dropped by the store's bounds check.
-    auto row_step = [&](int g, int v) {
+    // the ring slot of window row dy (0 = top) once input row index i (slot u)
+    // is consumed: walking down the newest row is the bottom one, walking up
+    // the top one; the tap chains always run top to bottom (bit-exactness)
+    auto row_step = [&](auto upc, int g, int v) {
+        constexpr bool UP = decltype(upc)::value;
         const int u = (K - 1 + v) % K;      // window slot of the newest row
         const int q = (K - 1 + v) % D;      // its prefetch slot
         const int i = K - 1 + g * D + v;    // its input row index
         const uint2 px = fix_pair(pre[q]);
         pre[q] = load_row(i + D);
         consume(u, px);
-        const int y = ys + g * D + v;       // output row completed by row i
+        const int y = UP ? ye - 1 - (g * D + v) : ys + g * D + v;  // output row completed by row i
+        auto slot = [&](int dy) { return UP ? (u + K - dy) % K : (u + 1 + dy) % K; };
         // both output columns at once: packed FMAs over the (w[dx], w[dx+1]) pairs
         f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
         if constexpr (SEP) {
-            gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[(u + 1 + dy) % K]; });
+            gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[slot(dy)]; });
             const float sx = sep_scale<F, K, false>(taps);
             gx = gx * f2_t{sx, sx};
             if constexpr (TWO) {
-                gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[(u + 1 + dy) % K]; });
+                gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[slot(dy)]; });
                 const float sy = sep_scale<F, K, true>(taps);
                 gy = gy * f2_t{sy, sy};
             }
@@ -685,7 +702,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             bool sx = false, sy = false;
 #pragma unroll
             for (int dy = 0; dy < K; ++dy) {
-                const int r = (u + 1 + dy) % K;
+                const int r = slot(dy);
 #pragma unroll
                 for (int dx = 0; dx < K; ++dx) {
                     const f2_t pv = (dx & 1) ? wo[r][dx >> 1] : we[r][dx >> 1];
@@ -710,8 +727,8 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         // (g, g, g, alpha): one v_perm_b32 per pixel — selector bytes 0-2
         // take g's low byte (g <= 255), byte 3 takes the source pixel's
         // alpha (selector 7 = byte 3 of the first operand); no alpha mask
-        const uint32_t v0 = __builtin_amdgcn_perm(alp0[(u + 1 + A) % K], g0, 0x07000000u);
-        const uint32_t v1 = __builtin_amdgcn_perm(alp1[(u + 1 + A) % K], g1, 0x07000000u);
+        const uint32_t v0 = __builtin_amdgcn_perm(alp0[slot(A)], g0, 0x07000000u);
+        const uint32_t v1 = __builtin_amdgcn_perm(alp1[slot(A)], g1, 0x07000000u);
         // Branch-free stores: a buffer descriptor spanning exactly this
         // output row; lanes (or padded rows) with nothing to store get an
         // out-of-range offset and the hardware bounds check drops them.
@@ -719,7 +736,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         // unknowable to hipcc and cost a vmcnt(0) drain of the ring.
         // rows past the segment get a zero-length descriptor (scalar select),
         // lanes with nothing to store a constant out-of-range offset
-        const bool row_ok = y < ye;
+        const bool row_ok = UP ? y >= ys : y < ye;
         const int yc = row_ok ? y : ys;
         const __amdgpu_buffer_rsrc_t orow =
             __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
@@ -738,18 +755,22 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // a wave-uniform exit: rows past the segment are never computed
     const int nrows = ye - ys;
     const int nfull = nrows / D;
-    for (int g = 0; g < nfull; ++g) {
-#pragma unroll
-        for (int v = 0; v < D; ++v) row_step(g, v);
-    }
     const int rem = nrows - nfull * D;
-    if (rem > 0) {
+    auto run = [&](auto upc) {
+        for (int g = 0; g < nfull; ++g) {
 #pragma unroll
-        for (int v = 0; v < D; ++v) {
-            if (v >= rem) break;
-            row_step(nfull, v);
+            for (int v = 0; v < D; ++v) row_step(upc, g, v);
         }
-    }
+        if (rem > 0) {
+#pragma unroll
+            for (int v = 0; v < D; ++v) {
+                if (v >= rem) break;
+                row_step(upc, nfull, v);
+            }
+        }
+    };
+    if (up) run(std::true_type{});  // wave-uniform branch
+    else run(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------

@@ -58,9 +58,19 @@ int launch_stream(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, 
 // of the unrolled row group.
 inline constexpr int kSegRows = 8;
 
+// Wave order of the launches (conv_wave_kernel's strip_minor bits): 1 =
+// strip-minor; 3 = strip-minor with alternating segment directions, so
+// vertically adjacent segments read their shared rows at the same time (L2
+// hits). Used for the long-segment two-filter separable path (launch_sep,
+// MAG2): sobel5 4096^2 over 6 rotated slab pairs (tools/kbench.py --rotate 6)
+// 31.8 -> 30.3 us, 4% above the 29.05 us strip-copy floor. The short-segment
+// paths keep 1 until measured on the same box.
+inline constexpr int kWaveOrder = 1;
+inline constexpr int kWaveOrderAlt = 3;
+
 template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, int BUFLD = 1>
 int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = 1,
+                const Taps &taps, bool vec, hipStream_t s, int seg = kSegRows, int strip_minor = kWaveOrder,
                 edge::RowSrc rs = edge::RowSrc{}) {
     if (!rs.up) rs.up = in;
     if (!rs.dn) rs.dn = in;
@@ -106,12 +116,12 @@ int launch_named(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
                  const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs) {
     if constexpr (F::kK == K && F::kA == A && F::kMode == MODE) {
         if (same_taps<F, K * K>(taps))
-            return launch_wave<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
+            return launch_wave<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
     }
     if constexpr (sizeof...(More) > 0)
         return launch_named<K, A, MODE, More...>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
     else
-        return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, 1, rs);
+        return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
 }
 
 template <int K, int A, int MODE>
@@ -170,15 +180,16 @@ int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int
     // lighter single-filter passes short segments (MI355X 4096^2, named_taps_ab:
     // sobel5 auto 24.7 us vs 26.1 at 8; gauss5 8 rows 23.4 us vs 25.1 auto)
     constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
+    constexpr int order = MODE == MPX_CONV_MAG2 ? kWaveOrderAlt : kWaveOrder;
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
-            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
+            return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
         if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
-            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
+            return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }
-    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, 1, rs);
+    return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
 }
 
 

@@ -98,7 +98,9 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         MPX_CHECK_ARG(k == 5 && p1 >= 0, "separable variants: k = 5, segment rows >= 0 (0 = auto)");
         const Taps st = make_taps(k, wx, wy, true, true);
         const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
-        const int sm = p2 >= 1000 ? 0 : 1;
+        // p2 in [1000, 2000): strip-major; [2000, 3000): strip-minor with
+        // alternating segment direction (the production MAG2 order)
+        const int sm = p2 >= 2000 ? 3 : p2 >= 1000 ? 0 : 1;
         // p2 % 1000 = minimum prefetch depth in rows (0 / 4: production 5, 8: 10, 12: 15)
         const int pf = p2 % 1000;
         if (kind == 3 && pf == 8)
@@ -141,7 +143,9 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         // p1 = segment rows; p2 >= 1000 orders waves strip-major
         MPX_CHECK_ARG(p1 >= 1, "segment rows must be positive");
         const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
-        const int sm = p2 >= 1000 ? 0 : 1;
+        // p2 in [1000, 2000): strip-major; [2000, 3000): strip-minor with
+        // alternating segment direction (the production MAG2 order)
+        const int sm = p2 >= 2000 ? 3 : p2 >= 1000 ? 0 : 1;
         if (k == 5) {
             if (kind == 2)
                 return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps>(in, out, w, w, 0, h, 0, h - 1, taps, vec2, s, p1, sm);

@@ -288,3 +288,24 @@ def test_fast_sqrt_exhaustive(gpu, capsys):
     with capsys.disabled():
         print(f"\nfast sqrt mismatches over all fp32 in [0, 65025]: production {counts[0]}, bare v_sqrt {counts[1]}")
     assert counts[0] == 0
+
+
+@pytest.mark.parametrize("hw", [(5, 64), (23, 130), (47, 260), (200, 300), (1001, 517), (4096, 4096)])
+@pytest.mark.parametrize("seg", [0, 8, 11])
+def test_conv_alternating_segments_exact(gpu, hw, seg):
+    """Separable sobel5 with odd segments walking their rows upwards (tuning
+    variant kind 3, p2 = 2000) is bit-identical to the CPU reference, segment
+    tails and image edges included."""
+    import ctypes
+
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    f = ops.get_filter("sobel5")
+    wx, wy = f.c_taps()
+    img = smooth_img(*hw, seed=hw[0] + seg)
+    d = img.to(gpu)
+    out = torch.empty_like(d)
+    _native.check(L.mpx_conv_variant(d.data_ptr(), out.data_ptr(), hw[1], hw[0], 5, 3, seg, 2000, 1, wx, wy, 0))
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ops.conv(img, f))

@@ -85,6 +85,10 @@ def main():
     fs5 = ops.get_filter("sobel5")
     swx, swy = fs5.c_taps()
     sref = ops.conv(img, fs5)
+    for seg in (0, 16, 32, 48):  # alternating segment direction (production MAG2 order candidate)
+        variants[f"sobel5-sep/wave-const/seg{seg}/alt"] = (
+            (lambda seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 2000, 1,
+                                                              swx, swy, 0))), sref)
     for seg in (0, 8, 20, 24):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
