@@ -118,6 +118,7 @@ def test_harness_verify_cpu_catches_one_lsb(tmp_path):
     pixel of the metric_calc/large images fails; the honest program passes."""
     lab = _copy_lab(tmp_path, "lab2")
     shutil.copytree(os.path.join(ROOT, "labs", "lab2", "metric_calc"), lab / "metric_calc")
+    shutil.rmtree(lab / "metric_calc" / "large_out_gt")  # no GT: the CPU oracle decides
     real = os.path.join(ROOT, "labs", "lab2", "src", "cpu_omp_exe")
     fake = lab / "src" / "lsb_exe"
     fake.write_text(f"""#!{sys.executable}
