@@ -35,7 +35,7 @@ GPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/to_plot_hip_exe labs/lab$(L)/s
 CPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/cpu_exe labs/lab$(L)/src/cpu_omp_exe)
 MISC_APPS := labs/lab3/src/read_input_exe bin/gpu_info bin/hw1 bin/hw2 bin/mpx_mgpu
 
-.PHONY: all lib apps clean
+.PHONY: all lib apps tools clean
 all: lib apps
 lib: $(PYLIB) $(ALIB)
 apps: $(GPU_APPS) $(CPU_APPS) $(MISC_APPS)
@@ -103,6 +103,11 @@ bin/hw1: native/apps/hw1_quadratic.c | $(B)
 
 bin/hw2: native/apps/hw2_bubble_sort.c | $(B)
 	$(CC) $(CSER) $< -o $@
+
+# ---- stand-alone measurement tools (not part of `all`) ----
+tools: bin/mfma_valu_overlap
+bin/mfma_valu_overlap: tools/mfma_valu_overlap.hip | $(B)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 # ---- host-only sanitizer builds of the CPU references ----
 # GPU ASan / xnack+ code objects are not available on the MI355X pool, so the

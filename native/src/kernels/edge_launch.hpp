@@ -6,6 +6,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "edge_kernels.hpp"
 
@@ -61,12 +62,23 @@ inline constexpr int kSegRows = 8;
 // Wave order of the launches (conv_wave_kernel's strip_minor bits): 1 =
 // strip-minor; 3 = strip-minor with alternating segment directions, so
 // vertically adjacent segments read their shared rows at the same time (L2
-// hits). Used for the long-segment two-filter separable path (launch_sep,
-// MAG2): sobel5 4096^2 over 6 rotated slab pairs (tools/kbench.py --rotate 6)
-// 31.8 -> 30.3 us, 4% above the 29.05 us strip-copy floor. The short-segment
-// paths keep 1 until measured on the same box.
-inline constexpr int kWaveOrder = 1;
+// hits). Same-box A/B over 6 rotated 4096^2 slab pairs (tools/kbench.py
+// --rotate 6, tools/gpu_r2_order_ab.sh, two rounds each): sobel5 33.5 -> 32.4
+// us (kernel alone 31.8 -> 30.3), sobel5_dense 42.0 -> 40.0, gauss5 33.8 ->
+// 33.2, Roberts 32.0 -> 31.4 — every path at least as fast, so 3 everywhere.
+inline constexpr int kWaveOrder = 3;
 inline constexpr int kWaveOrderAlt = 3;
+
+// MPX_CONV_ORDER=1|3 forces the wave order of every conv launch (same-box A/B
+// of the production paths with tools/kbench.py); read once per process.
+inline int wave_order_override() {
+    static const int v = [] {
+        const char *e = std::getenv("MPX_CONV_ORDER");
+        const int o = e ? std::atoi(e) : 0;
+        return (o == 1 || o == 3) ? o : 0;
+    }();
+    return v;
+}
 
 template <int K, int A, int MODE, bool FAST, class F = edge::RuntimeTaps, int OWX = 0, int PF = 4, int BUFLD = 1>
 int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
@@ -74,6 +86,7 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
                 edge::RowSrc rs = edge::RowSrc{}) {
     if (!rs.up) rs.up = in;
     if (!rs.dn) rs.dn = in;
+    if (const int o = wave_order_override()) strip_minor = o;
     using G = edge::WaveGeom<K, A, OWX>;
     const int strips = (w + G::OW - 1) / G::OW;
     if (seg <= 0) {
