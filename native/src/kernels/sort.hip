@@ -479,6 +479,132 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(6))) 
     }
 }
 
+// LDS-only workgroup barrier: orders LDS accesses without waiting for the
+// block's global loads (the next tile's prefetch stays in flight across it)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// scan256_excl with LDS-only barriers
+__device__ __forceinline__ uint32_t scan256_excl_lds(uint32_t v, uint32_t *s_wsum) {
+    const int t = threadIdx.x, lane = t & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (t < 256 && lane == 63) s_wsum[t >> 6] = x;
+    lds_barrier();
+    uint32_t add = 0;
+    for (int w = 0; w < (t >> 6) && w < 4; ++w) add += s_wsum[w];
+    lds_barrier();
+    return x - v + add;
+}
+
+// reduce-then-scan scatter, persistent: kPersistBlocksPerCU blocks per CU walk
+// the tiles of their XCD's contiguous range (consecutive tiles stay XCD-local
+// so their output runs merge in L2) and load the next tile's keys while the
+// current one is ranked, scanned, staged and written — the per-tile phases
+// that left the memory system idle in the one-tile-per-block kernel. Barriers
+// are LDS-only so the prefetch stays in flight across them.
+constexpr int kPersistBlocksPerCU = 2;
+
+__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_kernel(
+    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift, int in_mode, int out_mode,
+    const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
+    __shared__ uint32_t s_keys[kRTile];
+    __shared__ uint32_t s_cnt[kRWaves][256];
+    __shared__ uint32_t s_dstart[256];
+    __shared__ uint32_t s_gbase[256];
+    __shared__ uint32_t s_wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t *tbl = reinterpret_cast<uint64_t *>(s_keys) + w * 256;
+    const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
+    const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
+    int tile = (int)((int64_t)ntiles * xcd / kNumXCDs) + (int)blockIdx.x / kNumXCDs;
+    if (tile >= t1) return;  // block-uniform
+    // digit bases of the whole array (the same for every tile of the pass)
+    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);
+
+    uint32_t raw[kRPer], nxt[kRPer];
+    auto load_tile = [&](uint32_t (&dst)[kRPer], int tl) {
+        const int64_t base = (int64_t)tl * kRTile + w * kRWaveKeys + lane;
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) {
+            const int64_t i = base + e * 64;
+            dst[e] = i < n ? in[i] : 0u;
+        }
+    };
+    load_tile(raw, tile);
+    for (; tile < t1; tile += per) {
+        const int64_t tile0 = (int64_t)tile * kRTile;
+        if (tile + per < t1) load_tile(nxt, tile + per);  // in flight under this tile's work
+        const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + tile] : 0u;
+        for (int i = t; i < kRWaves * 256; i += kRThreads) {
+            (&s_cnt[0][0])[i] = 0;
+            reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
+        }
+        lds_barrier();
+        uint32_t key[kRPer], rank[kRPer];
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e)  // pads (past n) rank last and are never stored
+            key[e] = tile0 + w * kRWaveKeys + lane + e * 64 < n ? to_key(raw[e], in_mode) : 0xffffffffu;
+        constexpr int kRG = 4;
+#pragma unroll
+        for (int g = 0; g < kRPer; g += kRG) {
+            uint64_t m[kRG];
+#pragma unroll
+            for (int e = 0; e < kRG; ++e) m[e] = match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
+            uint32_t old[kRG], pre[kRG];
+#pragma unroll
+            for (int e = 0; e < kRG; ++e) {
+                pre[e] = lanes_below(m[e]);
+                old[e] = 0;
+                if (pre[e] == 0) old[e] = atomicAdd(&s_cnt[w][(key[g + e] >> shift) & 255u], (uint32_t)__popcll(m[e]));
+            }
+#pragma unroll
+            for (int e = 0; e < kRG; ++e) {
+                const int leader = (int)__builtin_ctzll(m[e]);
+                rank[g + e] = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old[e]) + pre[e];
+            }
+        }
+        lds_barrier();
+        uint32_t cnt = 0;
+        if (t < 256) {
+#pragma unroll
+            for (int ww = 0; ww < kRWaves; ++ww) {
+                const uint32_t c = s_cnt[ww][t];
+                s_cnt[ww][t] = cnt;
+                cnt += c;
+            }
+        }
+        const uint32_t dstart = scan256_excl_lds(cnt, s_wsum);
+        if (t < 256) {
+            s_dstart[t] = dstart;
+            s_gbase[t] = excl + dbase - dstart;
+        }
+        lds_barrier();
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) {
+            const uint32_t d = (key[e] >> shift) & 255u;
+            s_keys[s_dstart[d] + s_cnt[w][d] + rank[e]] = key[e];
+        }
+        lds_barrier();
+#pragma unroll 4
+        for (int i = t; i < kRTile; i += kRThreads) {
+            const uint32_t k = s_keys[i];
+            const int64_t pos = (int64_t)s_gbase[(k >> shift) & 255u] + i;
+            if (pos < n) out[pos] = from_key(k, out_mode);
+        }
+        lds_barrier();  // s_keys / s_gbase are rewritten by the next tile
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) raw[e] = nxt[e];
+    }
+}
+
 // reduce-then-scan, step 1: the tile's digit counts (per-wave LDS atomics,
 // order irrelevant), digit-major
 // (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
@@ -569,7 +695,9 @@ RadixWs radix_layout(void *ws, int64_t n) {
     return r;
 }
 
-// Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan.
+// Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan
+// (one tile per block), 3 = reduce-then-scan with the persistent prefetching
+// scatter.
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
@@ -578,7 +706,7 @@ constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (prof
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 2;
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 3;
     const int ntiles = (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
@@ -602,8 +730,14 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             hipLaunchKernelGGL(radix_scan_kernel, dim3(256), dim3(256), 0, s, r.status, ntiles, r.hist);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst, n,
-                               8 * p, in_mode, out_mode, r.hist, r.status, r.ctr, r.err, ntiles);
+            if (variant == 3) {
+                const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
+                hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src, dst, n,
+                                   8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
+            } else {
+                hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst,
+                                   n, 8 * p, in_mode, out_mode, r.hist, r.status, r.ctr, r.err, ntiles);
+            }
         }
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     }
@@ -728,9 +862,10 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 }
 
 // Tuning entry (tools/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
-// (decoupled look-back), 2 = reduce-then-scan.
+// (decoupled look-back), 2 = reduce-then-scan, 3 = reduce-then-scan with the
+// persistent scatter.
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 2) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 3) return MPX_ERR_ARG;
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }

@@ -250,12 +250,13 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("kind", ["int", "float"])
-@pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7])
+@pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
-    """Both radix schedules (1 onesweep look-back, 2 reduce-then-scan) against
-    the total order, independent of which one AUTO picks at this size."""
+    """Every radix schedule (1 onesweep look-back, 2 reduce-then-scan, 3 the
+    same with the persistent prefetching scatter) against the total order,
+    independent of which one AUTO picks at this size."""
     from cuda_mpi_openmp_amd import _native
 
     L = _native.lib()

@@ -56,7 +56,7 @@ def main():
             ms, out = gpu_ms(ops.sort_, src)
             variants = {}
             if dt != torch.uint8:
-                for v, nm in ((1, "onesweep"), (2, "reduce_scan")):
+                for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (3, "reduce_scan_persistent")):
                     vms, vout = gpu_ms(lambda x, v=v: variant_sort(x, v), src)
                     variants[nm] = {"ms": round(vms, 3), "ok": bool(torch.equal(vout, out))}
             vals, idx = torch.empty_like(src), torch.empty(src.shape, dtype=torch.int64, device=dev)
