@@ -597,7 +597,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
             r = make_uint2(v.x, v.y);
         } else if constexpr (VEC && BUFLD == 0) {
             r = *reinterpret_cast<const uint2 *>(row + cc);
-        } else if constexpr (VEC) {  // w even: the pair is entirely inside, left or right
+        } else if constexpr (VEC) {  // w even: the pair is entirely inside, left or right (BUFLD 1, 3)
             // buffer load: the row base lives in the (scalar) descriptor and the
             // lane's byte offset is loop-invariant — no per-row address VALU
             const __amdgpu_buffer_rsrc_t rrow = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0,
@@ -744,7 +744,8 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         if constexpr (VEC) {
             typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
             const u32x2_t pv = {v0, v1};
-            __builtin_amdgcn_raw_buffer_store_b64(pv, orow, st0 ? ox * 4 : kDrop, 0, 0);
+            // BUFLD 3 (tuning variant): non-temporal output stores (cache policy NT)
+            __builtin_amdgcn_raw_buffer_store_b64(pv, orow, st0 ? ox * 4 : kDrop, 0, BUFLD == 3 ? 2 : 0);
         } else {
             __builtin_amdgcn_raw_buffer_store_b32(v0, orow, st0 ? ox * 4 : kDrop, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(v1, orow, st1 ? ox * 4 + 4 : kDrop, 0, 0);

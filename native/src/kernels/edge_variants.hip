@@ -30,12 +30,12 @@ __global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigne
 // Memory-pattern probe: the wave-strip streaming order of conv_wave_kernel with
 // no arithmetic (copy in -> out). V = 32-bit pixels per lane (2: 8-B loads,
 // 4: 16-B loads), ring of D rows in flight per wave.
-template <int V, int D>
-__global__ __launch_bounds__(256) void strip_copy_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+template <int V, int D, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void strip_copy_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int h, int seg, int nwaves, int strips) {
     typedef uint32_t vt __attribute__((ext_vector_type(V)));
     const int lane = threadIdx.x & 63;
-    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gw >= nwaves) return;
     const int strip = gw % strips, sg = gw / strips;
     const int ys = sg * seg, ye = min(ys + seg, h);
@@ -61,19 +61,51 @@ __global__ __launch_bounds__(256) void strip_copy_kernel(const uint32_t *__restr
     }
 }
 
+// Linear-copy floor for the same bytes (v = 0 in the probe): one 16-B vector
+// per thread like lab1's vsub (its best HBM pattern), plain or non-temporal.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void linear_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
+                                                          int64_t nvec) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+    else out[i] = in[i];
+}
+
 }  // namespace
 MPX_MODULE_ANCHOR(edge_variants)
 
 extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, int h, int v, int d, int seg,
                                     void *stream) {
     using namespace mpx;
-    MPX_CHECK_ARG(in && out && w > 0 && h > 0 && seg > 0 && w % 4 == 0, "bad arguments");
+    MPX_CHECK_ARG(in && out && w > 0 && h > 0 && w % 4 == 0, "bad arguments");
+    hipStream_t s0 = as_stream(stream);
+    if (v == 0) {  // linear copy: d = 0 plain, 1 non-temporal
+        const int64_t nvec = (int64_t)w * h / 4;
+        const dim3 g((unsigned)((nvec + 255) / 256)), b(256);
+        if (d) hipLaunchKernelGGL(linear_copy_kernel<true>, g, b, 0, s0, (const u32x4_t *)in, (u32x4_t *)out, nvec);
+        else hipLaunchKernelGGL(linear_copy_kernel<false>, g, b, 0, s0, (const u32x4_t *)in, (u32x4_t *)out, nvec);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        return MPX_OK;
+    }
+    MPX_CHECK_ARG(seg > 0, "seg must be > 0");
+    // d >= 100: 16 waves per workgroup (d - 100 rows in flight) instead of 4 —
+    // the strips of one row band then start and advance together
+    const int wpb = d >= 100 ? 16 : 4;
+    if (d >= 100) d -= 100;
     const int strips = (w + 64 * v - 1) / (64 * v);
     const int nwaves = strips * ((h + seg - 1) / seg);
-    const dim3 grid((nwaves + 3) / 4), blk(256);
+    const dim3 grid((nwaves + wpb - 1) / wpb), blk(64 * wpb);
     hipStream_t s = as_stream(stream);
-#define MPX_PROBE(VV, DD) \
-    if (v == VV && d == DD) { hipLaunchKernelGGL((strip_copy_kernel<VV, DD>), grid, blk, 0, s, in, out, w, h, seg, nwaves, strips); return MPX_OK; }
+#define MPX_PROBE(VV, DD)                                                                                             \
+    if (v == VV && d == DD) {                                                                                        \
+        if (wpb == 16)                                                                                              \
+            hipLaunchKernelGGL((strip_copy_kernel<VV, DD, 16>), grid, blk, 0, s, in, out, w, h, seg, nwaves, strips); \
+        else                                                                                                         \
+            hipLaunchKernelGGL((strip_copy_kernel<VV, DD>), grid, blk, 0, s, in, out, w, h, seg, nwaves, strips);     \
+        return MPX_OK;                                                                                               \
+    }
     MPX_PROBE(2, 4) MPX_PROBE(2, 8) MPX_PROBE(4, 4) MPX_PROBE(4, 8) MPX_PROBE(4, 2)
 #undef MPX_PROBE
     set_error("unsupported probe v=%d d=%d", v, d);
@@ -122,6 +154,7 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         // p2: 0 buffer loads (production), 1 plain global loads, 2 non-temporal global loads
         if (sep) {
             if (p2 == 1) return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 0>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+            if (p2 == 3) return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 3>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
             if (p2 == 2) return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 2>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
             return launch_wave<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, 0, 4, 1>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
         }

@@ -104,6 +104,9 @@ def main():
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
+    variants["sobel5-sep/stores-nt"] = (
+        (lambda: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, 3, 1, swx, swy, 0))),
+        sref)
     for p2, nm in ((0, "buffer"), (1, "global"), (2, "global-nt")):  # row-load A/B
         variants[f"sobel5-sep/loads-{nm}"] = (
             (lambda p2=p2: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, p2, 1,
@@ -125,6 +128,13 @@ def main():
         variants[f"copy/strip-v{v}-d{d}-seg{seg}"] = (
             (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
                                                                             seg, 0))), img)
+    for v, d, seg in ((2, 104, 8), (2, 104, 24), (4, 104, 8), (4, 104, 24), (4, 104, 64)):  # 16 waves per block
+        variants[f"copy/strip-v{v}-d{d - 100}-seg{seg}-wpb16"] = (
+            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
+                                                                            seg, 0))), img)
+    for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
+        variants[f"copy/linear-{nm}"] = (
+            (lambda d=d: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
