@@ -48,6 +48,7 @@ int main(int argc, char **argv) {
                                      if (n) HIP_CHECK(hipMemcpy(d.get(), orig.get(), buf.size(), hipMemcpyDeviceToDevice));
                                  });
     if (n) HIP_CHECK(hipMemcpy(buf.data(), d.get(), buf.size(), hipMemcpyDeviceToHost));
+    MPX_CHECK(mpx_sort_ws_status(ws.get(), n, dtype));
 #ifndef MPX_SUBMISSION
     std::printf("HIP execution time: <%f ms>\n", ms);
     std::fflush(stdout);

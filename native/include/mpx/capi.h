@@ -203,6 +203,9 @@ int mpx_jacobi_f32(const float *u, float *un, int cols, int pitch, int r0, int r
  * mpx_sort allocates and frees its own scratch and synchronises the stream. */
 int64_t mpx_sort_workspace_bytes(int64_t n, int dtype);
 int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, void *stream);
+/* After the sort's stream drained: non-zero if a bounded look-back wait of the
+ * sort that last used `workspace` gave up (hardware-fault detector). */
+int mpx_sort_ws_status(const void *workspace, int64_t n, int dtype);
 int mpx_sort(void *data, int64_t n, int dtype, void *stream);
 
 /* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */

@@ -836,13 +836,30 @@ int sort_impl(void *data, int64_t n, int dtype, void *ws, int64_t ws_bytes, void
 
 // Convenience form without a caller workspace (tools, one-off sorts): the
 // scratch is allocated for this call and freed after the stream drains.
+// Did a look-back wait of the last sort in `ws` give up (kSpinLimit)? Only
+// the onesweep schedule (n <= kOnesweepMaxN) waits; its predecessors are
+// always resident (tile ids in launch order), so this is a hardware-fault
+// detector. Synchronous: call after the sort's stream has drained.
+int sort_ws_status(const void *ws, int64_t n, int dtype) {
+    if (dtype == MPX_SORT_U8 || !ws || !use_radix(n)) return MPX_OK;
+    const RadixWs r = radix_layout(const_cast<void *>(ws), n);
+    uint32_t err = 0;
+    MPX_RETURN_IF_HIP_ERROR(hipMemcpy(&err, r.err, sizeof(err), hipMemcpyDeviceToHost));
+    if (err) {
+        set_error("sort: a decoupled look-back wait gave up (a predecessor tile never published)");
+        return MPX_ERR_HIP;
+    }
+    return MPX_OK;
+}
+
 int sort_alloc(void *data, int64_t n, int dtype, void *stream) {
     const int64_t bytes = sort_workspace_bytes(std::max<int64_t>(n, 0), dtype);
     void *ws = nullptr;
     if (bytes > 0) MPX_RETURN_IF_HIP_ERROR(hipMalloc(&ws, (size_t)bytes));
-    const int rc = sort_impl(data, n, dtype, ws, bytes, stream);
+    int rc = sort_impl(data, n, dtype, ws, bytes, stream);
     if (ws) {
         const hipError_t e = hipStreamSynchronize(as_stream(stream));
+        if (rc == MPX_OK && e == hipSuccess) rc = sort_ws_status(ws, n, dtype);
         (void)hipFree(ws);
         MPX_RETURN_IF_HIP_ERROR(e);
     }
@@ -856,6 +873,10 @@ MPX_MODULE_ANCHOR(sort)
 extern "C" int mpx_sort(void *data, int64_t n, int dtype, void *stream) { return mpx::sort_alloc(data, n, dtype, stream); }
 
 extern "C" int64_t mpx_sort_workspace_bytes(int64_t n, int dtype) { return mpx::sort_workspace_bytes(n, dtype); }
+
+extern "C" int mpx_sort_ws_status(const void *workspace, int64_t n, int dtype) {
+    return mpx::sort_ws_status(workspace, n, dtype);
+}
 
 extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, void *stream) {
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream);

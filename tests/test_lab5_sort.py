@@ -267,3 +267,4 @@ def test_gpu_radix_variants(gpu, variant, kind, n):
     ws = torch.empty(nb, dtype=torch.uint8, device=gpu)
     _native.check(L.mpx_sort_variant(d.data_ptr(), n, dt, ws.data_ptr(), nb, variant, _native.stream_of(d)))
     assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
+    _native.check(L.mpx_sort_ws_status(ws.data_ptr(), n, dt))  # no look-back wait gave up
