@@ -19,3 +19,15 @@ def test_scale_driver_cpu_dry_run(tmp_path):
     assert two["efficiency"] is not None and two["world_size_seen"]["torch_distributed"] == 2
     assert runs[("conv/peer", 2)]["status"] == "skipped" and runs[("conv/peer", 2)]["reason"]
     assert (tmp_path / "scaling.csv").exists() and (tmp_path / "scaling.png").exists()
+
+
+def test_scale_driver_cpu_lab1_lab3(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale.py"), "--device", "cpu", "--gpus", "1,2",
+                        "--only", "lab", "--out", str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    runs = {(x["name"], x["n"]): x for x in json.load(open(tmp_path / "scaling.json"))["runs"]}
+    for name in ("lab1/vsub", "lab3/classify"):
+        for n in (1, 2):
+            x = runs[(name, n)]
+            assert x["status"] == "ok" and x["n_reported"] == n and x["verified"] is True, x
+        assert runs[(name, 2)]["efficiency"] is not None

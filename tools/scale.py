@@ -10,7 +10,9 @@ same commands a user would type):
     peer halos and with RCCL halos — every rank owns a 4096^2 slab;
   * Jacobi 16384^2 fp64 (strong scaling): ``tools/bench_jacobi.py --gpus N``
     with device-signalled peer halos and with RCCL halos;
-  * the native one-process runtime: ``bin/mpx_mgpu conv|jacobi --gpus N``.
+  * the native one-process runtime: ``bin/mpx_mgpu conv|jacobi --gpus N``;
+  * lab1 vector subtraction and lab3 classification (weak scaling, 2^26 fp32
+    elements / one 8192^2 slab per rank): ``tools/bench_workloads.py``.
 
 and writes ``<out>/scaling.json`` (one record per run: N, value, ms/step,
 efficiency vs N = 1, transport, world size the job saw), ``scaling.csv`` and
@@ -101,6 +103,12 @@ def plan(n: int, a, ndev: int) -> List[dict]:
         jobs.append({"name": f"jacobi/{halo}", "kind": "strong",
                      "skip": skip,
                      "cmd": [py, "tools/bench_jacobi.py", "--gpus", str(n), "--halo", halo, *dev, *jac_sz]})
+    for wl in ("vsub", "classify"):
+        sz = (["--elems", "65536"] if wl == "vsub" else ["--size", "96"]) if cpu else []
+        st = ["--steps", "3", "--warmup", "1"] if cpu else (
+            ["--steps", "20", "--warmup", "3"] if a.quick else ["--steps", "100", "--warmup", "10"])
+        jobs.append({"name": f"lab{1 if wl == 'vsub' else 3}/{wl}", "kind": "weak", "skip": lacks,
+                     "cmd": [py, "tools/bench_workloads.py", "--workload", wl, "--gpus", str(n), *dev, *sz, *st]})
     mg = os.path.join(ROOT, "bin", "mpx_mgpu")
     if cpu:
         jobs.append({"name": "mgpu/conv", "kind": "weak", "skip": "native runtime needs GPUs", "cmd": []})
@@ -172,13 +180,12 @@ def plot(rows: List[dict], path: str, title: str) -> Optional[str]:
     ns = sorted({r["n"] for r in rows})
     for name in sorted({r["name"] for r in rows if r["kind"] == "weak"}):
         pts = [(r["n"], r["value"]) for r in rows if r["name"] == name and r["status"] == "ok" and r.get("value")]
-        if pts:
-            ax1.plot(*zip(*pts), marker="o", label=name)
-            b = [v for n, v in pts if n == 1]
-            if b:
-                ax1.plot(ns, [b[0] * n for n in ns], ls=":", color="gray")
+        b = [v for n, v in pts if n == 1]
+        if pts and b:  # workloads have different units: plot throughput relative to one rank
+            ax1.plot([n for n, _ in pts], [v / b[0] for _, v in pts], marker="o", label=name)
+    ax1.plot(ns, ns, ls=":", color="gray", label="ideal")
     ax1.set_xlabel("GPUs")
-    ax1.set_ylabel("Gpixel/s (whole job)")
+    ax1.set_ylabel("whole-job throughput / 1-rank throughput")
     ax1.set_title("weak scaling (dotted: ideal)")
     ax1.set_xticks(ns)
     ax1.legend(fontsize=8)
