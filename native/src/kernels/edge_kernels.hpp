@@ -913,6 +913,196 @@ __global__ __launch_bounds__(256) void conv_wave4_kernel(const uint32_t *__restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// Band kernel for SEPARABLE filters, 16-B lanes, no overlapping strips.
+//
+// conv_wave4_kernel spends lanes 0 and 63 on halo columns (248 of 256 loaded
+// columns produce), so its strips start at 992-B offsets and every row piece
+// straddles one more 128-B line than it needs. Here a wave owns exactly 256
+// columns (x0 = 256 * strip): every lane loads and stores one aligned 16-B
+// quad per row (the linear copy's request shape), and the four columns a strip
+// needs beyond its edges come from one extra 8-B "apron" load per row that
+// only lanes 0 (x0-2, x0-1) and 63 (x0+256, x0+257) issue — the other lanes'
+// offsets are out of range and the hardware drops them. Waves run strip-minor
+// with alternating segment directions (odd segments walk up, see
+// conv_wave_kernel), which is what the row-band copy probe showed to be the
+// HBM-friendly order (tools/kbench.py copy/band-*: 27.2 us rotated vs 29.1 us
+// for the wave-strip copy). Clamp-to-edge needs no special code inside the
+// image: quads right of the image replicate its last pixel (fix_quad), and the
+// apron falls back to the lane's own edge pixel at x = 0 and x = w.
+// Requires w % 4 == 0, pitch % 4 == 0 and 16-B aligned rows.
+// ---------------------------------------------------------------------------
+// One wave's segment walk in one direction (UP: bottom row first), prologue
+// included, so nothing but scalars is live across the direction branch.
+template <int K, int A, int MODE, bool FAST, class F, bool UP>
+__device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                     int w, int pitch, int ys, int ye, int y_lo, int y_hi, int x0,
+                                                     const Taps &taps, RowSrc rs) {
+    constexpr int R = K - 1 - A;
+    constexpr int NV = 4 + A + R;
+    constexpr bool TWO = (MODE == MPX_CONV_MAG2);
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    const int lane = threadIdx.x & 63;
+    constexpr bool up = UP;
+    const int cin = x0 + 4 * lane;
+    const bool st = cin < w;
+    const int cc = min(cin, w - 4);
+    const bool q_right = cin >= w;
+    // apron: lane 0 reads the two columns left of the strip, lane 63 the two
+    // right of it; at the image edges the lane's own edge pixel stands in
+    const bool ap_left = lane == 0, ap_right = lane == 63;
+    const bool ap_have = (ap_left && x0 > 0) || (ap_right && x0 + 256 < w);
+    constexpr int kDrop = 0x7ffffff0;
+    const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : kDrop;
+    const int iy0 = ys - A;
+    const int iy_last = ye - 1 + R;
+    auto row_ptr = [&](int i) {
+        const int gy = mpx_clampi(up ? iy_last - i : iy0 + i, y_lo, y_hi);
+        const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
+        return src + (int64_t)gy * pitch;
+    };
+    auto load_row = [&](int i, u32x2_t &ap) -> u32x4_t {
+        const uint32_t *row = row_ptr(i);
+        const __amdgpu_buffer_rsrc_t rr =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, w * 4, 0x00020000);
+        const u32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 0);
+        ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        return q;
+    };
+    auto fix_quad = [&](u32x4_t q) -> u32x4_t {
+        return q_right ? u32x4_t{q.w, q.w, q.w, q.w} : q;
+    };
+
+    constexpr int D = K;  // prefetch ring: K rows ahead
+    u32x4_t pre[D];
+    u32x2_t apr[D];
+    f2_t hxr[K][2], hyr[K][2];
+    uint32_t alp[K];
+
+    auto consume = [&](int u, u32x4_t px, u32x2_t ap) {
+        const f2_t l01 = luma2(px.x, px.y), l23 = luma2(px.z, px.w);
+        alp[u] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px.w, px.z, 0x07030000u),
+                                       __builtin_amdgcn_perm(px.y, px.x, 0x07030000u), 0x07060302u);
+        const f2_t la = luma2(ap.x, ap.y);
+        float wv[NV];
+        wv[A + 0] = l01.x;
+        wv[A + 1] = l01.y;
+        wv[A + 2] = l23.x;
+        wv[A + 3] = l23.y;
+        if constexpr (A >= 1) {
+            const float d = from_prev(l23.y);
+            wv[A - 1] = ap_left ? (ap_have ? la.y : l01.x) : d;
+        }
+        if constexpr (A >= 2) {
+            const float d = from_prev(l23.x);
+            wv[A - 2] = ap_left ? (ap_have ? la.x : l01.x) : d;
+        }
+        if constexpr (R >= 1) {
+            const float d = from_next(l01.x);
+            wv[A + 4] = ap_right ? (ap_have ? la.x : l23.y) : d;
+        }
+        if constexpr (R >= 2) {
+            const float d = from_next(l01.y);
+            wv[A + 5] = ap_right ? (ap_have ? la.y : l23.y) : d;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            auto pair = [&](int dx) { return f2_t{wv[2 * e + dx], wv[2 * e + dx + 1]}; };
+            hxr[u][e] = sep_chain<F, K, 0>(taps, pair);
+            if constexpr (TWO) hyr[u][e] = sep_chain<F, K, 2>(taps, pair);
+        }
+    };
+
+#pragma unroll
+    for (int q = 0; q < D; ++q) pre[q] = load_row(q, apr[q]);
+#pragma unroll
+    for (int u = 0; u < K - 1; ++u) {
+        const u32x4_t px = fix_quad(pre[u]);
+        const u32x2_t ap = apr[u];
+        pre[u] = load_row(u + D, apr[u]);
+        consume(u, px, ap);
+    }
+    auto row_step = [&](int g, int v) {
+        const int u = (K - 1 + v) % K;
+        const int q = (K - 1 + v) % D;
+        const int i = K - 1 + g * D + v;
+        const u32x4_t px = fix_quad(pre[q]);
+        const u32x2_t ap = apr[q];
+        pre[q] = load_row(i + D, apr[q]);
+        consume(u, px, ap);
+        const int y = UP ? ye - 1 - (g * D + v) : ys + g * D + v;
+        auto slot = [&](int dy) { return UP ? (u + K - dy) % K : (u + 1 + dy) % K; };
+        uint32_t gray[4];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            f2_t gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[slot(dy)][e]; });
+            const float sx = sep_scale<F, K, false>(taps);
+            gx = gx * f2_t{sx, sx};
+            if constexpr (TWO) {
+                f2_t gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[slot(dy)][e]; });
+                const float sy = sep_scale<F, K, true>(taps);
+                gy = gy * f2_t{sy, sy};
+                const f2_t sq = gx * gx + gy * gy;
+                if constexpr (FAST) {
+                    mag2_to_gray(sq.x, sq.y, gray[2 * e], gray[2 * e + 1]);
+                } else {
+                    gray[2 * e] = mag_to_gray<false>(sq.x);
+                    gray[2 * e + 1] = mag_to_gray<false>(sq.y);
+                }
+            } else {
+                gray[2 * e] = finish_gray<MODE, FAST>(gx.x, 0.0f);
+                gray[2 * e + 1] = finish_gray<MODE, FAST>(gx.y, 0.0f);
+            }
+        }
+        const uint32_t a = alp[slot(A)];
+        u32x4_t o;
+        o.x = __builtin_amdgcn_perm(a, gray[0], 0x04000000u);
+        o.y = __builtin_amdgcn_perm(a, gray[1], 0x05000000u);
+        o.z = __builtin_amdgcn_perm(a, gray[2], 0x06000000u);
+        o.w = __builtin_amdgcn_perm(a, gray[3], 0x07000000u);
+        const bool row_ok = UP ? y >= ys : y < ye;
+        const int yc = row_ok ? y : ys;
+        const __amdgpu_buffer_rsrc_t orow =
+            __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(o, orow, st ? cin * 4 : kDrop, 0, 0);
+    };
+    const int nrows = ye - ys;
+    const int nfull = nrows / D;
+    const int rem = nrows - nfull * D;
+    for (int g = 0; g < nfull; ++g) {
+#pragma unroll
+        for (int v = 0; v < D; ++v) row_step(g, v);
+    }
+    if (rem > 0) {
+#pragma unroll
+        for (int v = 0; v < D; ++v) {
+            if (v >= rem) break;
+            row_step(nfull, v);
+        }
+    }
+}
+
+template <int K, int A, int MODE, bool FAST, class F>
+__global__ __launch_bounds__(256) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                         int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                                                         int seg, int nwaves, int strips, int alt, Taps taps,
+                                                         RowSrc rs) {
+    static_assert(F::kSep, "conv_band4_kernel evaluates separable filters");
+    static_assert(A <= 2 && K - 1 - A <= 2, "apron covers two columns on each side");
+    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (gw >= nwaves) return;  // wave-uniform
+    const int strip = gw % strips;
+    const int sg = gw / strips;
+    const int ys = oy0 + sg * seg;
+    const int ye = min(ys + seg, oy1);
+    if (alt && (sg & 1))  // wave-uniform: odd segments walk up
+        band4_walk<K, A, MODE, FAST, F, true>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+    else
+        band4_walk<K, A, MODE, FAST, F, false>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+}
+
 // Gray value packing helper for the non-stream kernels.
 template <int MODE, bool FAST>
 __device__ __forceinline__ uint32_t gray_px(float gx, float gy, uint32_t a) {

@@ -172,6 +172,49 @@ int launch_wave4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     return MPX_OK;
 }
 
+// Band kernel (conv_band4_kernel): 256-column strips, aprons, strip-minor with
+// alternating segment directions. seg <= 0: one resident round of per_simd
+// waves per SIMD (104 VGPRs: 4 resident), at least 8 rows per segment.
+// MI355X sobel5 4096^2, 6 rotated pairs (tools/kbench.py): auto at 4 waves
+// (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
+// 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
+inline constexpr int kBand4PerSimd = 4;
+template <int K, int A, int MODE, bool FAST, class F>
+int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                 const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kBand4PerSimd,
+                 int alt = 1) {
+    MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
+    if (!rs.up) rs.up = in;
+    if (!rs.dn) rs.dn = in;
+    const int strips = (w + 255) / 256;
+    if (seg <= 0) {
+        const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
+        const int64_t work = (int64_t)(oy1 - oy0) * strips;
+        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
+    }
+    const int segs = (oy1 - oy0 + seg - 1) / seg;
+    const int64_t nwaves = (int64_t)strips * segs;
+    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
+    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0,
+                       s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
+    return MPX_OK;
+}
+
+// The band kernel serves the separable 5x5 launches whose rows (and neighbour
+// rows) are 16-B aligned; MPX_CONV_BAND=0 falls back to the 8-B-lane wave
+// kernel (same-box A/B), read once per process.
+inline bool band_enabled() {
+    static const bool v = [] {
+        const char *e = std::getenv("MPX_CONV_BAND");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs) {
+    return band_enabled() && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
+           (!rs.up || aligned16(rs.up)) && (!rs.dn || aligned16(rs.dn));
+}
+
 template <class F, int K>
 inline bool same_sep_taps(const Taps &t, bool two) {
     auto eq = [](float a, float b) { return __builtin_bit_cast(uint32_t, a) == __builtin_bit_cast(uint32_t, b); };
@@ -195,6 +238,8 @@ int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int
     constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
     constexpr int order = MODE == MPX_CONV_MAG2 ? kWaveOrderAlt : kWaveOrder;
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
+        if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true) && band_ok(in, out, w, pitch, rs))
+            return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
             return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }

@@ -73,6 +73,53 @@ __global__ __launch_bounds__(256) void linear_copy_kernel(const u32x4_t *__restr
     else out[i] = in[i];
 }
 
+// Row-band probe (v = 8): a 16-wave workgroup owns a band of R rows across
+// 4096 columns, one 16-B vector per thread per row (the linear copy's request
+// shape), walking the band's R + 4 rows (5-row vertical window, 2 halo rows
+// each side) with an 8-row register ring. out[y] = in[y-2] ^ in[y] ^ in[y+2]
+// keeps every halo load live. F bit 0: per-row LDS exchange with the
+// neighbouring thread + barrier (the horizontal pass's cost); bit 1: odd
+// bands walk upwards; bit 2: no XCD remap; bit 3: non-temporal stores;
+// bit 4: 512-thread workgroups over 2048 columns.
+template <int F>
+__global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
+                                                         int w4, int h, int R, int nchunks) {
+    __shared__ uint32_t xch[2][1025];
+    const int b = (F & 4) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+    const int band = b / nchunks, chunk = b - band * nchunks;
+    const int t = threadIdx.x;
+    const int c = chunk * (int)blockDim.x + t;
+    const int ys = band * R, ye = min(ys + R, h);
+    const bool up = (F & 2) && (band & 1);
+    auto row_of = [&](int j) {  // j-th row of the walk (j = 0 .. R+3), clamped to the image
+        const int y = up ? ye + 1 - j : ys - 2 + j;
+        return min(max(y, 0), h - 1);
+    };
+    auto ld = [&](int j) { return in[(int64_t)row_of(min(j, R + 3)) * w4 + c]; };
+    u32x4_t r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = ld(j);
+    for (int g = 0; g < R; g += 8) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            u32x4_t o = r[v] ^ r[(v + 2) & 7] ^ r[(v + 4) & 7];
+            if constexpr (F & 1) {
+                xch[v & 1][t] = o.x;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                o.y ^= xch[v & 1][t + 1];
+            }
+            const int j = g + v + 2;  // output walk index -> row
+            if (g + v < ye - ys) {
+                if constexpr (F & 8) __builtin_nontemporal_store(o, out + (int64_t)row_of(j) * w4 + c);
+                else out[(int64_t)row_of(j) * w4 + c] = o;
+            }
+            r[v] = ld(g + v + 8);
+        }
+    }
+}
+
 }  // namespace
 MPX_MODULE_ANCHOR(edge_variants)
 
@@ -90,6 +137,25 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
         return MPX_OK;
     }
     MPX_CHECK_ARG(seg > 0, "seg must be > 0");
+    if (v == 8) {  // row bands: seg = rows per band (multiple of 8), d = flag bits
+        MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 32, "band probe: w % 4096 == 0, seg % 4 == 0");
+        const int tpb = (d & 16) ? 512 : 1024;
+        const int nchunks = w / (4 * tpb), nb = (h + seg - 1) / seg;
+        const dim3 g((unsigned)(nb * nchunks)), b(tpb);
+        const u32x4_t *vi = (const u32x4_t *)in;
+        u32x4_t *vo = (u32x4_t *)out;
+        hipStream_t sb = as_stream(stream);
+        switch (d) {
+#define MPX_BAND(F) \
+    case F: hipLaunchKernelGGL(band_copy_kernel<F>, g, b, 0, sb, vi, vo, w / 4, h, seg, nchunks); break;
+            MPX_BAND(0) MPX_BAND(1) MPX_BAND(2) MPX_BAND(3) MPX_BAND(4) MPX_BAND(10) MPX_BAND(11) MPX_BAND(18)
+            MPX_BAND(19) MPX_BAND(26)
+            default: set_error("unsupported band flags %d", d); return MPX_ERR_ARG;
+#undef MPX_BAND
+        }
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        return MPX_OK;
+    }
     // d >= 100: 16 waves per workgroup (d - 100 rows in flight) instead of 4 —
     // the strips of one row band then start and advance together
     const int wpb = d >= 100 ? 16 : 4;
@@ -161,6 +227,15 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         if (p2 == 1) return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 0>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
         if (p2 == 2) return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 2>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
         return launch_wave<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0, 4, 1>(in, out, w, w, 0, h, 0, h - 1, st, true, s, seg);
+    }
+    if (kind == 8) {
+        // band kernel (conv_band4_kernel): p1 = segment rows (0 = auto), p2 % 100 =
+        // waves per SIMD the auto segments target (0 = default), p2 >= 100: no alternation
+        MPX_CHECK_ARG(k == 5 && p1 >= 0 && w % 4 == 0 && aligned16(in) && aligned16(out), "band variant: k = 5, w % 4 == 0");
+        const Taps st = make_taps(k, wx, wy, true, true);
+        return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(
+            in, out, w, w, 0, h, 0, h - 1, st, s, p1, edge::RowSrc{}, p2 % 100 > 0 ? p2 % 100 : edgel::kBand4PerSimd,
+            p2 >= 100 ? 0 : 1);
     }
     if (kind == 5) {
         // 16-B-lane separable sobel5 (conv_wave4_kernel): p1 = segment rows (0 = auto),

@@ -101,6 +101,10 @@ def main():
         variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 5, seg,
                                                                        per, 1, swx, swy, 0))), sref)
+    for seg, per in ((0, 0), (0, 4), (0, 6), (12, 0), (16, 0), (20, 0), (24, 0), (16, 100), (24, 100)):
+        variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
+            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
+                                                                       per, 1, swx, swy, 0))), sref)
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
@@ -135,6 +139,11 @@ def main():
     for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
         variants[f"copy/linear-{nm}"] = (
             (lambda d=d: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
+    for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26)] + [(16, 0), (16, 4)]:
+        if True:  # row bands, 16-B vector per thread (ref None: XOR of rows, no reference)
+            variants[f"copy/band-seg{seg}-f{fl}"] = (
+                (lambda fl=fl, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
+                                                                              fl, seg, 0))), None)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
@@ -152,7 +161,7 @@ def main():
         out.zero_()
         fn()
         torch.cuda.synchronize()
-        ok = torch.equal(out, ref)
+        ok = ref is None or torch.equal(out, ref)
         if not ok:
             print(json.dumps({"variant": name, "ERROR": "mismatch vs production"}), flush=True)
     times = {k: [] for k in variants}
