@@ -934,7 +934,7 @@ __global__ __launch_bounds__(256) void conv_wave4_kernel(const uint32_t *__restr
 // ---------------------------------------------------------------------------
 // One wave's segment walk in one direction (UP: bottom row first), prologue
 // included, so nothing but scalars is live across the direction branch.
-template <int K, int A, int MODE, bool FAST, class F, bool UP>
+template <int K, int A, int MODE, bool FAST, class F, bool UP, int OPT>
 __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                      int w, int pitch, int ys, int ye, int y_lo, int y_hi, int x0,
                                                      const Taps &taps, RowSrc rs) {
@@ -1066,7 +1066,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const int yc = row_ok ? y : ys;
         const __amdgpu_buffer_rsrc_t orow =
             __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(o, orow, st ? cin * 4 : kDrop, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(o, orow, st ? cin * 4 : kDrop, 0, (OPT & 2) ? 2 : 0);
     };
     const int nrows = ye - ys;
     const int nfull = nrows / D;
@@ -1084,8 +1084,10 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     }
 }
 
-template <int K, int A, int MODE, bool FAST, class F>
-__global__ __launch_bounds__(256) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+// OPT (tuning variants): bit 0 caps registers for 5 waves per SIMD, bit 1
+// non-temporal output stores.
+template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                          int seg, int nwaves, int strips, int alt, Taps taps,
                                                          RowSrc rs) {
@@ -1098,9 +1100,9 @@ __global__ __launch_bounds__(256) void conv_band4_kernel(const uint32_t *__restr
     const int ys = oy0 + sg * seg;
     const int ye = min(ys + seg, oy1);
     if (alt && (sg & 1))  // wave-uniform: odd segments walk up
-        band4_walk<K, A, MODE, FAST, F, true>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+        band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
     else
-        band4_walk<K, A, MODE, FAST, F, false>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+        band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
 }
 
 // Gray value packing helper for the non-stream kernels.

@@ -179,7 +179,7 @@ int launch_wave4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
 // 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
 inline constexpr int kBand4PerSimd = 4;
-template <int K, int A, int MODE, bool FAST, class F>
+template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
 int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                  const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kBand4PerSimd,
                  int alt = 1) {
@@ -195,23 +195,25 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     const int segs = (oy1 - oy0 + seg - 1) / seg;
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
-    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0,
+    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0,
                        s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
     return MPX_OK;
 }
 
 // The band kernel serves the separable 5x5 launches whose rows (and neighbour
-// rows) are 16-B aligned; MPX_CONV_BAND=0 falls back to the 8-B-lane wave
-// kernel (same-box A/B), read once per process.
-inline bool band_enabled() {
-    static const bool v = [] {
+// rows) are 16-B aligned, with non-temporal output stores (sobel5 4096^2, 6
+// rotated pairs: 28.9 us vs 29.4 plain stores vs 30.3 for the 8-B-lane wave
+// kernel, tools/kbench.py). MPX_CONV_BAND=0: wave kernel, 1: band kernel with
+// plain stores (same-box A/B); read once per process.
+inline int band_mode() {
+    static const int v = [] {
         const char *e = std::getenv("MPX_CONV_BAND");
-        return !(e && e[0] == '0');
+        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
     }();
     return v;
 }
 inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs) {
-    return band_enabled() && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
+    return band_mode() != 0 && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
            (!rs.up || aligned16(rs.up)) && (!rs.dn || aligned16(rs.dn));
 }
 
@@ -238,8 +240,11 @@ int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int
     constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
     constexpr int order = MODE == MPX_CONV_MAG2 ? kWaveOrderAlt : kWaveOrder;
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
-        if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true) && band_ok(in, out, w, pitch, rs))
-            return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+        if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true) && band_ok(in, out, w, pitch, rs)) {
+            if (band_mode() == 1)
+                return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+            return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+        }
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
             return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }
