@@ -1085,15 +1085,17 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 }
 
 // OPT (tuning variants): bit 0 caps registers for 5 waves per SIMD, bit 1
-// non-temporal output stores.
+// non-temporal output stores, bit 2 16-wave workgroups (a band row's 16 strips
+// of a 4096-wide image on one CU).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+__global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                          int seg, int nwaves, int strips, int alt, Taps taps,
                                                          RowSrc rs) {
     static_assert(F::kSep, "conv_band4_kernel evaluates separable filters");
     static_assert(A <= 2 && K - 1 - A <= 2, "apron covers two columns on each side");
-    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int WPB = (OPT & 4) ? 16 : 4;
+    const int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gw >= nwaves) return;  // wave-uniform
     const int strip = gw % strips;
     const int sg = gw / strips;

@@ -195,7 +195,9 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     const int segs = (oy1 - oy0 + seg - 1) / seg;
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
-    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0,
+    constexpr int wpb = (OPT & 4) ? 16 : 4;
+    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + wpb - 1) / wpb)),
+                       dim3(64 * wpb), 0,
                        s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
     return MPX_OK;
 }

@@ -101,8 +101,7 @@ def main():
         variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 5, seg,
                                                                        per, 1, swx, swy, 0))), sref)
-    for seg, per in ((0, 0), (0, 5), (16, 0), (24, 0), (16, 100), (0, 1005), (16, 1000), (13, 1000), (0, 2000),
-                     (8, 2000), (0, 3005), (32, 0), (32, 1000)):
+    for seg, per in ((0, 0), (16, 0), (0, 2000), (8, 2000), (24, 2000), (0, 6000), (8, 6000), (24, 6000)):
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
                                                                        per, 1, swx, swy, 0))), sref)
