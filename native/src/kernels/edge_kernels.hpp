@@ -914,7 +914,8 @@ __global__ __launch_bounds__(256) void conv_wave4_kernel(const uint32_t *__restr
 }
 
 // ---------------------------------------------------------------------------
-// Band kernel for SEPARABLE filters, 16-B lanes, no overlapping strips.
+// Band kernel, 16-B lanes, no overlapping strips (separable and dense windows
+// up to 5x5 with at most two columns of reach on each side).
 //
 // conv_wave4_kernel spends lanes 0 and 63 on halo columns (248 of 256 loaded
 // columns produce), so its strips start at 992-B offsets and every row piece
@@ -941,6 +942,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     constexpr int R = K - 1 - A;
     constexpr int NV = 4 + A + R;
     constexpr bool TWO = (MODE == MPX_CONV_MAG2);
+    constexpr bool SEP = F::kSep;
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
     const int lane = threadIdx.x & 63;
@@ -975,10 +977,13 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         return q_right ? u32x4_t{q.w, q.w, q.w, q.w} : q;
     };
 
-    constexpr int D = K;  // prefetch ring: K rows ahead
+    // prefetch ring of D >= 4 rows, a multiple of K (compile-time slots when
+    // the row loop is unrolled D times)
+    constexpr int D = K * ((4 + K - 1) / K);
     u32x4_t pre[D];
     u32x2_t apr[D];
-    f2_t hxr[K][2], hyr[K][2];
+    f2_t hxr[SEP ? K : 1][2], hyr[SEP ? K : 1][2];  // separable: per-row horizontal sums
+    float win[SEP ? 1 : K][NV];                      // dense: per-row luminance windows
     uint32_t alp[K];
 
     auto consume = [&](int u, u32x4_t px, u32x2_t ap) {
@@ -1007,11 +1012,16 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             const float d = from_next(l01.y);
             wv[A + 5] = ap_right ? (ap_have ? la.y : l23.y) : d;
         }
+        if constexpr (SEP) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            auto pair = [&](int dx) { return f2_t{wv[2 * e + dx], wv[2 * e + dx + 1]}; };
-            hxr[u][e] = sep_chain<F, K, 0>(taps, pair);
-            if constexpr (TWO) hyr[u][e] = sep_chain<F, K, 2>(taps, pair);
+            for (int e = 0; e < 2; ++e) {
+                auto pair = [&](int dx) { return f2_t{wv[2 * e + dx], wv[2 * e + dx + 1]}; };
+                hxr[u][e] = sep_chain<F, K, 0>(taps, pair);
+                if constexpr (TWO) hyr[u][e] = sep_chain<F, K, 2>(taps, pair);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) win[u][j] = wv[j];
         }
     };
 
@@ -1037,13 +1047,31 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         uint32_t gray[4];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            f2_t gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[slot(dy)][e]; });
-            const float sx = sep_scale<F, K, false>(taps);
-            gx = gx * f2_t{sx, sx};
+            f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
+            if constexpr (SEP) {
+                gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[slot(dy)][e]; });
+                const float sx = sep_scale<F, K, false>(taps);
+                gx = gx * f2_t{sx, sx};
+                if constexpr (TWO) {
+                    gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[slot(dy)][e]; });
+                    const float sy = sep_scale<F, K, true>(taps);
+                    gy = gy * f2_t{sy, sy};
+                }
+            } else {
+                // (dy, dx) order, one fma per tap and output (conv_wave_kernel)
+                bool sx = false, sy = false;
+#pragma unroll
+                for (int dy = 0; dy < K; ++dy) {
+                    const int r = slot(dy);
+#pragma unroll
+                    for (int dx = 0; dx < K; ++dx) {
+                        const f2_t pv = {win[r][2 * e + dx], win[r][2 * e + dx + 1]};
+                        tap_step<F::kConst>(gx, sx, tap_x<F>(taps, dy * K + dx), pv);
+                        if constexpr (TWO) tap_step<F::kConst>(gy, sy, tap_y<F>(taps, dy * K + dx), pv);
+                    }
+                }
+            }
             if constexpr (TWO) {
-                f2_t gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[slot(dy)][e]; });
-                const float sy = sep_scale<F, K, true>(taps);
-                gy = gy * f2_t{sy, sy};
                 const f2_t sq = gx * gx + gy * gy;
                 if constexpr (FAST) {
                     mag2_to_gray(sq.x, sq.y, gray[2 * e], gray[2 * e + 1]);
@@ -1092,7 +1120,6 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                          int seg, int nwaves, int strips, int alt, Taps taps,
                                                          RowSrc rs) {
-    static_assert(F::kSep, "conv_band4_kernel evaluates separable filters");
     static_assert(A <= 2 && K - 1 - A <= 2, "apron covers two columns on each side");
     constexpr int WPB = (OPT & 4) ? 16 : 4;
     const int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -111,6 +111,66 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     return MPX_OK;
 }
 
+// Band kernel (conv_band4_kernel): 256-column strips, aprons, strip-minor with
+// alternating segment directions. seg <= 0: one resident round of per_simd
+// waves per SIMD (104 VGPRs: 4 resident), at least 8 rows per segment.
+// MI355X sobel5 4096^2, 6 rotated pairs (tools/kbench.py): auto at 4 waves
+// (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
+// 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
+inline constexpr int kBand4PerSimd = 4;
+template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
+int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                 const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kBand4PerSimd,
+                 int alt = 1) {
+    MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
+    if (!rs.up) rs.up = in;
+    if (!rs.dn) rs.dn = in;
+    const int strips = (w + 255) / 256;
+    if (seg <= 0) {
+        const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
+        const int64_t work = (int64_t)(oy1 - oy0) * strips;
+        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
+    }
+    const int segs = (oy1 - oy0 + seg - 1) / seg;
+    const int64_t nwaves = (int64_t)strips * segs;
+    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
+    constexpr int wpb = (OPT & 4) ? 16 : 4;
+    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + wpb - 1) / wpb)),
+                       dim3(64 * wpb), 0,
+                       s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
+    return MPX_OK;
+}
+
+// The band kernel serves every launch whose window reaches at most two columns
+// on each side (K <= 5 except 4x4-style anchors) and whose rows (and neighbour
+// rows) are 16-B aligned, with non-temporal output stores. MI355X 4096^2, 6
+// rotated pairs (tools/kbench.py, µs): sobel5 separable 28.9 (30.3 with the
+// 8-B-lane wave kernel; 29.4 with plain stores), sobel5_dense 32.7 (41.4),
+// Roberts 27.8 (30.4). MPX_CONV_BAND=0: wave kernel, 1: band kernel with plain
+// stores (same-box A/B); read once per process.
+inline int band_mode() {
+    static const int v = [] {
+        const char *e = std::getenv("MPX_CONV_BAND");
+        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
+    }();
+    return v;
+}
+inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs) {
+    return band_mode() != 0 && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
+           (!rs.up || aligned16(rs.up)) && (!rs.dn || aligned16(rs.dn));
+}
+
+template <int K, int A>
+inline constexpr bool kBandFits = A <= 2 && K - 1 - A <= 2;
+
+template <int K, int A, int MODE, class F>
+int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
+    if (band_mode() == 1)
+        return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+    return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+}
+
 // Named filters whose taps are compiled in (zero taps disappear); selected
 // whenever the caller's taps are bit-identical to them.
 template <class F, int N>
@@ -128,13 +188,21 @@ template <int K, int A, int MODE, class F, class... More>
 int launch_named(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                  const Taps &taps, bool vec, hipStream_t s, const edge::RowSrc &rs) {
     if constexpr (F::kK == K && F::kA == A && F::kMode == MODE) {
-        if (same_taps<F, K * K>(taps))
+        if (same_taps<F, K * K>(taps)) {
+            if constexpr (kBandFits<K, A>)
+                if (band_ok(in, out, w, pitch, rs))
+                    return launch_band<K, A, MODE, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
             return launch_wave<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
+        }
     }
-    if constexpr (sizeof...(More) > 0)
+    if constexpr (sizeof...(More) > 0) {
         return launch_named<K, A, MODE, More...>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
-    else
+    } else {
+        if constexpr (kBandFits<K, A>)
+            if (band_ok(in, out, w, pitch, rs))
+                return launch_band<K, A, MODE, edge::RuntimeTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
         return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
+    }
 }
 
 template <int K, int A, int MODE>
@@ -172,53 +240,6 @@ int launch_wave4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     return MPX_OK;
 }
 
-// Band kernel (conv_band4_kernel): 256-column strips, aprons, strip-minor with
-// alternating segment directions. seg <= 0: one resident round of per_simd
-// waves per SIMD (104 VGPRs: 4 resident), at least 8 rows per segment.
-// MI355X sobel5 4096^2, 6 rotated pairs (tools/kbench.py): auto at 4 waves
-// (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
-// 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
-inline constexpr int kBand4PerSimd = 4;
-template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
-int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                 const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kBand4PerSimd,
-                 int alt = 1) {
-    MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
-    if (!rs.up) rs.up = in;
-    if (!rs.dn) rs.dn = in;
-    const int strips = (w + 255) / 256;
-    if (seg <= 0) {
-        const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
-        const int64_t work = (int64_t)(oy1 - oy0) * strips;
-        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
-    }
-    const int segs = (oy1 - oy0 + seg - 1) / seg;
-    const int64_t nwaves = (int64_t)strips * segs;
-    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
-    constexpr int wpb = (OPT & 4) ? 16 : 4;
-    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + wpb - 1) / wpb)),
-                       dim3(64 * wpb), 0,
-                       s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
-    return MPX_OK;
-}
-
-// The band kernel serves the separable 5x5 launches whose rows (and neighbour
-// rows) are 16-B aligned, with non-temporal output stores (sobel5 4096^2, 6
-// rotated pairs: 28.9 us vs 29.4 plain stores vs 30.3 for the 8-B-lane wave
-// kernel, tools/kbench.py). MPX_CONV_BAND=0: wave kernel, 1: band kernel with
-// plain stores (same-box A/B); read once per process.
-inline int band_mode() {
-    static const int v = [] {
-        const char *e = std::getenv("MPX_CONV_BAND");
-        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
-    }();
-    return v;
-}
-inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs) {
-    return band_mode() != 0 && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
-           (!rs.up || aligned16(rs.up)) && (!rs.dn || aligned16(rs.dn));
-}
-
 template <class F, int K>
 inline bool same_sep_taps(const Taps &t, bool two) {
     auto eq = [](float a, float b) { return __builtin_bit_cast(uint32_t, a) == __builtin_bit_cast(uint32_t, b); };
@@ -241,19 +262,23 @@ int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int
     // sobel5 auto 24.7 us vs 26.1 at 8; gauss5 8 rows 23.4 us vs 25.1 auto)
     constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
     constexpr int order = MODE == MPX_CONV_MAG2 ? kWaveOrderAlt : kWaveOrder;
+    constexpr bool fits = kBandFits<K, A>;
+    const bool band = fits && band_ok(in, out, w, pitch, rs);
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
-        if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true) && band_ok(in, out, w, pitch, rs)) {
-            if (band_mode() == 1)
-                return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-            return launch_band4<K, A, MODE, true, edge::Sobel5SepTaps, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-        }
+        if (band && same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
+            return launch_band<K, A, MODE, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
         if (same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
             return launch_wave<K, A, MODE, true, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_LIN1) {
+        if (band && same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
+            return launch_band<K, A, MODE, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
         if (same_sep_taps<edge::Gauss5SepTaps, 5>(taps, false))
             return launch_wave<K, A, MODE, true, edge::Gauss5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
     }
+    if constexpr (fits)
+        if (band)
+            return launch_band<K, A, MODE, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
     return launch_wave<K, A, MODE, true, edge::RuntimeSepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, seg, order, rs);
 }
 

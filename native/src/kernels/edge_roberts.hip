@@ -164,7 +164,8 @@ __global__ void roberts_thin_kernel(const uint32_t *__restrict__ in, uint32_t *_
     }
 }
 
-// Internal-linkage tag for the tuned instantiation. conv_wave_kernel<...,
+// Internal-linkage tag for the tuned instantiation (band kernel when the rows
+// are 16-B aligned, else wave kernel). conv_wave_kernel<...,
 // edge::RobertsTaps> is also instantiated by the production and variants TUs;
 // a kernel name registered from several fat binaries may resolve to one of the
 // large code objects, whose first launch then costs ~1 ms more than this 43 KB
@@ -181,8 +182,11 @@ int roberts_impl(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by
     if (bx == 0 && by == 0 && gx == 0 && gy == 0) {  // tuned path: wave kernel with compiled-in Roberts taps
         const Taps taps = edgel::make_taps(2, kRobertsX, kRobertsY, true);
         const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
-        const int rc = edgel::launch_wave<2, 0, MPX_CONV_MAG2, true, RobertsTuned>(in, out, w, w, 0, h, 0, h - 1,
-                                                                                        taps, vec2, as_stream(stream));
+        const int rc = edgel::band_ok(in, out, w, w, edge::RowSrc{})
+                           ? edgel::launch_band<2, 0, MPX_CONV_MAG2, RobertsTuned>(in, out, w, w, 0, h, 0, h - 1, taps,
+                                                                                   as_stream(stream), edge::RowSrc{})
+                           : edgel::launch_wave<2, 0, MPX_CONV_MAG2, true, RobertsTuned>(in, out, w, w, 0, h, 0, h - 1,
+                                                                                         taps, vec2, as_stream(stream));
         if (rc != MPX_OK) return rc;
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;

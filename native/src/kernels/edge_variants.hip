@@ -246,6 +246,21 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         set_error("unsupported band OPT %d", p2 / 1000);
         return MPX_ERR_ARG;
     }
+    if (kind == 9) {
+        // dense band kernel, compiled-in taps (k = 2 Roberts, k = 5 sobel5_dense):
+        // p1 = segment rows (0 = auto), p2 % 100 = waves per SIMD for auto, p2 / 1000 = OPT
+        MPX_CHECK_ARG(p1 >= 0 && w % 4 == 0 && aligned16(in) && aligned16(out), "band variant: w % 4 == 0");
+        const Taps tp = make_taps(k, wx, wy, true);
+        const int per = p2 % 100 > 0 ? p2 % 100 : edgel::kBand4PerSimd;
+        if (k == 2) {
+            if (p2 / 1000 == 2)
+                return edgel::launch_band4<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 2>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
+            return edgel::launch_band4<2, 0, MPX_CONV_MAG2, true, edge::RobertsTaps, 0>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
+        }
+        if (p2 / 1000 == 2)
+            return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps, 2>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
+        return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps, 0>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
+    }
     if (kind == 5) {
         // 16-B-lane separable sobel5 (conv_wave4_kernel): p1 = segment rows (0 = auto),
         // p2 = waves per SIMD the auto segments target (0 = production default)
