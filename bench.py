@@ -217,7 +217,7 @@ def run(args) -> int:
             "config": {
                 "model": f"lab2 2D convolution {args.size}x{args.size} image, "
                          f"{d0.filter.k}x{d0.filter.k} filter ({d0.filter.name}"
-                         f"{', separable 1x5+5x1 passes' if d0.filter.separable else ''}, wave-streaming HIP kernel)",
+                         f"{', separable 1x5+5x1 passes' if d0.filter.separable else ''}, band-streaming HIP kernel)",
                 "global_batch": n,
                 "seq_len": args.size,
                 "parallelism": f"slab{n}" + (("+halo-peer-fused" if d0.peer is not None else "+halo-pipelined"
