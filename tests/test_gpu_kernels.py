@@ -58,6 +58,18 @@ def test_conv_matches_cpu_exact_and_torch(gpu, filt, hw):
     assert torch.equal(g[..., 3], img[..., 3])
 
 
+@pytest.mark.parametrize("filt", ["roberts", "sobel3", "sobel5", "gauss5", "log5", "sobel5_dense"])
+@pytest.mark.parametrize("w", [4, 8, 252, 256, 260, 512, 516, 1028])
+def test_conv_band_kernel_strip_edges(gpu, filt, w):
+    """Aligned widths take the band kernel (256-column strips, 8-B aprons at the
+    strip edges, clamp-to-edge by the lane's own pixel at x = 0 and x = w):
+    partial strips, exactly one strip, one lane, every segment height."""
+    f = ops.get_filter(filt)
+    for h in (1, 2, 5, 17, 33, 70):
+        img = rand_img(h, w, seed=w + h)
+        assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f)), (h, w)
+
+
 @pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "sharpen3", "sobel5_dense",
                                   "log5"])
 def test_conv_named_taps_equal_runtime_taps(gpu, filt):
