@@ -517,7 +517,6 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
     __shared__ uint32_t s_keys[kRTile];
     __shared__ uint32_t s_cnt[kRWaves][256];
-    __shared__ uint32_t s_dstart[256];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -572,25 +571,27 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             }
         }
         lds_barrier();
-        uint32_t cnt = 0;
+        uint32_t cnt = 0, wexcl[kRWaves];
         if (t < 256) {
 #pragma unroll
             for (int ww = 0; ww < kRWaves; ++ww) {
-                const uint32_t c = s_cnt[ww][t];
-                s_cnt[ww][t] = cnt;
-                cnt += c;
+                wexcl[ww] = cnt;
+                cnt += s_cnt[ww][t];
             }
         }
         const uint32_t dstart = scan256_excl_lds(cnt, s_wsum);
         if (t < 256) {
-            s_dstart[t] = dstart;
+            // one table per wave holding tile-local digit start + the wave's
+            // offset: the staging scatter below gathers once per key, not twice
+#pragma unroll
+            for (int ww = 0; ww < kRWaves; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
             s_gbase[t] = excl + dbase - dstart;
         }
         lds_barrier();
 #pragma unroll
         for (int e = 0; e < kRPer; ++e) {
             const uint32_t d = (key[e] >> shift) & 255u;
-            s_keys[s_dstart[d] + s_cnt[w][d] + rank[e]] = key[e];
+            s_keys[s_cnt[w][d] + rank[e]] = key[e];
         }
         lds_barrier();
 #pragma unroll 4

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Profiling driver: every workload's production kernels at the BASELINE sizes,
-a few times each after warm-up (run under rocprofv3)."""
+a few times each after warm-up (run under rocprofv3). lab2 cycles 6
+independent 4096^2 input/output pairs (768 MiB, 3x the MALL) so the counters
+describe HBM streaming, as bench.py does."""
 import os
 import sys
 
@@ -14,14 +16,16 @@ REPS = 3
 
 
 def main():
-    which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lab1", "lab2", "lab3", "jacobi"]
+    which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lab1", "lab2", "lab3", "jacobi", "lab5"]
     dev = torch.device("cuda:0")
     if "lab2" in which:
-        img = torch.randint(0, 256, (4096, 4096, 4), dtype=torch.uint8, device=dev)
-        out = torch.empty_like(img)
+        pairs = [(torch.randint(0, 256, (4096, 4096, 4), dtype=torch.uint8, device=dev),
+                  torch.empty((4096, 4096, 4), dtype=torch.uint8, device=dev)) for _ in range(6)]
         for f in ("sobel5", "sobel5_dense", "gauss5", "roberts", "sobel3"):
-            for _ in range(REPS + 1):
+            for k in range(REPS + 6):
+                img, out = pairs[k % 6]
                 ops.conv(img, f, out)
+        del pairs
     if "lab1" in which:
         a = torch.rand(1 << 26, device=dev)
         b = torch.rand(1 << 26, device=dev)
@@ -43,6 +47,15 @@ def main():
         res = torch.zeros(1, dtype=torch.float64, device=dev)
         for _ in range(REPS + 1):
             ops.jacobi_sweep(u, un, 1, n + 1, res)
+    if "lab5" in which:
+        for dt in (torch.int32, torch.float32):
+            src = (torch.randint(-2**31, 2**31 - 1, (1 << 26,), dtype=torch.int32, device=dev) if dt == torch.int32
+                   else torch.randn(1 << 26, device=dev))
+            x = torch.empty_like(src)
+            for _ in range(REPS + 1):
+                x.copy_(src)
+                ops.sort_(x)
+        del src, x
     torch.cuda.synchronize()
 
 
