@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         }
         uint32_t B[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
         uint32_t S[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
-        for (int c = 0; c < nc; ++c) {
+        auto one_class = [&](int c) {
             const float *w = fp.w[c];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -208,7 +208,17 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
                 rank_key(make_key_s(d.x, (uint32_t)c), B[2 * h], S[2 * h]);
                 rank_key(make_key_s(d.y, (uint32_t)c), B[2 * h + 1], S[2 * h + 1]);
             }
+        };
+        // four classes per iteration: their weights' scalar loads issue
+        // together (one s_waitcnt per four classes instead of per class)
+        int c = 0;
+        for (; c + 4 <= nc; c += 4) {
+            one_class(c);
+            one_class(c + 1);
+            one_class(c + 2);
+            one_class(c + 3);
         }
+        for (; c < nc; ++c) one_class(c);
         uint4 o;
         o.x = finish_pixel(q.x, B[0], S[0], fp.T2, nc, cp, amb);
         o.y = finish_pixel(q.y, B[1], S[1], fp.T2, nc, cp, amb);
