@@ -330,11 +330,19 @@ __device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t *s_wsum) {
 // the mask is deterministic whatever order the lanes land in). Three LDS ops
 // per 64 keys instead of an 8-ballot VALU match (~50 VALU per 64 keys), which
 // made the rank instruction-bound.
+// Each lane ORs and clears only its half-wave's 32-bit word of the slot
+// (ds_or_b32 / ds_write_b32: half the bytes and bank slots of a 64-bit
+// access); the read-back takes both words.
+// All three accesses go through uint32_t: a 64-bit read of the slot would not
+// alias the 32-bit OR and clear for the compiler (type-based alias analysis),
+// which may then move the clear above the read.
 __device__ __forceinline__ uint64_t match_digit_lds(uint32_t d, int lane, uint64_t *tbl) {
-    atomicOr(reinterpret_cast<unsigned long long *>(&tbl[d]), 1ull << lane);
-    const uint64_t m = tbl[d];
-    tbl[d] = 0;
-    return m;
+    uint32_t *slot = reinterpret_cast<uint32_t *>(tbl) + 2 * d;
+    uint32_t *word = slot + (lane >> 5);
+    atomicOr(word, 1u << (lane & 31));
+    const uint32_t lo = slot[0], hi = slot[1];
+    *word = 0;
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
