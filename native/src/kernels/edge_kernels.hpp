@@ -1125,10 +1125,15 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
     const int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (gw >= nwaves) return;  // wave-uniform
     const int strip = gw % strips;
-    const int sg = gw / strips;
+    const int segs = nwaves / strips;  // nwaves = strips * segs
+    // alt bit 1 (slab with rows in a neighbour's HBM, RowSrc): both boundary
+    // segments first — their halo loads go over xGMI, the slowest of the
+    // launch, so their waves start in the first round (as in conv_wave_kernel)
+    const int sg0 = gw / strips;
+    const int sg = (!(alt & 2) || segs < 3 || sg0 == 0) ? sg0 : (sg0 == 1 ? segs - 1 : sg0 - 1);
     const int ys = oy0 + sg * seg;
     const int ye = min(ys + seg, oy1);
-    if (alt && (sg & 1))  // wave-uniform: odd segments walk up
+    if ((alt & 1) && (sg & 1))  // wave-uniform: odd segments walk up
         band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
     else
         band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);

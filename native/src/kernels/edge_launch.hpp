@@ -125,6 +125,7 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
     if (!rs.up) rs.up = in;
     if (!rs.dn) rs.dn = in;
+    if (rs.up != in || rs.dn != in) alt |= 2;  // remote halo rows: boundary segments first
     const int strips = (w + 255) / 256;
     if (seg <= 0) {
         const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
