@@ -160,9 +160,23 @@ __device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_
 
 // ---------------------------------------------------------------------------
 // FAST32: VALU, 4 pixels per lane as two packed pairs.
+//
+// Undecided pixels (top-2 margin within the fp32 bound, ~0.02%) are not
+// re-ranked in fp64 inside the loop, where one such lane stalls its whole wave
+// for a full fp64 chain: their indices go to a per-block LDS list and the
+// block re-ranks them together after its grid-stride loop (all lanes busy)
+// and overwrites the provisional fp32 result. A full list falls back to the
+// inline fp64 chain.
 // ---------------------------------------------------------------------------
+constexpr int kAmbCap = 512;
+
 __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, FastParams fp, uint32_t *amb) {
+    __shared__ int64_t s_amb[kAmbCap];
+    __shared__ uint32_t s_ambpx[kAmbCap];
+    __shared__ uint32_t s_namb;
+    if (threadIdx.x == 0) s_namb = 0;
+    __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     uint4 *v = reinterpret_cast<uint4 *>(img);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -219,12 +233,27 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             one_class(c + 3);
         }
         for (; c < nc; ++c) one_class(c);
-        uint4 o;
-        o.x = finish_pixel(q.x, B[0], S[0], fp.T2, nc, cp, amb);
-        o.y = finish_pixel(q.y, B[1], S[1], fp.T2, nc, cp, amb);
-        o.z = finish_pixel(q.z, B[2], S[2], fp.T2, nc, cp, amb);
-        o.w = finish_pixel(q.w, B[3], S[3], fp.T2, nc, cp, amb);
-        v[i] = o;
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[k] = (px[k] & 0x00ffffffu) | ((B[k] & 31u) << 24);
+            if (__builtin_expect(!decided(B[k], S[k], fp.T2), 0)) {
+                if (amb) atomicAdd(amb, 1u);
+                const uint32_t slot = atomicAdd(&s_namb, 1u);
+                if (slot < (uint32_t)kAmbCap) {  // deferred
+                    s_amb[slot] = i * 4 + k;
+                    s_ambpx[slot] = px[k];
+                } else {
+                    o[k] = classify_direct(px[k], nc, cp);
+                }
+            }
+        }
+        v[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+    const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
+    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+        img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
     }
 }
 
