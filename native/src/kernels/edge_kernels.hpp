@@ -954,7 +954,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // apron: lane 0 reads the two columns left of the strip, lane 63 the two
     // right of it; at the image edges the lane's own edge pixel stands in
     const bool ap_left = lane == 0, ap_right = lane == 63;
-    const bool ap_have = (ap_left && x0 > 0) || (ap_right && x0 + 256 < w);
+    // OPT bit 4 (cost probe only, wrong at strip edges): no apron loads
+    const bool ap_have = !(OPT & 16) && ((ap_left && x0 > 0) || (ap_right && x0 + 256 < w));
     constexpr int kDrop = 0x7ffffff0;
     const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : kDrop;
     const int iy0 = ys - A;
@@ -1114,7 +1115,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 
 // OPT (tuning variants): bit 0 caps registers for 5 waves per SIMD, bit 1
 // non-temporal output stores, bit 2 16-wave workgroups (a band row's 16 strips
-// of a 4096-wide image on one CU).
+// of a 4096-wide image on one CU), bit 4 no apron loads (cost probe: wrong
+// results at the strip edges).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
