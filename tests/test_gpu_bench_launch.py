@@ -1,0 +1,26 @@
+"""bench.py's own N-rank launch on the GPU box: two ranks rehearsed on the one
+GPU (gloo control plane, peer halos over IPC), the path the driver's 1/2/4/8
+scaling run takes with one rank per GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from .helpers import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_self_launch_two_ranks_peer(gpu):
+    env = dict(os.environ, MPX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--rotate", "2", "--size", "512", "--no-cpu-baseline", "--halo", "peer"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 2 and rec["world_size_seen"]["torch_distributed"] == 2
+    assert rec["verified_bit_exact"] is True and rec["verified_pixels"] == 2 * 2 * 512 * 512
+    assert rec["config"]["transport"] == "xgmi-peer"
+    assert len(rec["per_rank_ms_per_step"]) == 2
