@@ -93,7 +93,7 @@ def main() -> int:
     ok = parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
     if ctx.rank == 0:
         print(json.dumps({"workload": a.workload, "n_gpus": n_ranks, "steps": a.steps, "warmup": a.warmup,
-                          "value": round(value, 3), "unit": unit, "ms_per_step": round(el * 1e3 / a.steps, 5),
+                          "value": float(f"{value:.6g}"), "unit": unit, "ms_per_step": round(el * 1e3 / a.steps, 5),
                           "per_rank_ms": [round(t * 1e3 / a.steps, 5) for t in per_rank], "scaling": "weak",
                           "verified": ok, **extra}), flush=True)
     parallel.shutdown()

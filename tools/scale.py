@@ -157,11 +157,11 @@ def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
         r["efficiency"] = None
         if r["status"] != "ok" or b is None:
             continue
-        if r["kind"] == "weak" and r.get("value") and b.get("value"):
+        if r["kind"] == "weak" and r.get("value") is not None and b.get("value"):
             r["efficiency"] = round(r["value"] / (r["n"] * b["value"]), 4)
             if rehearse:
                 r["retained"] = round(r["value"] / b["value"], 4)
-        elif r["kind"] == "strong" and r.get("ms") and b.get("ms"):
+        elif r["kind"] == "strong" and r.get("ms") is not None and b.get("ms"):
             r["efficiency"] = round(b["ms"] / (r["n"] * r["ms"]), 4)
             r["speedup"] = round(b["ms"] / r["ms"], 3)
             if rehearse:
