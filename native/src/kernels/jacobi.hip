@@ -140,6 +140,7 @@ __global__ __launch_bounds__(256) void jacobi_kernel(const T *__restrict__ u, T 
 // wave-strip kernel (16-B vectors, cols % NV == 0, pitch % NV == 0)
 // ---------------------------------------------------------------------------
 constexpr int kStripVec = 62;             // output vectors per wave
+constexpr int kJacobiRows = 8;            // rows per wave (row block) of the production sweeps
 constexpr uint32_t kDrop = 0x7ffffff0u;   // buffer offset past any range: store dropped
 
 template <typename T> struct JWide;
@@ -202,8 +203,45 @@ __device__ __forceinline__ void peer_wait(const uint32_t *flag, uint32_t target,
     }
 }
 
-template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true, bool PEER = false>
-__global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
+// Max over the wave of non-negative values through DPP (row_shr 1/2/4/8 within
+// each 16-lane row, then row_bcast 15/31 across rows; lanes with no source
+// read +0, the identity here), read from lane 63. VALU only, in place of a
+// 6 (fp32) / 12 (fp64) step __shfl_xor tree through the LDS crossbar.
+template <int CTRL, int RMASK, typename T>
+__device__ __forceinline__ T dpp_max_step(T v) {
+    T o;
+    if constexpr (sizeof(T) == 8) {
+        const uint2 b = __builtin_bit_cast(uint2, v);
+        uint2 r;
+        r.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b.x, CTRL, RMASK, 0xf, true);
+        r.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b.y, CTRL, RMASK, 0xf, true);
+        o = __builtin_bit_cast(T, r);
+    } else {
+        o = __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, RMASK, 0xf, true));
+    }
+    return o > v ? o : v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max_dpp(T v) {
+    v = dpp_max_step<0x111, 0xf>(v);  // row_shr:1
+    v = dpp_max_step<0x112, 0xf>(v);  // row_shr:2
+    v = dpp_max_step<0x114, 0xf>(v);  // row_shr:4
+    v = dpp_max_step<0x118, 0xf>(v);  // row_shr:8 -> lane 15 of each row holds its row's max
+    v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+    v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3 -> lane 63 holds the max
+    if constexpr (sizeof(T) == 8) {
+        const uint2 b = __builtin_bit_cast(uint2, v);
+        return __builtin_bit_cast(T, make_uint2((uint32_t)__builtin_amdgcn_readlane((int)b.x, 63),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)b.y, 63)));
+    } else {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+    }
+}
+
+template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true, bool PEER = false, bool ALT = false,
+          int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
                                                           int nwaves, T *__restrict__ resid, mpx_jacobi_peer pr) {
     using V = typename JWide<T>::type;
@@ -256,80 +294,103 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
             if constexpr (LNT) return __builtin_nontemporal_load(p);  // tuning variant
             else return *p;
         };
-        // ring: row x_{i0-1+t} lives in slot t % 5; the loop advances 5 rows so
-        // every slot index is a compile-time constant (no register rotation,
-        // whose moves would force a wait on the in-flight prefetch)
-        V S[5];
-        S[0] = ld(i0 - 1);
-        S[1] = ld(i0);
-        S[2] = ld(min(i0 + 1, i1));
-        S[3] = ld(min(i0 + 2, i1));
-        S[4] = V{};  // first written by step 0; a copy of S[3] would wait on its load
         const uint32_t soff = out_lane ? (uint32_t)(cv * NV * sizeof(T)) : kDrop;
         const int j0 = cv * NV;
-        __builtin_amdgcn_sched_barrier(0);
-        auto step = [&](auto kc, int i) {
-            constexpr int k = decltype(kc)::value;
-            const int r = i + k;                   // row computed in this step
-            S[(k + 4) % 5] = ld(min(r + 3, i1));   // x_{r+3} replaces x_{r-2}
-            const V up = S[k % 5], cen = S[(k + 1) % 5], dn = S[(k + 2) % 5];
-            const T left = dpp_shift<T>(cen[NV - 1], 0x138);  // lane - 1's last element
-            const T right = dpp_shift<T>(cen[0], 0x130);      // lane + 1's first element
-            V res;
-#pragma unroll
-            for (int e = 0; e < NV; ++e) {
-                const int j = j0 + e;
-                const T l = e == 0 ? left : cen[e - 1];
-                const T rr = e == NV - 1 ? right : cen[e + 1];
-                const T sm = ((up[e] + dn[e]) + (l + rr)) * (T)0.25;
-                const bool interior = j > 0 && j < cols - 1;
-                res[e] = interior ? sm : cen[e];
-                const T d = sm > cen[e] ? sm - cen[e] : cen[e] - sm;
-                rmax = fmax(rmax, (interior && out_lane) ? d : (T)0);  // select + v_max: no exec branch
+        // One walk over the block's rows, prologue included (each direction its
+        // own inlined body: nothing but scalars is live across the branch).
+        // UPW (ALT, odd row blocks): bottom row first, so two vertically
+        // adjacent blocks read the halo rows they share at the same moment.
+        // ring: row x_{i0-1+t} (x_{i1-t} walking up) lives in slot t % 5; the
+        // loop advances 5 rows so every slot index is a compile-time constant
+        // (no register rotation, whose moves would force a wait on the
+        // in-flight prefetch)
+        auto walk = [&](auto upc) {
+            constexpr bool UPW = decltype(upc)::value;
+            V S[5];
+            if constexpr (UPW) {
+                S[0] = ld(i1);
+                S[1] = ld(i1 - 1);
+                S[2] = ld(max(i1 - 2, i0 - 1));
+                S[3] = ld(max(i1 - 3, i0 - 1));
+            } else {
+                S[0] = ld(i0 - 1);
+                S[1] = ld(i0);
+                S[2] = ld(min(i0 + 1, i1));
+                S[3] = ld(min(i0 + 2, i1));
             }
-            // rows past i1 (tail group) store nowhere: offset out of range
-            const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
-                un + (int64_t)min(r, i1 - 1) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            if (PEER && edge && (r == r0 || r == r1 - 1))  // a row the neighbours read: write through
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0,
-                                                       kCpolSystem);
-            else
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, r < i1 ? soff : kDrop, 0, AUX);
-            // keep each step's prefetch at its start: the scheduler otherwise sinks
-            // loads past the next step's use and the wait counts collapse to 0
+            S[4] = V{};  // first written by step 0; a copy of S[3] would wait on its load
             __builtin_amdgcn_sched_barrier(0);
-        };
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        using I3 = std::integral_constant<int, 3>;
-        using I4 = std::integral_constant<int, 4>;
-        // straight-line groups of 5 rows with no branch inside a group (a branch
-        // between the steps costs the wait counts their precision: 10-rows-per-
-        // wave sweeps measured 9% slower with per-step exits), then the 1-4 tail
-        // rows; TAIL_EXIT = false (tuning variant) instead runs the tail as a
-        // whole group, computing the surplus rows on clamped data and dropping
-        // them at the buffer store
-        int i = i0;
-        const int iend = TAIL_EXIT ? i0 + (i1 - i0) / 5 * 5 : i1;
-        for (; i < iend; i += 5) {
-            step(I0{}, i);
-            step(I1{}, i);
-            step(I2{}, i);
-            step(I3{}, i);
-            step(I4{}, i);
-        }
-        if (TAIL_EXIT && i < i1) {
-            step(I0{}, i);
-            if (i + 1 < i1) {
+            auto step = [&](auto kc, int i) {
+                constexpr int k = decltype(kc)::value;
+                const int r = UPW ? i - k : i + k;  // row computed in this step
+                // x_{r+3} replaces x_{r-2} (walking up: x_{r-3} replaces x_{r+2})
+                S[(k + 4) % 5] = UPW ? ld(max(r - 3, i0 - 1)) : ld(min(r + 3, i1));
+                const V up = S[(UPW ? k + 2 : k) % 5], cen = S[(k + 1) % 5], dn = S[(UPW ? k : k + 2) % 5];
+                const T left = dpp_shift<T>(cen[NV - 1], 0x138);  // lane - 1's last element
+                const T right = dpp_shift<T>(cen[0], 0x130);      // lane + 1's first element
+                V res;
+#pragma unroll
+                for (int e = 0; e < NV; ++e) {
+                    const int j = j0 + e;
+                    const T l = e == 0 ? left : cen[e - 1];
+                    const T rr = e == NV - 1 ? right : cen[e + 1];
+                    const T sm = ((up[e] + dn[e]) + (l + rr)) * (T)0.25;
+                    const bool interior = j > 0 && j < cols - 1;
+                    res[e] = interior ? sm : cen[e];
+                    const T d = sm > cen[e] ? sm - cen[e] : cen[e] - sm;
+                    rmax = fmax(rmax, (interior && out_lane) ? d : (T)0);  // select + v_max: no exec branch
+                }
+                // rows outside the block (tail group) store nowhere: offset out of range
+                const bool rok = UPW ? r >= i0 : r < i1;
+                const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
+                    un + (int64_t)(UPW ? max(r, i0) : min(r, i1 - 1)) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
+                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                if (PEER && edge && (r == r0 || r == r1 - 1))  // a row the neighbours read: write through
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0,
+                                                           kCpolSystem);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0, AUX);
+                // keep each step's prefetch at its start: the scheduler otherwise sinks
+                // loads past the next step's use and the wait counts collapse to 0
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            using I4 = std::integral_constant<int, 4>;
+            // straight-line groups of 5 rows with no branch inside a group (a branch
+            // between the steps costs the wait counts their precision: 10-rows-per-
+            // wave sweeps measured 9% slower with per-step exits), then the 1-4 tail
+            // rows; TAIL_EXIT = false (tuning variant) instead runs the tail as a
+            // whole group, computing the surplus rows on clamped data and dropping
+            // them at the buffer store
+            const int nrow = i1 - i0;
+            const int ngrp = TAIL_EXIT ? nrow / 5 : (nrow + 4) / 5;
+            int i = UPW ? i1 - 1 : i0;
+            for (int g = 0; g < ngrp; ++g, i += UPW ? -5 : 5) {
+                step(I0{}, i);
                 step(I1{}, i);
-                if (i + 2 < i1) {
-                    step(I2{}, i);
-                    if (i + 3 < i1) step(I3{}, i);
+                step(I2{}, i);
+                step(I3{}, i);
+                step(I4{}, i);
+            }
+            const int rem = TAIL_EXIT ? nrow - ngrp * 5 : 0;
+            if (rem > 0) {
+                step(I0{}, i);
+                if (rem > 1) {
+                    step(I1{}, i);
+                    if (rem > 2) {
+                        step(I2{}, i);
+                        if (rem > 3) step(I3{}, i);
+                    }
                 }
             }
-        }
+        };
+        if (ALT && (rb & 1))  // wave-uniform
+            walk(std::true_type{});
+        else
+            walk(std::false_type{});
         if constexpr (PEER) {
             if (edge) {
                 // the write-through edge-row stores are acknowledged at system scope
@@ -347,14 +408,21 @@ __global__ __launch_bounds__(256) void jacobi_wave_kernel(const T *__restrict__ 
             }
         }
     }
-    if (resid) {
+    if (resid) {  // block-uniform; no wave returned early, so the barrier is safe
+        // one agent-scope load + atomic per workgroup, not per wave: the load
+        // misses every XCD's L2 (~1-2 us), and per wave those tails cost the
+        // residual sweep ~60 us at 16384^2
         using B = typename JVec<T>::bits;
+        __shared__ T s_m[WPB];
+        const T m = wave_max_dpp(rmax);
+        if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            T mm = s_m[0];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const T o = __shfl_xor(rmax, m);
-            rmax = o > rmax ? o : rmax;
+            for (int q = 1; q < WPB; ++q) mm = s_m[q] > mm ? s_m[q] : mm;
+            if (mm > (T)0) residual_max(reinterpret_cast<B *>(resid), __builtin_bit_cast(B, mm));
         }
-        if ((threadIdx.x & 63) == 0 && rmax > (T)0) residual_max(reinterpret_cast<B *>(resid), __builtin_bit_cast(B, rmax));
     }
 }
 
@@ -367,18 +435,17 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
     if ((pitch % NV == 0) && (cols % NV == 0) && aligned16(u) && aligned16(un)) {
         const int strips = (cols / NV + kStripVec - 1) / kStripVec;
         const int rows = r1 - r0;
-        // 5 rows per wave = one straight-line group (tools/jbench.py,
-        // profiles/jacobi.md: 16384^2 fp64 R5 756 us / R4 769 / R8 763 / R16 795
-        // / R64 910; fp32 R5 370 / R4 402) — many short waves hide HBM latency
-        // better than amortising the two halo rows, which neighbouring waves
-        // re-read from L2; stores nontemporal (aux NT): the next sweep reads
-        // u_new from HBM anyway, and keeping it out of L2 leaves L2 to those
-        // shared halo rows
-        int R = 5;
+        // 8 rows per wave, odd row blocks walking up (ALT: two vertically
+        // adjacent blocks read their shared halo rows at the same moment) —
+        // tools/jbench.py, profiles/jacobi.md: 16384^2 fp64 R8+alt 728 us vs
+        // 763 (R5, all down) / 767 (R8, all down); fp32 363 vs 370 / 396.
+        // Stores nontemporal (aux NT): the next sweep reads u_new from HBM
+        // anyway, and keeping it out of L2 leaves L2 to the shared halo rows
+        int R = kJacobiRows;
         while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
-        hipLaunchKernelGGL((jacobi_wave_kernel<T, 2>), dim3((nwaves + 3) / 4), dim3(256), 0, as_stream(stream), u, un,
-                           cols, pitch, r0, r1, strips, R, nwaves, resid, mpx_jacobi_peer{});
+        hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
+                           as_stream(stream), u, un, cols, pitch, r0, r1, strips, R, nwaves, resid, mpx_jacobi_peer{});
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;
     }
@@ -408,10 +475,10 @@ int launch_jacobi_peer(const T *u, T *un, int cols, int pitch, int rows, T *resi
     for (const void *q : {pr.up_row[0], pr.up_row[1], pr.dn_row[0], pr.dn_row[1]})
         MPX_CHECK_ARG(!q || aligned16(q), "neighbour rows must be 16-byte aligned");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
-    int R = 5;
+    int R = kJacobiRows;
     while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
     const int nwaves = strips * ((rows + R - 1) / R);
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, true, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
                        as_stream(stream), u, un, cols, pitch, 1, rows + 1, strips, R, nwaves, resid, pr);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
@@ -450,8 +517,9 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
                                   int R, int aux, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(u && un && cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0 && R >= 1, "bad arguments");
-    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6 || aux == 10,
-                  "aux must be 0, 2, 6 (2 + non-temporal loads) or 10 (2 without the tail exit)");
+    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6 || aux == 10 || aux == 18 || aux == 50,
+                  "aux must be 0, 2, 6 (2 + non-temporal loads), 10 (2 without the tail exit) or 18 (2 + "
+                  "alternating walk directions), 50 (18 with 16-wave workgroups)");
     const int NV = fp64 ? 2 : 4;
     MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un), "needs the vector layout");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
@@ -464,17 +532,25 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
 #define MPX_JVN(T)                                                                                             \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, true>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
                        strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
+#define MPX_JVA(T)                                                                                             \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true>), g, b, 0, s, (const T *)u, (T *)un, cols,  \
+                       pitch, r0, r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
+#define MPX_JVW(T)                                                                                             \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true, 16>), dim3((nwaves + 15) / 16), dim3(1024),  \
+                       0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVX(T)                                                                                             \
     hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, false>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, \
                        r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
     if (fp64) {
-        if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
+        if (aux == 50) MPX_JVW(double); else if (aux == 18) MPX_JVA(double); else if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
     } else {
-        if (aux == 10) MPX_JVX(float); else if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
+        if (aux == 50) MPX_JVW(float); else if (aux == 18) MPX_JVA(float); else if (aux == 10) MPX_JVX(float); else if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
     }
 #undef MPX_JV
 #undef MPX_JVN
 #undef MPX_JVX
+#undef MPX_JVA
+#undef MPX_JVW
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }

@@ -25,10 +25,16 @@ def main():
         res_t = torch.zeros(1, dtype=dt, device=dev)
         var = {"production": lambda: ops.jacobi_sweep(u, un, 1, n + 1),
                "production+residual": lambda: (res_t.zero_(), ops.jacobi_sweep(u, un, 1, n + 1, res_t))}
-        for R in (3, 4, 5, 8, 10, 16, 64):
-            for aux in (2, 10):
+        Rs = [int(x) for x in os.environ.get("JBENCH_R", "3,4,5,8,10,16,64").split(",")]
+        auxs = [int(x) for x in os.environ.get("JBENCH_AUX", "2,10").split(",")]
+        for R in Rs:
+            for aux in auxs:  # 18: alternating walk directions
                 var[f"R{R}/aux{aux}"] = (lambda R=R, aux=aux: _native.check(L.mpx_jacobi_variant(
                     u.data_ptr(), un.data_ptr(), n, n, 1, n + 1, None, int(dt == torch.float64), R, aux, 0)))
+                if os.environ.get("JBENCH_RESID"):
+                    var[f"R{R}/aux{aux}+residual"] = (lambda R=R, aux=aux: (res_t.zero_(), _native.check(
+                        L.mpx_jacobi_variant(u.data_ptr(), un.data_ptr(), n, n, 1, n + 1, res_t.data_ptr(),
+                                             int(dt == torch.float64), R, aux, 0))))
         res = {k: [] for k in var}
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for name, fn in var.items():
