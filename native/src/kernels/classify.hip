@@ -35,6 +35,8 @@
 //     replaced by the class index): best = min(best, key), second =
 //     med3(best, key, second). A bias folded into the constant weight makes
 //     every computed value positive, so unsigned key order is value order.
+#include <cstdlib>
+
 #include "internal.hpp"
 
 #include <cmath>
@@ -170,8 +172,12 @@ __device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_
 // ---------------------------------------------------------------------------
 constexpr int kAmbCap = 512;
 
+// NQ: 16-B vectors (4 pixels each) per thread and loop trip; nvec counts
+// groups of NQ vectors.
+template <int NQ>
 __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, FastParams fp, uint32_t *amb) {
+    constexpr int NP = 4 * NQ;  // pixels per thread and trip
     __shared__ int64_t s_amb[kAmbCap];
     __shared__ uint32_t s_ambpx[kAmbCap];
     __shared__ uint32_t s_namb;
@@ -183,14 +189,25 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
     // software-pipelined grid-stride loop: the next 16-B vector is in flight
     // while this one is ranked (a thread walks ~32 vectors at 8192^2; without
     // the prefetch each step exposes a full HBM round trip)
-    uint4 qn = i < nvec ? v[i] : uint4{};
-    for (; i < nvec; i += stride) {
-        const uint4 q = qn;
-        if (i + stride < nvec) qn = v[i + stride];
-        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
-        f2_t f[2][9];
+    uint4 qn[NQ];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+    for (int qq = 0; qq < NQ; ++qq) qn[qq] = i < nvec ? v[i * NQ + qq] : uint4{};
+    for (; i < nvec; i += stride) {
+        uint32_t px[NP];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+            px[4 * qq + 0] = qn[qq].x;
+            px[4 * qq + 1] = qn[qq].y;
+            px[4 * qq + 2] = qn[qq].z;
+            px[4 * qq + 3] = qn[qq].w;
+        }
+        if (i + stride < nvec) {
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) qn[qq] = v[(i + stride) * NQ + qq];
+        }
+        f2_t f[NP / 2][9];
+#pragma unroll
+        for (int h = 0; h < NP / 2; ++h) {
             // channel - 128, exact in fp32 (v_cvt_f32_ubyteN + one packed add).
             // NB: (float)__builtin_amdgcn_sbfe(x, o, 8) is miscompiled by hipcc
             // 7.2 into v_cvt_f32_u32_sdwa sext(x) (negative values convert as
@@ -210,12 +227,13 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             f[h][7] = g;
             f[h][8] = bl;
         }
-        uint32_t B[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
-        uint32_t S[4] = {kKeyInit, kKeyInit, kKeyInit, kKeyInit};
+        uint32_t B[NP], S[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) B[q] = S[q] = kKeyInit;
         auto one_class = [&](int c) {
             const float *w = fp.w[c];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < NP / 2; ++h) {
                 f2_t d = {w[9], w[9]};
 #pragma unroll
                 for (int k = 0; k < 9; ++k) d = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d);
@@ -233,22 +251,24 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             one_class(c + 3);
         }
         for (; c < nc; ++c) one_class(c);
-        uint32_t o[4];
+        uint32_t o[NP];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < NP; ++k) {
             o[k] = (px[k] & 0x00ffffffu) | ((B[k] & 31u) << 24);
             if (__builtin_expect(!decided(B[k], S[k], fp.T2), 0)) {
                 if (amb) atomicAdd(amb, 1u);
                 const uint32_t slot = atomicAdd(&s_namb, 1u);
                 if (slot < (uint32_t)kAmbCap) {  // deferred
-                    s_amb[slot] = i * 4 + k;
+                    s_amb[slot] = i * NP + k;
                     s_ambpx[slot] = px[k];
                 } else {
                     o[k] = classify_direct(px[k], nc, cp);
                 }
             }
         }
-        v[i] = make_uint4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+            v[i * NQ + qq] = make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]);
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
@@ -672,14 +692,24 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             done = nchunks * 128;
         }
     } else if (chosen == MPX_CLS_FAST) {
-        const int64_t nvec = npix / 4;
+        // 8 pixels per thread and trip (two 16-B vectors): same box, 8192^2,
+        // nc 4 / 16 / 32: 126 / 357-359 / 616-626 us vs 127 / 361-365 / 638-641
+        // with 4 (profiles/lab3_classify.md). MPX_CLS_NQ=1 selects 4 (A/B); read once
+        static const int nq = [] {
+            const char *e = std::getenv("MPX_CLS_NQ");
+            return (e && e[0] == '1') ? 1 : 2;
+        }();
+        const int64_t nvec = npix / (4 * nq);
         if (nvec > 0) {
             const int blk = block > 0 ? block : 256;
             const int64_t blocks = (nvec + blk - 1) / blk;
             const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
-            hipLaunchKernelGGL(classify_fast32_kernel, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            if (nq == 2)
+                hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            else
+                hipLaunchKernelGGL(classify_fast32_kernel<1>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            done = nvec * 4;
+            done = nvec * 4 * nq;
         }
     }
     if (done < npix) {
