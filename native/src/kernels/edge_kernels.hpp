@@ -775,150 +775,12 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Wave-streaming kernel for SEPARABLE filters with 16-B lanes (4 pixels per
-// lane, 256 columns per wave; production path when width, pitch and every
-// row source are 16-B aligned). Same streaming scheme as conv_wave_kernel —
-// prefetch ring of raw rows, one horizontal pass per input row into a K-row
-// ring of sums, vertical pass per output row — but each lane loads/stores one
-// dwordx4 per row, and the per-row scalar work, DPP moves and address
-// arithmetic are spread over four pixels instead of two. Lane 0 and lane 63
-// only supply halo columns (A, R <= 4): 248 output columns per strip.
-// ---------------------------------------------------------------------------
-template <int K, int A, int MODE, bool FAST, class F, int PF = 4>
-__global__ __launch_bounds__(256) void conv_wave4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                         int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                                                         int seg, int segs_per_strip, int nwaves, int strips,
-                                                         Taps taps, RowSrc rs) {
-    static_assert(F::kSep, "conv_wave4_kernel evaluates separable filters");
-    constexpr int R = K - 1 - A;
-    static_assert(A <= 4 && R <= 4, "halo wider than one lane");
-    constexpr int OW = 248;
-    constexpr int NV = 4 + A + R;  // window values per lane and row
-    constexpr bool TWO = (MODE == MPX_CONV_MAG2);
-    const int lane = threadIdx.x & 63;
-    const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (gw >= nwaves) return;  // wave-uniform
-    const int strip = gw % strips;
-    const int sg0 = gw / strips;
-    const int sg = (segs_per_strip < 3 || sg0 == 0) ? sg0 : (sg0 == 1 ? segs_per_strip - 1 : sg0 - 1);
-    const int ys = oy0 + sg * seg;
-    const int ye = min(ys + seg, oy1);
-    const int cin = strip * OW - 4 + 4 * lane;  // this lane's first input column (multiple of 4)
-    const bool st = lane >= 1 && lane <= 62 && cin < w;
-    const int iy0 = ys - A;
-    const int cc = mpx_clampi(cin, 0, w - 4);
-    const bool q_left = cin < 0, q_right = cin >= w;
-    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-    auto load_row = [&](int i) -> u32x4_t {
-        const int gy = mpx_clampi(iy0 + i, y_lo, y_hi);
-        const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
-        const u32x4_t r = *reinterpret_cast<const u32x4_t *>(src + (int64_t)gy * pitch + cc);
-        __builtin_amdgcn_sched_barrier(0);
-        return r;
-    };
-    auto fix_quad = [&](u32x4_t q) -> u32x4_t {
-        // a quad lies entirely inside, left or right of the image (w % 4 == 0)
-        u32x4_t p;
-        p.x = q_right ? q.w : q.x;
-        p.y = q_left ? q.x : (q_right ? q.w : q.y);
-        p.z = q_left ? q.x : (q_right ? q.w : q.z);
-        p.w = q_left ? q.x : q.w;
-        return p;
-    };
-
-    constexpr int D = K * ((PF + K - 1) / K);
-    u32x4_t pre[D];
-    f2_t hxr[K][2], hyr[K][2];
-    uint32_t alp[K];  // packed alpha bytes of each ring row's four pixels
-
-    auto consume = [&](int u, u32x4_t px) {
-        const f2_t l01 = luma2(px.x, px.y), l23 = luma2(px.z, px.w);
-        alp[u] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px.w, px.z, 0x07030000u),
-                                       __builtin_amdgcn_perm(px.y, px.x, 0x07030000u), 0x07060302u);
-        float wv[NV];
-        wv[A + 0] = l01.x;
-        wv[A + 1] = l01.y;
-        wv[A + 2] = l23.x;
-        wv[A + 3] = l23.y;
-        if constexpr (A >= 1) wv[A - 1] = from_prev(l23.y);
-        if constexpr (A >= 2) wv[A - 2] = from_prev(l23.x);
-        if constexpr (A >= 3) wv[A - 3] = from_prev(l01.y);
-        if constexpr (A >= 4) wv[A - 4] = from_prev(l01.x);
-        if constexpr (R >= 1) wv[A + 4] = from_next(l01.x);
-        if constexpr (R >= 2) wv[A + 5] = from_next(l01.y);
-        if constexpr (R >= 3) wv[A + 6] = from_next(l23.x);
-        if constexpr (R >= 4) wv[A + 7] = from_next(l23.y);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            auto pair = [&](int dx) { return f2_t{wv[2 * e + dx], wv[2 * e + dx + 1]}; };
-            hxr[u][e] = sep_chain<F, K, 0>(taps, pair);
-            if constexpr (TWO) hyr[u][e] = sep_chain<F, K, 2>(taps, pair);
-        }
-    };
-
-#pragma unroll
-    for (int q = 0; q < D; ++q) pre[q] = load_row(q);
-#pragma unroll
-    for (int u = 0; u < K - 1; ++u) {
-        const u32x4_t px = fix_quad(pre[u]);
-        pre[u] = load_row(u + D);
-        consume(u, px);
-    }
-    const int ngroups = (ye - ys + D - 1) / D;
-    for (int g = 0; g < ngroups; ++g) {
-#pragma unroll
-        for (int v = 0; v < D; ++v) {
-            const int u = (K - 1 + v) % K;
-            const int q = (K - 1 + v) % D;
-            const int i = K - 1 + g * D + v;
-            const u32x4_t px = fix_quad(pre[q]);
-            pre[q] = load_row(i + D);
-            consume(u, px);
-            const int y = ys + g * D + v;
-            uint32_t gray[4];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                f2_t gx = sep_chain<F, K, 1>(taps, [&](int dy) { return hxr[(u + 1 + dy) % K][e]; });
-                const float sx = sep_scale<F, K, false>(taps);
-                gx = gx * f2_t{sx, sx};
-                if constexpr (TWO) {
-                    f2_t gy = sep_chain<F, K, 3>(taps, [&](int dy) { return hyr[(u + 1 + dy) % K][e]; });
-                    const float sy = sep_scale<F, K, true>(taps);
-                    gy = gy * f2_t{sy, sy};
-                    const f2_t sq = gx * gx + gy * gy;
-                    if constexpr (FAST) {
-                        mag2_to_gray(sq.x, sq.y, gray[2 * e], gray[2 * e + 1]);
-                    } else {
-                        gray[2 * e] = mag_to_gray<false>(sq.x);
-                        gray[2 * e + 1] = mag_to_gray<false>(sq.y);
-                    }
-                } else {
-                    gray[2 * e] = finish_gray<MODE, FAST>(gx.x, 0.0f);
-                    gray[2 * e + 1] = finish_gray<MODE, FAST>(gx.y, 0.0f);
-                }
-            }
-            // (g, g, g, alpha_i): selector byte 3 = 4 + i picks alpha byte i
-            const uint32_t a = alp[(u + 1 + A) % K];
-            u32x4_t o;
-            o.x = __builtin_amdgcn_perm(a, gray[0], 0x04000000u);
-            o.y = __builtin_amdgcn_perm(a, gray[1], 0x05000000u);
-            o.z = __builtin_amdgcn_perm(a, gray[2], 0x06000000u);
-            o.w = __builtin_amdgcn_perm(a, gray[3], 0x07000000u);
-            const bool row_ok = y < ye;
-            const int yc = row_ok ? y : ys;
-            const __amdgpu_buffer_rsrc_t orow =
-                __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, w * 4, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(o, orow, (st && row_ok) ? cin * 4 : 0x7ffffff0, 0, 0);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Band kernel, 16-B lanes, no overlapping strips (separable and dense windows
 // up to 5x5 with at most two columns of reach on each side).
 //
-// conv_wave4_kernel spends lanes 0 and 63 on halo columns (248 of 256 loaded
-// columns produce), so its strips start at 992-B offsets and every row piece
+// A 16-B-lane wave kernel with halo lanes (lanes 0 and 63 only loading halo
+// columns, 248 of 256 columns produce; removed in round 2, numbers in
+// profiles/lab2_conv.md) starts its strips at 992-B offsets, so every row piece
 // straddles one more 128-B line than it needs. Here a wave owns exactly 256
 // columns (x0 = 256 * strip): every lane loads and stores one aligned 16-B
 // quad per row (the linear copy's request shape), and the four columns a strip

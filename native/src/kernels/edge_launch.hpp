@@ -214,33 +214,6 @@ int launch_tiled(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
         in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
 }
 
-// 16-B-lane separable kernel (conv_wave4_kernel, tuning variant only): 248
-// output columns per wave strip; seg <= 0 sizes the segments for one resident
-// round of kWave4PerSimd waves per SIMD (at least 8 rows each). Measured on
-// MI355X (tools/kbench.py, sobel5 4096^2): best 25.6 us at 24-row segments,
-// no faster than the 8-B-lane production kernel (25.7 us) — the separable
-// kernel is issue-bound, and 4 pixels per lane cost 89 VGPRs (5 waves/SIMD).
-inline constexpr int kWave4PerSimd = 4;
-template <int K, int A, int MODE, bool FAST, class F, int PF = 4>
-int launch_wave4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
-                 const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kWave4PerSimd) {
-    constexpr int OW = 248;
-    if (!rs.up) rs.up = in;
-    if (!rs.dn) rs.dn = in;
-    const int strips = (w + OW - 1) / OW;
-    if (seg <= 0) {
-        const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
-        const int64_t work = (int64_t)(oy1 - oy0) * strips;
-        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
-    }
-    const int segs = (oy1 - oy0 + seg - 1) / seg;
-    const int64_t nwaves = (int64_t)strips * segs;
-    MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
-    hipLaunchKernelGGL((edge::conv_wave4_kernel<K, A, MODE, FAST, F, PF>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256),
-                       0, s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, segs, (int)nwaves, strips, taps, rs);
-    return MPX_OK;
-}
-
 template <class F, int K>
 inline bool same_sep_taps(const Taps &t, bool two) {
     auto eq = [](float a, float b) { return __builtin_bit_cast(uint32_t, a) == __builtin_bit_cast(uint32_t, b); };

@@ -261,14 +261,6 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
             return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps, 2>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
         return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5Taps, 0>(in, out, w, w, 0, h, 0, h - 1, tp, s, p1, edge::RowSrc{}, per);
     }
-    if (kind == 5) {
-        // 16-B-lane separable sobel5 (conv_wave4_kernel): p1 = segment rows (0 = auto),
-        // p2 = waves per SIMD the auto segments target (0 = production default)
-        MPX_CHECK_ARG(k == 5 && p1 >= 0 && w % 4 == 0 && aligned16(in) && aligned16(out), "wave4 variant: k = 5, w % 4 == 0");
-        const Taps st = make_taps(k, wx, wy, true, true);
-        return edgel::launch_wave4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(
-            in, out, w, w, 0, h, 0, h - 1, st, s, p1, edge::RowSrc{}, p2 > 0 ? p2 : edgel::kWave4PerSimd);
-    }
     const Taps taps = make_taps(k, wx, wy, true);
     if (kind == 1 || kind == 2) {
         // kind 1: runtime taps, kind 2: compiled-in taps of the named filter;

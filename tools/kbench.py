@@ -99,10 +99,6 @@ def main():
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
             (lambda seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 1000, 1,
                                                               swx, swy, 0))), sref)
-    for seg, per in ((0, 0), (0, 3), (0, 5), (0, 6), (8, 0), (12, 0), (16, 0), (24, 0), (32, 0)):
-        variants[f"sobel5-sep/wave4/seg{seg}/w{per}"] = (
-            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 5, seg,
-                                                                       per, 1, swx, swy, 0))), sref)
     for seg, per in ((0, 0), (0, 2000), (24, 2000), (0, 18000)):
         # 18000: no apron loads — a cost probe whose strip edges are wrong (no reference check)
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
