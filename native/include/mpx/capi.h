@@ -84,6 +84,10 @@ int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0
                     int y_hi, int k, int anchor, int mode, const float *wx, const float *wy,
                     void *stream);
 
+/* Minimum image size in pixels for the band kernel (smaller aligned images take
+ * the wave kernel); returns the previous value, n < 0 only queries. */
+long long mpx_conv_set_band_min(long long n);
+
 /* Tuning-harness entry (tools/kbench.py): kernel variants for k in {2, 5}, MAG2,
  * whole image. kind 0 = LDS streaming kernel (p1 = rows per wave 4/8/16,
  * p2 = tiles per workgroup, 0 = auto); kind 1 = wave-streaming kernel

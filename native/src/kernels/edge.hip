@@ -182,3 +182,10 @@ extern "C" int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pit
     return mpx::conv_impl(in, out, w, pitch, oy0, oy1, y_lo, y_hi, k, anchor, mode, wx, wy, stream, true);
 }
 
+
+// Minimum image size (pixels) for the band kernel; returns the previous value.
+// n < 0 only queries. Tests set 0 to run the band kernel on small images.
+extern "C" long long mpx_conv_set_band_min(long long n) {
+    if (n < 0) return mpx::edgel::g_band_min_pixels.load();
+    return mpx::edgel::g_band_min_pixels.exchange(n);
+}

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "edge_kernels.hpp"
@@ -156,8 +157,17 @@ inline int band_mode() {
     }();
     return v;
 }
-inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs) {
-    return band_mode() != 0 && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
+// Small images (below kBandMinPixels) keep the wave kernel: with one resident
+// round of 16-row segments a 1-Mpx image is only a few hundred waves, and the
+// reference harness's cold single launches on its 0.5-2 Mpx images measured
+// 19.1 us with the band kernel vs 15.2 us with the wave kernel (lab2 large
+// bucket median, tools/gpu_r2_same_method.sh).
+// mpx_conv_set_band_min() moves the threshold (tests cover the band kernel's
+// strip edges on small images).
+inline constexpr int64_t kBandMinPixels = int64_t(1) << 22;
+inline std::atomic<int64_t> g_band_min_pixels{kBandMinPixels};
+inline bool band_ok(const uint32_t *in, const uint32_t *out, int w, int pitch, const edge::RowSrc &rs, int rows) {
+    return band_mode() != 0 && (int64_t)w * rows >= g_band_min_pixels.load(std::memory_order_relaxed) && w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out) &&
            (!rs.up || aligned16(rs.up)) && (!rs.dn || aligned16(rs.dn));
 }
 
@@ -191,7 +201,7 @@ int launch_named(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     if constexpr (F::kK == K && F::kA == A && F::kMode == MODE) {
         if (same_taps<F, K * K>(taps)) {
             if constexpr (kBandFits<K, A>)
-                if (band_ok(in, out, w, pitch, rs))
+                if (band_ok(in, out, w, pitch, rs, oy1 - oy0))
                     return launch_band<K, A, MODE, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
             return launch_wave<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
         }
@@ -200,7 +210,7 @@ int launch_named(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
         return launch_named<K, A, MODE, More...>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, rs);
     } else {
         if constexpr (kBandFits<K, A>)
-            if (band_ok(in, out, w, pitch, rs))
+            if (band_ok(in, out, w, pitch, rs, oy1 - oy0))
                 return launch_band<K, A, MODE, edge::RuntimeTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);
         return launch_wave<K, A, MODE, true>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, vec, s, kSegRows, kWaveOrder, rs);
     }
@@ -237,7 +247,7 @@ int launch_sep(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int
     constexpr int seg = MODE == MPX_CONV_MAG2 ? 0 : kSegRows;
     constexpr int order = MODE == MPX_CONV_MAG2 ? kWaveOrderAlt : kWaveOrder;
     constexpr bool fits = kBandFits<K, A>;
-    const bool band = fits && band_ok(in, out, w, pitch, rs);
+    const bool band = fits && band_ok(in, out, w, pitch, rs, oy1 - oy0);
     if constexpr (K == 5 && A == 2 && MODE == MPX_CONV_MAG2) {
         if (band && same_sep_taps<edge::Sobel5SepTaps, 5>(taps, true))
             return launch_band<K, A, MODE, edge::Sobel5SepTaps>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, rs);

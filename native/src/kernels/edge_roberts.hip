@@ -182,7 +182,7 @@ int roberts_impl(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by
     if (bx == 0 && by == 0 && gx == 0 && gy == 0) {  // tuned path: wave kernel with compiled-in Roberts taps
         const Taps taps = edgel::make_taps(2, kRobertsX, kRobertsY, true);
         const bool vec2 = (w % 2 == 0) && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7u) == 0;
-        const int rc = edgel::band_ok(in, out, w, w, edge::RowSrc{})
+        const int rc = edgel::band_ok(in, out, w, w, edge::RowSrc{}, h)
                            ? edgel::launch_band<2, 0, MPX_CONV_MAG2, RobertsTuned>(in, out, w, w, 0, h, 0, h - 1, taps,
                                                                                    as_stream(stream), edge::RowSrc{})
                            : edgel::launch_wave<2, 0, MPX_CONV_MAG2, true, RobertsTuned>(in, out, w, w, 0, h, 0, h - 1,

@@ -61,13 +61,24 @@ def test_conv_matches_cpu_exact_and_torch(gpu, filt, hw):
 @pytest.mark.parametrize("filt", ["roberts", "sobel3", "sobel5", "gauss5", "log5", "sobel5_dense"])
 @pytest.mark.parametrize("w", [4, 8, 252, 256, 260, 512, 516, 1028])
 def test_conv_band_kernel_strip_edges(gpu, filt, w):
-    """Aligned widths take the band kernel (256-column strips, 8-B aprons at the
-    strip edges, clamp-to-edge by the lane's own pixel at x = 0 and x = w):
-    partial strips, exactly one strip, one lane, every segment height."""
+    """The band kernel (256-column strips, 8-B aprons at the strip edges,
+    clamp-to-edge by the lane's own pixel at x = 0 and x = w), forced onto small
+    aligned images: partial strips, exactly one strip, one lane, every segment
+    height; then the default size threshold (wave kernel) gives the same bytes."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
     f = ops.get_filter(filt)
-    for h in (1, 2, 5, 17, 33, 70):
-        img = rand_img(h, w, seed=w + h)
-        assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f)), (h, w)
+    old = L.mpx_conv_set_band_min(0)
+    try:
+        for h in (1, 2, 5, 17, 33, 70):
+            img = rand_img(h, w, seed=w + h)
+            assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f)), (h, w)
+    finally:
+        L.mpx_conv_set_band_min(old)
+    assert old >= 1 << 20
+    img = rand_img(33, w, seed=w)
+    assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f))
 
 
 @pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "sharpen3", "sobel5_dense",

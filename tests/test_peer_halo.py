@@ -34,10 +34,14 @@ def _img(h, w, seed):
     return torch.randint(0, 256, (h, w, 4), dtype=torch.uint8, generator=g)
 
 
-def _peer_worker(rank, world, port, h, w, filt, errq):
+def _peer_worker(rank, world, port, h, w, filt, errq, band=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank))
+        if band:  # the band kernel on these small slabs (its halo rows then come over IPC)
+            from cuda_mpi_openmp_amd import _native
+
+            _native.lib().mpx_conv_set_band_min(0)
         ctx = parallel.init(device="cuda", backend="gloo")
         det = SlabEdgeDetector(ctx, h, w, filt, halo="peer")
         assert det.transport == "xgmi-peer", det.transport
@@ -132,6 +136,16 @@ def _run_ranks(target, world, *args, timeout=240, **kwargs):
 def test_peer_halo_ranks_share_one_gpu(gpu, world, filt):
     h = 301 if world <= 3 else 8 * 37 + 5  # 8k+5: uneven slabs at 4 and 8 ranks
     _run_ranks(_peer_worker, world, h, 258, filt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (4, "sobel3"), (8, "sobel5_dense")])
+def test_peer_halo_band_kernel(gpu, world, filt):
+    """Aligned width (260 = one full 256-column strip + a partial one): the band
+    kernel reads its neighbours' halo rows over IPC (RowSrc), boundary segments
+    dispatched first."""
+    h = 301 if world <= 3 else 8 * 37 + 5
+    _run_ranks(_peer_worker, world, h, 260, filt, band=True)
 
 
 @pytest.mark.gpu
