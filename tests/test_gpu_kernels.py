@@ -270,9 +270,11 @@ def test_classify_single_point_class_nan(gpu):
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-# (2413, 4096) / (4822, 4096): enough waves for the production 5 rows per wave
-# (fp64 / fp32), with a 3- / 2-row tail in the last wave of each strip
-@pytest.mark.parametrize("shape", [(3, 3), (10, 7), (66, 130), (257, 1001), (2413, 4096), (4822, 4096)])
+# (2413, 4096) / (4822, 4096): 4 rows per wave (fp64) / 8 (fp32) with tails;
+# (1003, 16384): the production 8 rows per wave, odd row blocks walking up, and
+# a 3-row tail in a bottom block that walks up (125 full blocks + 3 rows)
+@pytest.mark.parametrize("shape", [(3, 3), (10, 7), (66, 130), (257, 1001), (2413, 4096), (4822, 4096),
+                                   (1003, 16384)])
 def test_jacobi_sweep(gpu, dtype, shape):
     rows, cols = shape
     g = torch.Generator().manual_seed(rows)
