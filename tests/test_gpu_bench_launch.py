@@ -24,3 +24,16 @@ def test_bench_self_launch_two_ranks_peer(gpu):
     assert rec["verified_bit_exact"] is True and rec["verified_pixels"] == 2 * 2 * 512 * 512
     assert rec["config"]["transport"] == "xgmi-peer"
     assert len(rec["per_rank_ms_per_step"]) == 2
+
+
+@pytest.mark.parametrize("workload,extra", [("vsub", ["--elems", str(1 << 20)]), ("classify", ["--size", "512"])])
+def test_bench_workloads_two_ranks(gpu, workload, extra):
+    """lab1 / lab3 weak-scaling jobs of tools/scale.py, two ranks rehearsed on the
+    one GPU: every rank's output verified."""
+    env = dict(os.environ, MPX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_workloads.py"), "--workload", workload,
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", *extra],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 2 and rec["verified"] is True and len(rec["per_rank_ms"]) == 2
