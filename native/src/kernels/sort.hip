@@ -7,29 +7,32 @@
 //   * int32 and float32 become order-preserving uint32 keys (sign flip; floats
 //     flip every bit when negative). Float order is the IEEE total order on the
 //     bit patterns: -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN.
-//   * n > kTile: LSD radix sort, 8-bit digits, 4 passes, onesweep style:
-//       - one histogram pass builds all four 256-bin digit histograms at once
-//         (LDS atomics per block, one global atomic per bin and block);
-//       - each digit pass is ONE kernel: a block takes the next 8192-key tile
-//         from an atomic tile counter, ranks its keys stably in LDS (per-wave
-//         peer masks of equal digits from an LDS OR table, mbcnt for the rank
-//         among lower lanes, per-wave digit counters), publishes its 256 digit counts and
-//         resolves its global digit offsets by decoupled look-back over the
-//         preceding tiles (flag + count packed in one 32-bit word, so a single
-//         relaxed agent-scope store publishes both), then stages the tile in
-//         LDS in digit order and writes it out in runs per digit;
-//       - the key transform rides on the first pass's loads and the inverse
-//         on the last pass's stores; 4 passes ping-pong data -> ws -> data.
-//     Traffic: 1 read (histogram) + 4 x (read + write) of the array, no
-//     compare network. Tile ids are taken in launch order, so a block only
-//     ever waits on tiles whose blocks are already resident.
+//   * n > kTile: LSD radix sort, 8-bit digits, 4 passes (radix_sort32), in
+//     one of two forms chosen by n:
+//       - n <= kOnesweepMaxN (2^18), onesweep: one histogram pass builds all
+//         four 256-bin digit histograms at once; each digit pass is ONE kernel
+//         in which a block takes the next 8192-key tile from an atomic tile
+//         counter, ranks its keys stably in LDS (per-wave peer masks of equal
+//         digits from an LDS OR table, mbcnt for the rank among lower lanes,
+//         per-wave digit counters), resolves its global digit offsets by
+//         decoupled look-back (flag + count in one 32-bit word), then stages
+//         the tile in LDS in digit order and writes it out in runs per digit;
+//       - larger n, reduce-then-scan: per pass a count kernel (per-tile digit
+//         counts), a scan kernel (per-tile offsets and digit totals) and a
+//         persistent scatter kernel (2 blocks per CU walking XCD-local tiles,
+//         next tile prefetched while this one is ranked as above). It
+//         re-reads each tile once more but never waits on a look-back chain,
+//         whose cross-XCD round trips bound onesweep at large n.
+//     The key transform rides on the first pass's loads and the inverse on
+//     the last pass's stores; 4 passes ping-pong data -> ws -> data.
 //   * n <= kTile (4096 keys): the whole bitonic network in LDS, one launch;
-//     n >= 2^30 (beyond the 30-bit look-back counts): the global bitonic
-//     network (stages > kTile as fused global half-cleaner passes).
-//   * uint8 uses a counting sort: 256 LDS histogram bins per block stored to a
-//     per-block row (no global atomics), one block reduces the rows and scans
-//     them into 257 bucket starts, and every block writes its output range by
-//     binary search over those starts staged in LDS.
+//     n >= 2^30 (beyond the 30-bit counts): the global bitonic network
+//     (stages > kTile as fused global half-cleaner passes, up to 3 per pass).
+//   * uint8 uses a counting sort: a per-block LDS histogram folded into 256
+//     global bin counts by one atomic per bin and block (hist_u8_kernel), then
+//     every block scans the 256 counts itself and writes its 16-B pieces of
+//     the output, each piece's value found by binary search over the bucket
+//     starts in LDS (fill_u8_kernel).
 //   * Scratch comes from a caller-provided workspace (mpx_sort_workspace_bytes
 //     / mpx_sort_ws): the Python op takes it from torch's caching allocator on
 //     the tensor's stream, so concurrent sorts on different streams or devices
