@@ -831,8 +831,16 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const uint32_t *row = row_ptr(i);
         const __amdgpu_buffer_rsrc_t rr =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, w * 4, 0x00020000);
-        const u32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 0);
-        ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, 0);
+        u32x4_t q;
+        // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
+        // non-temporal; bit 6: every row does (probes)
+        if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 2);
+            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, (OPT & 128) ? 0 : 2);
+        } else {
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 0);
+            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
         return q;
     };
@@ -978,7 +986,9 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // OPT (tuning variants): bit 0 caps registers for 5 waves per SIMD, bit 1
 // non-temporal output stores, bit 2 16-wave workgroups (a band row's 16 strips
 // of a 4096-wide image on one CU), bit 4 no apron loads (cost probe: wrong
-// results at the strip edges).
+// results at the strip edges), bit 5 non-temporal loads of rows no neighbouring
+// segment reads, bit 6 non-temporal loads of every row, bit 7 keeps the apron
+// loads plain under bit 5 / 6.
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,

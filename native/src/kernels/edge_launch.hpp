@@ -148,12 +148,15 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // rows) are 16-B aligned, with non-temporal output stores. MI355X 4096^2, 6
 // rotated pairs (tools/kbench.py, µs): sobel5 separable 28.9 (30.3 with the
 // 8-B-lane wave kernel; 29.4 with plain stores), sobel5_dense 32.7 (41.4),
-// Roberts 27.8 (30.4). MPX_CONV_BAND=0: wave kernel, 1: band kernel with plain
-// stores (same-box A/B); read once per process.
+// Roberts 27.8 (30.4). Default (2): NT stores, plain loads. MPX_CONV_BAND=0:
+// wave kernel, 1: band kernel with plain stores, 3: NT stores + non-temporal
+// loads of the rows no neighbouring segment re-reads (three same-box runs:
+// -2.8% / +2% / -1% on sobel5, sobel5_dense +6%: no stable gain, not the
+// default); read once per process.
 inline int band_mode() {
     static const int v = [] {
         const char *e = std::getenv("MPX_CONV_BAND");
-        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
     }();
     return v;
 }
@@ -179,7 +182,9 @@ int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
                 const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
     if (band_mode() == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-    return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+    if (band_mode() == 2)
+        return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+    return launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
 }
 
 // Named filters whose taps are compiled in (zero taps disappear); selected
