@@ -35,6 +35,7 @@
 //     replaced by the class index): best = min(best, key), second =
 //     med3(best, key, second). A bias folded into the constant weight makes
 //     every computed value positive, so unsigned key order is value order.
+#include <algorithm>
 #include <cstdlib>
 
 #include "internal.hpp"
@@ -701,9 +702,12 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         }();
         const int64_t nvec = npix / (4 * nq);
         if (nvec > 0) {
-            const int blk = block > 0 ? block : 256;
+            // the kernel is compiled for 256-thread workgroups
+            // (__launch_bounds__(256)): a larger caller block would not launch
+            // ("unspecified launch failure"), so it is capped
+            const int blk = block > 0 ? std::min(block, 256) : 256;
             const int64_t blocks = (nvec + blk - 1) / blk;
-            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            const int g = grid > 0 ? (int)useful_grid(grid, nvec, blk) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
             if (nq == 2)
                 hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             else
@@ -721,6 +725,9 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         if (g == 0 || chosen != MPX_CLS_DIRECT) {
             int64_t want = (n / 4 + blk - 1) / blk;
             g = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)kNumCUs * 8));
+        } else {
+            // caller geometry: thread t handles vector t (or pixel t) and tail pixel t
+            g = (int)useful_grid(g, vec ? std::max<int64_t>(n / 4, 4) : n, blk);
         }
         hipLaunchKernelGGL(classify_direct_kernel, dim3(g), dim3(blk), 0, s, rest, n, nc, cp, vec);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());

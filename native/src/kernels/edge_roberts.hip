@@ -197,7 +197,17 @@ int roberts_impl(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by
     const int VEC = vec ? 4 : 1;
     const size_t lds = sizeof(float) * (size_t)(by + 1) * (size_t)(VEC * bx + 4);
     MPX_CHECK_ARG(lds <= 64 * 1024, "tile does not fit the 64 KiB per-workgroup LDS limit");
+    // empty workgroups dropped (useful_grid): a block whose first tile column
+    // (row) lies past the image owns none, and with gx >= tiles_x every block
+    // owns exactly its own column either way. Tiles: (4 bx) x by pixels in the
+    // vector and thin kernels, bx x by in the scalar LDS kernel.
+    // The kernel is chosen from the caller's geometry before the clamp.
     const bool thin = (int64_t)bx * by * gx * gy < 16384;
+    {
+        const int64_t tw = (vec || thin) ? 4 * bx : bx;
+        gx = (int)useful_grid(gx, (w + tw - 1) / tw, 1);
+        gy = (int)useful_grid(gy, (h + by - 1) / by, 1);
+    }
     if (thin && vec)
         hipLaunchKernelGGL((roberts_thin_kernel<8, true>), dim3(gx, gy), dim3(bx, by), 0, as_stream(stream), in, out, w, h);
     else if (thin)

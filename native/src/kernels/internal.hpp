@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "mpx/capi.h"
@@ -59,5 +60,27 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     const void *module_anchor_##tag() { return reinterpret_cast<const void *>(&module_anchor_##tag##_kernel); }
 
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Caller launch geometries (the harness's [grid, block] sweeps) drive
+// grid-stride kernels in which a workgroup whose first item lies past the
+// work owns nothing: with grid >= ceil(items / per_block) every thread handles
+// at most its own first item, so launching only ceil(items / per_block)
+// workgroups gives every thread the same items and the same stride-free walk
+// — only the empty workgroups are dropped (a [[16,16],[1024,1024]] Roberts
+// launch on a 0.3 Mpx image is 1M workgroups of which 256 own a tile).
+// MPX_GEOM_LITERAL=1 launches the caller's grid as given (A/B, and the
+// reference methodology's literal launch); read once per process.
+inline bool geom_literal() {
+    static const bool v = [] {
+        const char *e = std::getenv("MPX_GEOM_LITERAL");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+inline int64_t useful_grid(int64_t grid, int64_t items, int64_t per_block) {
+    if (geom_literal() || grid <= 0 || per_block <= 0) return grid;
+    const int64_t need = items <= 0 ? 1 : (items + per_block - 1) / per_block;
+    return grid < need ? grid : need;
+}
 
 }  // namespace mpx

@@ -120,6 +120,13 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
         grid = (int)(g < 1 ? 1 : (g > cap ? cap : g));
     }
     if (block == 0) block = 256;
+    // empty workgroups of an oversized caller grid dropped (useful_grid): the
+    // vector kernel's thread t handles vector t and tail element t; the scalar
+    // kernel element t
+    {
+        const int64_t items = vec ? std::max<int64_t>(n / Vec16<T>::n, Vec16<T>::n) : n;
+        grid = (int)useful_grid(grid, items, block);
+    }
     const bool thin = (int64_t)grid * block < 16384;
     if (vec && thin)
         hipLaunchKernelGGL((vsub_vec_kernel<T, 8>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);

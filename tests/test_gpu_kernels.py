@@ -195,6 +195,53 @@ def test_classify_matches_cpu(gpu, nc, path):
     assert (t[..., 3] != cpu[..., 3]).float().mean() < 1e-3  # torch's summation order differs on near-ties
 
 
+@pytest.mark.parametrize("path", ["direct", "fast"])
+@pytest.mark.parametrize("geom", [(1024, 1024), (4096, 64), (3, 32), (1, 1)])
+def test_classify_oversized_geometry(gpu, path, geom):
+    """Caller grids far larger than the work: the empty workgroups are not
+    launched (useful_grid), and the result equals the CPU reference either way."""
+    img = smooth_img(37, 53, seed=5)  # 1961 pixels: vector body + 1-pixel tail
+    mu, inv = ops.class_stats(img, _random_classes(img, 5, 20, 5))
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    d = img.to(gpu)
+    ops.classify_(d, mu, inv, path=path, grid=geom[0], block=geom[1])
+    assert torch.equal(d.cpu(), cpu)
+
+
+@pytest.mark.parametrize("hw", [(7, 9), (300, 301), (1000, 1003), (1000, 1004)])
+@pytest.mark.parametrize("geom", [((16, 16), (1024, 1024)), ((3, 5), (700, 900)), ((64, 4), (2, 4096))])
+def test_roberts_oversized_geometry(gpu, hw, geom):
+    """Grids with more blocks than tiles (scalar and 16-B kernels)."""
+    img = smooth_img(*hw, seed=hw[1])
+    assert torch.equal(ops.roberts(img.to(gpu), geometry=geom).cpu(), ops.roberts(img))
+
+
+def test_geometry_literal_launch_matches(gpu, tmp_path):
+    """MPX_GEOM_LITERAL=1 (the caller's grid as given) produces the same bytes
+    as the default launch with the empty workgroups dropped."""
+    import subprocess
+    import sys
+    code = (
+        "import torch, sys\n"
+        "from cuda_mpi_openmp_amd import ops\n"
+        "from tests.helpers import smooth_img\n"
+        "img = smooth_img(300, 301, seed=3)\n"
+        "a = torch.arange(1003, dtype=torch.float64); b = torch.ones(1003, dtype=torch.float64)\n"
+        "r = ops.roberts(img.cuda(), geometry=((16, 16), (1024, 1024))).cpu()\n"
+        "v = ops.vsub(a.cuda(), b.cuda(), grid=1024, block=1024).cpu()\n"
+        "torch.save({'r': r, 'v': v}, sys.argv[1])\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for lit in ("0", "1"):
+        p = tmp_path / f"o{lit}.pt"
+        env = dict(os.environ, MPX_GEOM_LITERAL=lit, PYTHONPATH=root)
+        subprocess.run([sys.executable, "-c", code, str(p)], check=True, cwd=root, env=env, timeout=120)
+        outs.append(torch.load(p, weights_only=True))
+    assert torch.equal(outs[0]["r"], outs[1]["r"]) and torch.equal(outs[0]["v"], outs[1]["v"])
+    assert torch.equal(outs[0]["v"], torch.arange(1003, dtype=torch.float64) - 1)
+
+
 @pytest.mark.parametrize("path", CLS_PATHS)
 def test_classify_random_pixels_and_fallback_rate(gpu, path):
     """Uniform random pixels (the bench's input): identical classes; the exact
