@@ -14,10 +14,12 @@ CC        ?= gcc
 ARCH      ?= gfx950
 
 INC       := -Inative/include -I$(ROCM)/include
+# warnings are errors (-Wall -Werror); make WERROR= to relax
+WERROR    ?= -Werror
 HIPFLAGS  := --offload-arch=$(ARCH) -mcode-object-version=5 -O3 -std=c++17 -fPIC \
-             -ffp-contract=off -Wall -Wno-unused-function $(INC)
-COPT      := -O3 -fopenmp -ffp-contract=off -fPIC -Wall -std=gnu11 -Inative/include
-CSER      := -O0 -ffp-contract=off -Wall -Wno-unknown-pragmas -std=gnu11 -Inative/include
+             -ffp-contract=off -Wall -Wno-unused-function $(WERROR) $(INC)
+COPT      := -O3 -fopenmp -ffp-contract=off -fPIC -Wall $(WERROR) -std=gnu11 -Inative/include
+CSER      := -O0 -ffp-contract=off -Wall -Wno-unknown-pragmas $(WERROR) -std=gnu11 -Inative/include
 
 B         := build
 PYLIB     := cuda_mpi_openmp_amd/_lib/libmpx.so
