@@ -834,7 +834,9 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
         // non-temporal; bit 6: every row does (probes)
-        if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
+        if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, (OPT & 64) ? 2 : 0);
+        } else if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 2);
             ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, (OPT & 128) ? 0 : 2);
         } else {
@@ -847,6 +849,19 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     auto fix_quad = [&](u32x4_t q) -> u32x4_t {
         return q_right ? u32x4_t{q.w, q.w, q.w, q.w} : q;
     };
+    // OPT bit 3 (walks of at most 32 rows): every apron of the walk in ONE
+    // load up front instead of one 8-B load per row. Lane j holds walk row
+    // j >> 1's left (j even) or right (j odd) apron as two luma values; row
+    // i's consumer reads lanes 2i / 2i+1 with v_readlane (wave-uniform i).
+    f2_t ab = {0.0f, 0.0f};
+    if constexpr ((OPT & 8) != 0) {
+        const int nload = ye - ys + K - 1;  // <= 32, checked by the launcher
+        const int j = lane >> 1, side = lane & 1;
+        const bool have = !(OPT & 16) && (side ? x0 + 256 < w : x0 > 0);
+        const uint32_t *row = row_ptr(min(j, nload - 1));
+        const u32x2_t v = *reinterpret_cast<const u32x2_t *>(row + (have ? (side ? x0 + 256 : x0 - 2) : 0));
+        ab = luma2(v.x, v.y);
+    }
 
     // prefetch ring of D >= 4 rows, a multiple of K (compile-time slots when
     // the row loop is unrolled D times)
@@ -857,11 +872,21 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     float win[SEP ? 1 : K][NV];                      // dense: per-row luminance windows
     uint32_t alp[K];
 
-    auto consume = [&](int u, u32x4_t px, u32x2_t ap) {
+    auto consume = [&](int u, u32x4_t px, u32x2_t ap, int ri) {
         const f2_t l01 = luma2(px.x, px.y), l23 = luma2(px.z, px.w);
         alp[u] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px.w, px.z, 0x07030000u),
                                        __builtin_amdgcn_perm(px.y, px.x, 0x07030000u), 0x07060302u);
-        const f2_t la = luma2(ap.x, ap.y);
+        f2_t la;
+        if constexpr ((OPT & 8) != 0) {
+            auto rl = [&](float x, int l) {
+                return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+            };
+            const f2_t lft = {rl(ab.x, 2 * ri), rl(ab.y, 2 * ri)};
+            const f2_t rgt = {rl(ab.x, 2 * ri + 1), rl(ab.y, 2 * ri + 1)};
+            la = ap_left ? lft : rgt;
+        } else {
+            la = luma2(ap.x, ap.y);
+        }
         float wv[NV];
         wv[A + 0] = l01.x;
         wv[A + 1] = l01.y;
@@ -903,7 +928,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const u32x4_t px = fix_quad(pre[u]);
         const u32x2_t ap = apr[u];
         pre[u] = load_row(u + D, apr[u]);
-        consume(u, px, ap);
+        consume(u, px, ap, u);
     }
     auto row_step = [&](int g, int v) {
         const int u = (K - 1 + v) % K;
@@ -912,7 +937,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const u32x4_t px = fix_quad(pre[q]);
         const u32x2_t ap = apr[q];
         pre[q] = load_row(i + D, apr[q]);
-        consume(u, px, ap);
+        consume(u, px, ap, i);
         const int y = UP ? ye - 1 - (g * D + v) : ys + g * D + v;
         auto slot = [&](int dy) { return UP ? (u + K - dy) % K : (u + 1 + dy) % K; };
         uint32_t gray[4];
@@ -988,7 +1013,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // of a 4096-wide image on one CU), bit 4 no apron loads (cost probe: wrong
 // results at the strip edges), bit 5 non-temporal loads of rows no neighbouring
 // segment reads, bit 6 non-temporal loads of every row, bit 7 keeps the apron
-// loads plain under bit 5 / 6.
+// loads plain under bit 5 / 6, bit 3 one batched apron load per walk (walks of
+// at most 32 rows: segment + K - 1 <= 32).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,

@@ -133,6 +133,7 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
         const int64_t work = (int64_t)(oy1 - oy0) * strips;
         seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
     }
+    MPX_CHECK_ARG(!(OPT & 8) || seg + K - 1 <= 32, "batched aprons: walks of at most 32 rows");
     const int segs = (oy1 - oy0 + seg - 1) / seg;
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");

@@ -241,7 +241,7 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
     case O:                                                                                                   \
         return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, O>(in, out, w, w, 0, h, 0, h - 1, st, s, \
                                                                                       p1, edge::RowSrc{}, per, alt);
-            MPX_BAND4(0) MPX_BAND4(1) MPX_BAND4(2) MPX_BAND4(3) MPX_BAND4(6) MPX_BAND4(18) MPX_BAND4(34) MPX_BAND4(66) MPX_BAND4(162)
+            MPX_BAND4(0) MPX_BAND4(1) MPX_BAND4(2) MPX_BAND4(3) MPX_BAND4(6) MPX_BAND4(18) MPX_BAND4(34) MPX_BAND4(66) MPX_BAND4(162) MPX_BAND4(10) MPX_BAND4(11)
 #undef MPX_BAND4
         }
         set_error("unsupported band OPT %d", p2 / 1000);
