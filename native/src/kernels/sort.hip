@@ -564,7 +564,10 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
         for (int e = 0; e < kRPer; ++e)  // pads (past n) rank last and are never stored
             key[e] = tile0 + w * kRWaveKeys + lane + e * 64 < n ? to_key(raw[e], in_mode) : 0xffffffffu;
-        constexpr int kRG = 4;
+#ifndef MPX_SORT_RG  // slices ranked per batch (A/B builds override)
+#define MPX_SORT_RG 4
+#endif
+        constexpr int kRG = MPX_SORT_RG;
 #pragma unroll
         for (int g = 0; g < kRPer; g += kRG) {
             uint64_t m[kRG];
