@@ -29,9 +29,11 @@ template <typename V> __device__ __forceinline__ V vsub(V a, V b) { return a - b
 // grid-stride step: 4 for launches that fill the GPU, 8 for "thin" harness
 // geometries ([1, 32], [4, 64] ...: a few waves streaming a whole vector are
 // latency-bound, and only loads in flight per lane help them)
-template <typename T, int kUnroll>
-__global__ void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ c,
-                                int64_t n) {
+// LB: workgroup-size bound; the 16-deep thin form is compiled for <= 256
+// threads, which lifts the 128-VGPR cap of a 1024-thread bound (no spills)
+template <typename T, int kUnroll, int LB = 1024>
+__global__ __launch_bounds__(LB) void vsub_vec_kernel(const T *__restrict__ a, const T *__restrict__ b, T *__restrict__ c,
+                                                      int64_t n) {
     using V = typename Vec16<T>::type;
     constexpr int kV = Vec16<T>::n;
     const int64_t nvec = n / kV;
@@ -128,7 +130,16 @@ int launch_vsub(const T *a, const T *b, T *c, int64_t n, int grid, int block, vo
         grid = (int)useful_grid(grid, items, block);
     }
     const bool thin = (int64_t)grid * block < 16384;
-    if (vec && thin)
+    // very thin ([1, 32] .. [4, 64]: at most one wave per CU): 16 vectors in
+    // flight per operand — each lane walks thousands of vectors, so the
+    // round trips, not the issue, bound it
+    // (measured on MI355X, n = 10^6 fp64: [1, 32] 1383 -> 915 us, [4, 64] 151
+    // -> 113 us vs 8 deep; 32 deep is slower again, 1380 us: 64 loads exceed
+    // the 63 a wave's vmcnt can track, so the loop waits every trip)
+    const bool very_thin = (int64_t)grid * block <= 2048 && block <= 256;
+    if (vec && very_thin)
+        hipLaunchKernelGGL((vsub_vec_kernel<T, 16, 256>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
+    else if (vec && thin)
         hipLaunchKernelGGL((vsub_vec_kernel<T, 8>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
     else if (vec)
         hipLaunchKernelGGL((vsub_vec_kernel<T, 4>), dim3(grid), dim3(block), 0, as_stream(stream), a, b, c, n);
