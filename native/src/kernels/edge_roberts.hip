@@ -141,17 +141,28 @@ __global__ void roberts_thin_kernel(const uint32_t *__restrict__ in, uint32_t *_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (j0 + u >= ntiles || y[u] >= h || xs[u] >= w) continue;
+            // packed fp32 (v_pk_mul / v_pk_add): each element takes the same
+            // products and sums as mpx_luma and the scalar magnitude, so the
+            // bytes are unchanged; a wave here often has 4 live lanes, so its
+            // time is instruction issue and the pairs halve it
+            using edge::f2_t;
+            const f2_t la01 = edge::luma2(a[u][0], a[u][1]), la23 = edge::luma2(a[u][2], a[u][3]);
+            const f2_t lb01 = edge::luma2(b[u][0], b[u][1]), lb23 = edge::luma2(b[u][2], b[u][3]);
+            const f2_t l4 = edge::luma2(a[u][4], b[u][4]);  // (row a, row b) at x + 4
             uint32_t res[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float y00 = mpx_luma(a[u][k]), y10 = mpx_luma(a[u][k + 1]);
-                const float y01 = mpx_luma(b[u][k]), y11 = mpx_luma(b[u][k + 1]);
-                const float gxv = y11 - y00;
-                const float gyv = y10 - y01;
-                const float s0 = gxv * gxv;
-                const float s1 = gyv * gyv;
-                res[k] = mpx_px_gray(edge::mag_to_gray<true>(s0 + s1), mpx_px_a(a[u][k]));  // == trunc(sqrtf), see mag_to_gray
-            }
+            auto pair = [&](f2_t y00, f2_t y10, f2_t y01, f2_t y11, int k) {
+                const f2_t gxv = y11 - y00;
+                const f2_t gyv = y10 - y01;
+                const f2_t s0 = gxv * gxv;
+                const f2_t s1 = gyv * gyv;
+                const f2_t sq = s0 + s1;
+                uint32_t g0, g1;
+                edge::mag2_to_gray(sq.x, sq.y, g0, g1);  // == trunc(sqrtf) each, see mag2_to_gray
+                res[k] = mpx_px_gray(g0, mpx_px_a(a[u][k]));
+                res[k + 1] = mpx_px_gray(g1, mpx_px_a(a[u][k + 1]));
+            };
+            pair(la01, f2_t{la01.y, la23.x}, lb01, f2_t{lb01.y, lb23.x}, 0);
+            pair(la23, f2_t{la23.y, l4.x}, lb23, f2_t{lb23.y, l4.y}, 2);
             uint32_t *o = out + (int64_t)y[u] * w + xs[u];
             if (VEC) {
                 *reinterpret_cast<uint4 *>(o) = make_uint4(res[0], res[1], res[2], res[3]);
