@@ -24,7 +24,16 @@ like a stream of distinct frames would. The same K steps on one resident pair
 ``value_warm_cache``.
 
 ``value`` is the whole-job pixel throughput (N * 4096^2 * K / time, max time
-over ranks). Every output pixel of every rotated pair on every rank is
+over ranks).
+
+``value_streaming`` (``--stream``, on by default) times the same K steps with
+an input that changes every step: the filter is iterated (step k convolves
+step k-1's output) over the same rotated working set, so for N > 1 every step
+needs halo rows the neighbours produced in the previous step — ordered on the
+device by a signalled fetch kernel (peer) or by in-order RCCL send/recv.
+Verified after the timed region: the gathered N-rank result of every rotated
+slab equals a one-device whole-image run of the same frame sequence, and each
+rank's last step equals the CPU reference on its halo-filled input. Every output pixel of every rotated pair on every rank is
 compared bit-exactly with the OpenMP CPU reference after the timed region
 (``verified_bit_exact``); the GPU/CPU speedup compares one GPU's per-image
 time with that CPU reference on the same 4096^2 image (``speedup_vs_cpu``).
@@ -50,13 +59,9 @@ sys.path.insert(0, ROOT)
 BASELINE_METRIC = "Gpixel/s lab2 2D conv 4096x4096 + GPU/CPU speedup, at 1/2/4/8 MI355X"
 # best large-bucket Roberts run on the RTX A6000, ~0.78 Mpx / 0.17866 ms
 BASELINE_GPIXEL_PER_S = 4.4
-# Same-methodology comparison (harness, cold single launch per process, lab2
-# large bucket, tuned launch): 0.01520 ms here vs 0.17866 ms published;
-# profiles/harness_vs_baseline.md.
-SAME_METHOD = {"ratio": 11.8, "here_ms": 0.01520, "reference_ms": 0.17866,
-               "ratio_range": [9.1, 11.8],  # two runs on two boxes (cold launches vary by box)
-               "what": "lab2 Roberts, metric_calc/large bucket median, cold launch per process, via run_test.py",
-               "source": "profiles/harness_vs_baseline.md"}
+BASELINE_NOTE = ("estimate: A6000 Roberts 2x2 on a ~0.78 Mpx image, one cold launch (BASELINE.md) vs MI355X "
+                 "5x5 sobel5 on 4096^2 slabs, warm steps streaming from HBM; not like-for-like — the harness's "
+                 "same-methodology comparison is in profiles/harness_vs_baseline.md")
 
 
 def parse_args(argv=None):
@@ -81,6 +86,9 @@ def parse_args(argv=None):
     p.add_argument("--watchdog", type=float, default=None,
                    help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
     p.add_argument("--no-warm", action="store_true", help="skip the cache-resident (single pair) comparison run")
+    p.add_argument("--stream", dest="stream", action="store_true", default=True,
+                   help="also time the streaming (iterated-filter) run: value_streaming (default on)")
+    p.add_argument("--no-stream", dest="stream", action="store_false")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
@@ -144,6 +152,11 @@ def run(args) -> int:
     if args.graph > 0 and ctx.device.type == "cuda" and single_stream:
         from cuda_mpi_openmp_amd.utils.graphs import try_step_graph
 
+        if args.graph % len(dets):
+            # a graph of a partial rotation would replay only a subset of the
+            # pairs and shrink the working set back into the MALL
+            raise SystemExit(f"--graph {args.graph} must be a multiple of --rotate {len(dets)}")
+        cyc[0] = 0
         graph = try_step_graph(rot_step, args.graph, ctx.device)
         sync()
         ctx.barrier()
@@ -192,6 +205,13 @@ def run(args) -> int:
         ok = parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
         checked = int(parallel.all_reduce_sum_host(float(checked), ctx))
 
+    # ---- streaming: the same K steps with a real inter-rank dependency ----
+    stream_rec = None
+    if args.stream:
+        graph = None
+        stream_rec = run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel)
+        ok &= stream_rec.get("verified_bit_exact", True) is not False
+
     watchdog.stop()
     cpu_ms = None
     if ctx.rank == 0 and not args.no_cpu_baseline:
@@ -211,7 +231,7 @@ def run(args) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_GPIXEL_PER_S, 2),
-            "vs_reference_same_method": SAME_METHOD,
+            "vs_baseline_note": BASELINE_NOTE,
             "dtype": "fp32",
             "data": f"synthetic (uniform random RGBA8, {len(dets)} independent {args.size}x{args.size} slabs per GPU "
                     f"cycled by the timed steps)",
@@ -225,6 +245,7 @@ def run(args) -> int:
                                               if d0.pipeline else "+halo-overlap" if d0.overlap else "+halo-inorder")
                                              if n > 1 else ""),
                 "transport": d0.transport if n > 1 else None,
+                "peer_probe": (None if n == 1 or args.halo == "rccl" or ctx.device.type != "cuda" else "ok" if d0.peer is not None else "fallback"),
                 "image_hw": [args.size * n, args.size],
                 "halo_rows": [d0.filter.halo_up, d0.filter.halo_down],
                 "graph_steps": args.graph if graph is not None else 0,
@@ -240,6 +261,8 @@ def run(args) -> int:
         if warm is not None:
             rec["value_warm_cache"] = round(pixels / warm / 1e9, 3)
             rec["ms_per_step_warm_cache"] = round(warm * 1e3 / max(1, args.steps), 5)
+        if stream_rec is not None:
+            rec.update(stream_rec)
         if cpu_ms is not None:
             rec["cpu_ms_per_image"] = round(cpu_ms, 3)
             rec["cpu_threads"] = ops.vector._native.lib().mpx_cpu_threads()
@@ -250,6 +273,75 @@ def run(args) -> int:
         d.close()
     parallel.shutdown()
     return 0 if ok else 1
+
+
+def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
+    """value_streaming: K timed steps of the iterated filter over the rotated
+    slabs (each step's halo rows were produced by the neighbours' previous
+    step), then the N-rank == one-device check of every rotated slab."""
+    import torch
+
+    from cuda_mpi_openmp_amd.models.edge import SlabEdgeDetector, stream_reference
+
+    seeds = [1234 + 7919 * r for r in range(max(1, args.rotate))]
+    sdets = []
+    for sd in seeds:
+        d = SlabEdgeDetector(ctx, args.size * n, args.size, args.filter, halo=args.halo, stream=True)
+        d.fill_random(seed=sd + ctx.rank)
+        sdets.append(d)
+    cyc = [0]
+
+    def step():
+        sdets[cyc[0] % len(sdets)].step()
+        cyc[0] += 1
+
+    for _ in range(max(args.warmup, len(sdets))):
+        step()
+        watchdog.beat()
+    sync()
+    ctx.barrier()
+    cyc[0] = 0
+    mine = timed(step, args.steps)
+    watchdog.beat()
+    per_rank = parallel.all_gather_floats(mine, ctx)
+    elapsed = max(per_rank)
+    for d in sdets:
+        d.check_stream()
+    rec = {"value_streaming": round(n * args.size * args.size * args.steps / elapsed / 1e9, 3),
+           "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
+           "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
+           "transport_streaming": sdets[0].transport if n > 1 else None}
+    if not args.no_verify:
+        ok, checked = True, 0
+        for sd, d in zip(seeds, sdets):
+            good, cnt = verify_full(d, ops)  # this rank's last step vs the CPU reference
+            ok &= good
+            got = parallel.gather_slabs(d.stream_out.contiguous(), d.slab, ctx)
+            if ctx.rank == 0:  # the whole job vs one device running the same frames on the whole image
+                full0 = torch.cat([regen_slab(sd + r, d.slab.rows_of(r), args.size, ctx.device) for r in range(n)])
+                ref = stream_reference(full0, d.filter, d._sk)
+                same = torch.equal(got.to(ref.device), ref)
+                ok &= same
+                checked += ref.shape[0] * ref.shape[1] if same else 0
+        ok = parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
+        rec["verified_streaming"] = "N-rank result == one-device result of the same frame sequence (every pixel)"
+        rec["verified_bit_exact_streaming"] = ok
+        rec["verified_pixels_streaming"] = int(parallel.broadcast_object(checked, ctx))
+        rec["verified_bit_exact"] = None if ok else False
+    for d in sdets:
+        d.close()
+    if rec.get("verified_bit_exact") is None:
+        rec.pop("verified_bit_exact", None)
+    return rec
+
+
+def regen_slab(seed: int, rows: int, size: int, device):
+    """Rank r's initial frame (SlabEdgeDetector.fill_random with its seed)."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (rows, size, 4), dtype=torch.uint8, device=device, generator=g)
 
 
 def cpu_baseline_ms(det, size: int, ops) -> float:
@@ -274,7 +366,7 @@ def verify_full(det, ops):
     out_cpu = torch.empty((s.rows, det.w, 4), dtype=torch.uint8)
     ops.conv_rows(buf, out_cpu, det.filter, src_row0=s.own_offset, out_row0=0, oy0=0, oy1=s.rows, y_lo=s.y_lo,
                   y_hi=s.y_hi)
-    good = bool(torch.equal(out_cpu, det.out.to("cpu")))
+    good = bool(torch.equal(out_cpu, (det.stream_out if det.stream else det.out).to("cpu")))
     return good, s.rows * det.w
 
 

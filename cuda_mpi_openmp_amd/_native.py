@@ -58,6 +58,7 @@ _SIGNATURES = {
     "mpx_ipc_handle_size": (c_int, []),
     "mpx_ipc_get_handle": (c_int, [c_vp, c_vp, ctypes.POINTER(c_i64)]),
     "mpx_ipc_open": (c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "mpx_ipc_open_dev": (c_int, [c_int, c_vp, ctypes.POINTER(c_vp)]),
     "mpx_ipc_close": (c_int, [c_vp]),
     "mpx_memcpy_d2d": (c_int, [c_vp, c_vp, c_i64, c_vp]),
     "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
@@ -103,6 +104,14 @@ _SIGNATURES = {
     "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_ws_status": (c_int, [c_vp, c_i64, c_int]),
     "mpx_cpu_sort": (None, [c_vp, c_i64, c_int]),
+    "mpx_rows_checksum": (c_int, [c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp]),
+    "mpx_peer_probe_run": (c_int, [c_vp, c_vp]),
+    "mpx_halo_fetch_run": (c_int, [c_vp, c_vp]),
+    "mpx_sync_alloc": (c_int, [c_i64, ctypes.POINTER(c_vp), _ip]),
+    "mpx_sync_free": (c_int, [c_vp]),
+    "mpx_sync_write": (c_int, [c_vp, c_int, ctypes.c_uint]),
+    "mpx_sync_read": (c_int, [c_vp, c_int, ctypes.POINTER(ctypes.c_uint)]),
+    "mpx_sync_clear": (c_int, [c_vp, c_i64]),
 }
 
 

@@ -79,7 +79,21 @@ def main(argv: Optional[List[str]] = None) -> int:
     if args.warmup is not None:
         env["MPX_WARMUP"] = str(max(0, args.warmup))
     if args.n_gpus and args.n_gpus > 1:
+        # an N-GPU row must come from N GPUs: refuse when fewer are visible,
+        # unless explicitly rehearsing on shared devices (then the CSV records
+        # devices_used)
+        from ..parallel.launch import visible_devices
+
+        ndev = visible_devices()
+        shared = os.environ.get("MPX_ALLOW_SHARED") == "1"
+        if ndev < args.n_gpus and not shared:
+            print(f"[harness] --n_gpus {args.n_gpus} requested but {ndev} GPU(s) are visible; refusing to record "
+                  f"an N-GPU result (MPX_ALLOW_SHARED=1 rehearses on shared devices)", file=sys.stderr)
+            return 2
         env["MPX_NGPUS"] = str(args.n_gpus)
+        env["MPX_DEVICES_USED"] = str(max(1, min(args.n_gpus, ndev)))
+        if shared:
+            env["MPX_ALLOW_SHARED"] = "1"
     env = env or None
     tester = Tester(binary_path_gpu=args.binary_path_cuda, k_times=args.k_times, kernel_sizes=kernel_sizes,
                     metadata_columns2plot=meta, binary_path_cpu=args.binary_path_cpu, return_inp=args.return_inp,

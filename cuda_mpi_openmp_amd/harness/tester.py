@@ -76,6 +76,8 @@ class Tester:
                 row["wall_ms"] = rec.wall_ms
                 row["device"] = device
                 row["n_gpus"] = int((env or {}).get("MPX_NGPUS", 1)) if device == self.gpu_label else 0
+                row["devices_used"] = int((env or {}).get("MPX_DEVICES_USED", row["n_gpus"] and 1)) \
+                    if device == self.gpu_label else 0
                 self._throughput(row)
                 rows.append(row)
                 print(f"[Experiment bin_name=<{bin_name}> task={i} kernel_size=<{[k1, k2]}>] finished with "

@@ -38,6 +38,20 @@ class EdgeDetector:
         return ref.conv(img, self.filter)
 
 
+def stream_reference(full: torch.Tensor, filt: str | Filter, steps: int) -> torch.Tensor:
+    """The streaming benchmark's frame sequence on ONE device over the whole
+    image: ``steps`` iterated whole-image convolutions (step k convolves step
+    k-1's output). The N-rank ``SlabEdgeDetector(stream=True)`` must equal it
+    bit for bit."""
+    f = get_filter(filt) if isinstance(filt, str) else filt
+    a = full.contiguous().clone()
+    b = torch.empty_like(a)
+    for _ in range(steps):
+        ops.conv(a, f, b)
+        a, b = b, a
+    return a
+
+
 class SlabEdgeDetector:
     """One rank's share of a row-decomposed image convolution.
 
@@ -66,10 +80,20 @@ class SlabEdgeDetector:
       arranged by ``overlap``;
     * ``"auto"``: ``"peer"`` when every rank can map and verify its neighbours,
       else ``"rccl"``.
+
+    ``stream=True`` makes the input change every step, so the halo rows a rank
+    reads are new each step (a real inter-rank dependency): the
+    filter is iterated — step k convolves step k-1's output — over two
+    ping-pong input buffers. Step k's halo rows come from the neighbours'
+    step k-1 output, via a device-signalled fetch kernel (``peer``: publish the
+    step, wait for the neighbours to reach it, copy their boundary rows over
+    xGMI; ``parallel.peer.StreamHaloLink``) or an in-order RCCL send/recv
+    (``rccl``). Results equal a one-device run of the same frame sequence
+    on the whole image.
     """
 
     def __init__(self, ctx: DistContext, global_h: int, w: int, filt: str | Filter = "sobel5",
-                 overlap: bool | str = "auto", halo: str = "auto"):
+                 overlap: bool | str = "auto", halo: str = "auto", stream: bool = False):
         self.ctx = ctx
         self.filter = get_filter(filt) if isinstance(filt, str) else filt
         self.w = w
@@ -82,10 +106,12 @@ class SlabEdgeDetector:
         # 7-16 us; profiles/comm_step.md); torch.distributed keeps the overlap.
         if overlap == "auto":
             overlap = ctx.native is None
-        self.pipeline = overlap == "pipeline" and ctx.native is not None and ctx.device.type == "cuda"
-        self.overlap = bool(overlap) and not self.pipeline and overlap != "pipeline"
+        self.stream = bool(stream)
+        self.pipeline = (overlap == "pipeline" and ctx.native is not None and ctx.device.type == "cuda"
+                         and not self.stream)
+        self.overlap = bool(overlap) and not self.pipeline and overlap != "pipeline" and not self.stream
         dev = ctx.device
-        nbuf = 2 if self.pipeline else 1
+        nbuf = 2 if (self.pipeline or self.stream) else 1
         self.bufs = [torch.empty((self.slab.buffer_rows, w, 4), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
         self.out = torch.empty((self.slab.rows, w, 4), dtype=torch.uint8, device=dev)
         # pre-validated launches for the three row ranges of a step
@@ -98,9 +124,22 @@ class SlabEdgeDetector:
         self._interior = mk(self.bufs[0], *s.interior())
         self._boundary = [mk(self.bufs[0], a, b) for a, b in s.boundary()]
         self.peer = None
+        self.slink = None
+        self._sk = 0  # stream mode: steps done since the last load
         if halo not in ("auto", "peer", "rccl"):
             raise ValueError(f"unknown halo transport {halo!r}")
-        if halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
+        if self.stream:
+            # step reading buffer a writes the owned rows of buffer 1 - a
+            self._stream_launch = [ops.ConvLauncher(self.bufs[a], self.bufs[1 - a], self.filter, src_row0=s.own_offset,
+                                                    out_row0=s.own_offset, oy0=0, oy1=s.rows, y_lo=s.y_lo,
+                                                    y_hi=s.y_hi) for a in range(2)]
+            if halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
+                from ..parallel.peer import try_stream_halo
+
+                self.slink = try_stream_halo(ctx, s, self.bufs)
+                if self.slink is None and halo == "peer":
+                    raise RuntimeError("streaming peer halo transport unavailable (IPC mapping or probe failed)")
+        elif halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
             from ..parallel.peer import try_peer_halo
 
             self.peer = try_peer_halo(ctx, s, self.bufs[0][s.own_offset: s.own_offset + s.rows])
@@ -119,7 +158,16 @@ class SlabEdgeDetector:
     @property
     def buf(self) -> torch.Tensor:
         """The input buffer the most recent (or next, before any step) step reads."""
+        if self.stream:
+            return self.bufs[(self._sk - 1) % 2] if self._sk else self.bufs[0]
         return self.bufs[(self._k - 1) % len(self.bufs)] if self._k else self.bufs[0]
+
+    @property
+    def stream_out(self) -> torch.Tensor:
+        """Stream mode: the owned rows the most recent step wrote (its output,
+        the next step's input)."""
+        s = self.slab
+        return self.bufs[self._sk % 2][s.own_offset: s.own_offset + s.rows]
 
     @property
     def own(self) -> torch.Tensor:
@@ -135,6 +183,8 @@ class SlabEdgeDetector:
     def transport(self) -> str:
         if not self.ctx.is_distributed:
             return "none"
+        if self.slink is not None:
+            return "xgmi-peer-signalled-fetch"
         if self.peer is not None:
             return "xgmi-peer"
         return "native-rccl" if self.ctx.native is not None else "torch.distributed"
@@ -150,21 +200,37 @@ class SlabEdgeDetector:
         if self.peer is not None:
             self.peer.publish()
 
+    def _quiesce(self) -> None:
+        """Stream + peer mode, before host writes to the shared buffers: every
+        rank's queued steps (and so its fetches of our rows) have finished."""
+        if self.slink is not None:
+            torch.cuda.synchronize(self.bufs[0].device)
+            self.ctx.barrier()
+
     def load(self, slab_rows: torch.Tensor) -> None:
+        """Collective: set this rank's owned input rows (stream mode: frame 0)."""
         self._drain_comm()
+        self._quiesce()
         s = self.slab
         for b in self.bufs:
             b[s.own_offset: s.own_offset + s.rows].copy_(slab_rows)
-        self._publish()
+        self._restart()
 
     def fill_random(self, seed: int) -> None:
         self._drain_comm()
+        self._quiesce()
         g = torch.Generator(device=self.bufs[0].device)
         g.manual_seed(seed)
         s = self.slab
         rows = torch.randint(0, 256, (s.rows, self.w, 4), dtype=torch.uint8, device=self.bufs[0].device, generator=g)
         for b in self.bufs:
             b[s.own_offset: s.own_offset + s.rows].copy_(rows)
+        self._restart()
+
+    def _restart(self) -> None:
+        self._sk = 0
+        if self.slink is not None:
+            self.slink.reset()  # collective: step words back to 0
         self._publish()
 
     def _rows(self, a: int, b: int) -> None:
@@ -180,6 +246,8 @@ class SlabEdgeDetector:
         return self._step()
 
     def _step(self) -> torch.Tensor:
+        if self.stream:
+            return self._step_stream()
         if self.pipeline:
             return self._step_pipelined()
         st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
@@ -196,6 +264,24 @@ class SlabEdgeDetector:
             self.halo.exchange(self.buf)
             self._all(st)
         return self.out
+
+    def _step_stream(self) -> torch.Tensor:
+        k = self._sk + 1
+        a = (k - 1) % 2
+        st = torch.cuda.current_stream(self.bufs[0].device).cuda_stream if self.bufs[0].is_cuda else None
+        if self.ctx.is_distributed:
+            if self.slink is not None:
+                self.slink.fetch(k, st)           # device-ordered: no host round trip
+            else:
+                self.halo.exchange(self.bufs[a])  # in order on the current stream
+        self._stream_launch[a](st)
+        self._sk = k
+        return self.stream_out
+
+    def check_stream(self) -> None:
+        """Raise when a device-side halo wait of the streaming fetch gave up."""
+        if self.slink is not None and self.slink.timed_out():
+            raise RuntimeError(f"rank {self.ctx.rank}: streaming halo wait timed out near step {self._sk}")
 
     def _step_pipelined(self) -> torch.Tensor:
         nc = self.ctx.native
@@ -223,7 +309,12 @@ class SlabEdgeDetector:
         return self.out
 
     def close(self) -> None:
-        """Unmap the neighbours' slabs (peer mode)."""
+        """Unmap the neighbours' slabs (peer modes). Collective in stream+peer
+        mode (no rank unmaps while a neighbour may still read its rows)."""
+        if self.slink is not None:
+            self._quiesce()
+            self.slink.close()
+            self.slink = None
         if self.peer is not None:
             torch.cuda.synchronize(self.out.device)
             self.peer.close()

@@ -72,22 +72,18 @@ class SlabJacobi:
             self.overlap = False
         self.peer = None
         if halo not in ("rccl", "none") and ctx.is_distributed and dev.type == "cuda":
-            # two allocations (buffer 0 + the sync block, buffer 1), each shared by IPC
-            from .. import _native
+            # two allocations (buffer 0, buffer 1), each shared by IPC; the
+            # iteration words live in a separate sync block (parallel.peer.SyncBlock)
             from ..parallel.peer import try_jacobi_peer
 
             nel = shape[0] * shape[1]
-            es = torch.empty(0, dtype=dtype).element_size()
-            sync_el = max(1, 512 // es)
-            self._storages = [torch.zeros(nel + sync_el, dtype=dtype, device=dev),
-                              torch.zeros(nel, dtype=dtype, device=dev)]
-            self.u = self._storages[0][:nel].view(shape)
+            self._storages = [torch.zeros(nel, dtype=dtype, device=dev), torch.zeros(nel, dtype=dtype, device=dev)]
+            self.u = self._storages[0].view(shape)
             self.un = self._storages[1].view(shape)
-            sync = self._storages[0][nel:nel + sync_el].view(torch.int32)
-            assert sync.numel() * 4 >= _native.lib().mpx_jacobi_sync_bytes()
+            es = self.u.element_size()
             nv = 16 // es
             layout_ok = cols % nv == 0 and self.u.data_ptr() % 16 == 0 and self.un.data_ptr() % 16 == 0
-            self.peer = try_jacobi_peer(ctx, self.slab, self._storages, [self.u, self.un], sync, layout_ok)
+            self.peer = try_jacobi_peer(ctx, self.slab, self._storages, [self.u, self.un], layout_ok)
             if self.peer is None and halo == "peer":
                 raise RuntimeError("peer halo transport unavailable (IPC mapping failed or cols not a multiple of "
                                    f"{nv})")
@@ -114,6 +110,7 @@ class SlabJacobi:
 
     def fill(self, fn: Optional[Callable[[torch.Tensor, torch.Tensor], torch.Tensor]] = None, seed: int = 0) -> None:
         """Interior initial values: fn(global_row_index, col_index) or seeded noise."""
+        self._quiesce()
         s = self.slab
         rows = torch.arange(s.row0, s.row0 + s.rows, device=self.u.device).unsqueeze(1)
         cols = torch.arange(1, self.cols - 1, device=self.u.device).unsqueeze(0)
@@ -136,11 +133,24 @@ class SlabJacobi:
             return "xgmi-peer-signalled"
         return "native-rccl" if self.ctx.native is not None else "torch.distributed"
 
+    def _quiesce(self) -> None:
+        """Peer mode, before any host write to the IPC-shared buffers: every
+        rank's queued sweeps have finished (a neighbour's last untracked sweep
+        may still be reading our edge rows or waiting on our iteration word)."""
+        if self.peer is not None:
+            torch.cuda.synchronize(self.u.device)
+            self.ctx.barrier()
+
     def sync_halos(self) -> None:
         """Exchange u's slab-edge rows (needed once after (re)initialisation;
         afterwards every step refreshes the halos of the rows it computes).
-        Peer mode: publish the buffers and reset every rank's iteration word."""
+        Peer mode: publish the buffers and reset every rank's iteration word.
+        The captured cycle graphs hold the previous descriptor (the neighbours'
+        buffer parity) by value, so they are dropped here."""
         if self.peer is not None or self.no_halo:
+            if self.peer is not None:
+                self._quiesce()
+                self._graphs.clear()
             self.un.copy_(self.u)
             if self.peer is not None:
                 self.peer.publish(self.u, self.iteration)
@@ -171,9 +181,13 @@ class SlabJacobi:
                 self.resid.fill_(max(float(self.resid.item()), r))
 
     def step(self) -> Optional[float]:
-        _fault_hook(self.ctx.rank, self.iteration)
+        corrupt = _fault_hook(self.ctx.rank, self.iteration)
         if not self._halos_valid:
             self.sync_halos()
+        if corrupt:  # injected silent error: one halo value off by one (peer mode: the
+            # edge row the neighbour reads, since the kernel reads its halo in place)
+            row = 1 if self.peer is not None else 0 if self.slab.has_up else self.slab.rows + 1
+            self.u[row, self.cols // 2] += 1.0
         track = (self.iteration + 1) % self.check_every == 0
         self._advance(track)
         if track:
@@ -302,6 +316,8 @@ class SlabJacobi:
         ck = torch.load(f"{prefix}.rank{self.ctx.rank}.pt", weights_only=True)
         if (ck["global_rows"], ck["world"], ck["cols"]) != (self.slab.global_rows, self.ctx.world, self.cols):
             raise ValueError("checkpoint geometry does not match this solver")
+        self._quiesce()
+        self._graphs.clear()
         self.u.copy_(ck["u"].to(self.u.device, self.dtype))
         self.un.copy_(self.u)
         self.iteration = int(ck["iteration"])

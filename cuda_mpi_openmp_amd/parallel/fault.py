@@ -12,7 +12,10 @@ reference has no timeouts at all (its harness waits on subprocess.run). Here:
   blocked RCCL kernels) and exits the process with :data:`EXIT_HUNG`, so a
   launcher sees a prompt, attributable failure instead of a silent hang.
 * ``MPX_FAULT_INJECT="rank:iteration"`` (models/jacobi.py) raises
-  :class:`FaultInjected` on one rank, which the tests use to check the path.
+  :class:`FaultInjected` on one rank, which the tests use to check the path;
+  ``MPX_FAULT_INJECT="halo:rank:iteration"`` instead corrupts that rank's
+  received halo row before that iteration's sweep (silently wrong data), which
+  the N-rank == one-device verification must catch.
 """
 
 from __future__ import annotations
@@ -30,13 +33,20 @@ class FaultInjected(RuntimeError):
     """Raised by the MPX_FAULT_INJECT hook (tests of failure detection)."""
 
 
-def fault_hook(rank: int, it: int) -> None:
-    spec = os.environ.get("MPX_FAULT_INJECT")  # "rank:iteration"
+def fault_hook(rank: int, it: int) -> bool:
+    """Raise on "rank:iteration"; return True on "halo:rank:iteration" (the
+    caller corrupts its halo row); False otherwise."""
+    spec = os.environ.get("MPX_FAULT_INJECT")
     if not spec:
-        return
-    r, i = (int(v) for v in spec.split(":"))
+        return False
+    parts = spec.split(":")
+    corrupt = parts[0] == "halo"
+    r, i = (int(v) for v in parts[-2:])
     if r == rank and i == it:
+        if corrupt:
+            return True
         raise FaultInjected(f"injected fault on rank {rank} at iteration {it}")
+    return False
 
 
 class Watchdog:

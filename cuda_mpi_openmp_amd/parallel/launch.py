@@ -38,10 +38,53 @@ def free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def visible_devices() -> int:
-    import torch
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
-    return int(torch.cuda.device_count())  # counts devices without creating a HIP context
+
+def _kfd_gpu_count(root: str = KFD_NODES) -> Optional[int]:
+    """GPU agents in the KFD topology (nodes whose gfx_target_version is set;
+    CPU nodes report 0) — read from sysfs, no HIP runtime involved. None when
+    the topology is unreadable."""
+    try:
+        names = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in names:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version":
+                        n += int(v.strip() or 0) != 0
+                        break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def _visible_filter(n: int) -> int:
+    """Apply the runtime's device-visibility variables to n physical GPUs."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        toks = [t for t in v.split(",") if t.strip() != ""]
+        n = min(n, len(toks)) if v.strip() else 0
+    return n
+
+
+def visible_devices() -> int:
+    """GPUs this process would see, counted from the KFD sysfs topology and the
+    visibility variables — the launcher never loads or initialises HIP before
+    spawning its ranks. Falls back to torch's count only when
+    sysfs is unreadable."""
+    n = _kfd_gpu_count()
+    if n is None:
+        import torch
+
+        return int(torch.cuda.device_count())
+    return _visible_filter(n)
 
 
 def launcher_cmd(script: str, argv: Sequence[str], nproc: int, port: Optional[int] = None) -> List[str]:

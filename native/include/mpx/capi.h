@@ -159,9 +159,55 @@ int mpx_ipc_handle_size(void);
 int mpx_ipc_get_handle(const void *ptr, void *handle, int64_t *offset);
 /* maps a peer's allocation on the current device (peer access enabled lazily) */
 int mpx_ipc_open(const void *handle, void **base);
+/* the same with hipSetDevice(device) first (mapping from a helper thread) */
+int mpx_ipc_open_dev(int device, const void *handle, void **base);
 int mpx_ipc_close(void *base);
 /* stream-ordered device-to-device copy (either side may be IPC-mapped) */
 int mpx_memcpy_d2d(void *dst, const void *src, int64_t bytes, void *stream);
+
+/* ---------------- one-sided transports: probes, streaming halo fetch (peer.hip) ---------------- */
+/* *out += position-sensitive checksum of nrows rows read with the kernels' 16-byte
+ * buffer loads (sys != 0: system-scope cache policy); zero *out first. */
+int mpx_rows_checksum(const void *rows, int64_t row_bytes, int nrows, int64_t pitch_bytes, int sys,
+                      unsigned long long *out, void *stream);
+/* Signalled start-up probe (one workgroup): write a (rank, buffer)-pattern into
+ * own_rows[0..3] (buffer = index / 2; NULL = skip) with system-scope stores,
+ * publish sync[0] = magic (release), then for each side s with flag[s]: wait
+ * flag[s] >= magic (bounded; sync[64] = 1 on give-up) and compare
+ * nb_rows[s][0..1] with the neighbour's pattern; mismatching words are added
+ * to sync[96]. row_bytes: a multiple of 4 (16-byte accesses when every row is
+ * 16-byte aligned and row_bytes a multiple of 16, 4-byte ones otherwise). */
+typedef struct mpx_peer_probe {
+    void *own_rows[4];
+    const void *nb_rows[2][2];
+    const unsigned int *flag[2];
+    unsigned int *sync;
+    int64_t row_bytes;
+    int rank;
+    unsigned int magic;
+    unsigned int spin_limit;
+} mpx_peer_probe;
+int mpx_peer_probe_run(const mpx_peer_probe *p, void *stream);
+/* Streaming halo fetch: publish sync[0] = step (release), then per side s with a
+ * neighbour: wait flag[s] >= step (bounded), copy bytes[s] from src[s] (its
+ * boundary rows, system-scope loads) to dst[s] (this rank's halo rows). */
+typedef struct mpx_halo_fetch {
+    const void *src[2];
+    void *dst[2];
+    int64_t bytes[2];
+    const unsigned int *flag[2];
+    unsigned int *sync;
+    unsigned int step;
+    unsigned int spin_limit;
+} mpx_halo_fetch;
+int mpx_halo_fetch_run(const mpx_halo_fetch *f, void *stream);
+/* IPC-exportable sync block: uncached (kind 2), fine-grained (1) or coarse (0) memory, zeroed */
+int mpx_sync_alloc(int64_t bytes, void **ptr, int *kind);
+int mpx_sync_free(void *ptr);
+/* synchronous host access to word `word` (0..127) of a sync block */
+int mpx_sync_write(unsigned int *sync, int word, unsigned int value);
+int mpx_sync_read(const unsigned int *sync, int word, unsigned int *value);
+int mpx_sync_clear(unsigned int *sync, int64_t bytes);
 
 /* ---------------- 2-D Jacobi (distributed stencil tier) ---------------- */
 /*

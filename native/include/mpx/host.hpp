@@ -160,11 +160,11 @@ inline void tuned_if_nonpositive(int &a, int &b) {
 }
 
 // ---- multi-device parts (MPX_NGPUS=N, harness --n_gpus N) ----
-// The lab programs split their work into N parts; part p runs on device
-// p % (visible devices) with its own stream and events, so the split logic is
-// exercised even on a box with fewer GPUs. The reported time is the max over
-// parts of each part's kernel time — the parallel time when the parts own
-// distinct GPUs.
+// The lab programs split their work into N parts; part p runs on device p
+// with its own stream and events. The reported time is the max over parts of
+// each part's kernel time — the parallel time of N GPUs. Fewer visible
+// devices than parts is refused (exit 2) unless MPX_ALLOW_SHARED=1 rehearses
+// the split on shared devices (part p on device p % visible).
 inline int parts_from_env() {
     const char *s = std::getenv("MPX_NGPUS");
     const int n = s ? std::atoi(s) : 1;
@@ -181,6 +181,14 @@ class Parts {
     explicit Parts(int n) : p_(n) {
         int ndev = 0;
         HIP_CHECK(hipGetDeviceCount(&ndev));
+        // an N-part time is an N-GPU time only on N devices: refuse to share
+        // one unless asked to rehearse (MPX_ALLOW_SHARED=1)
+        const char *shared = std::getenv("MPX_ALLOW_SHARED");
+        if (n > ndev && !(shared && shared[0] == '1')) {
+            std::fprintf(stderr, "[ERROR] MPX_NGPUS=%d but %d device(s) are visible (MPX_ALLOW_SHARED=1 to share)\n",
+                         n, ndev);
+            std::exit(2);
+        }
         for (int i = 0; i < n; ++i) {
             p_[i].dev = i % ndev;
             HIP_CHECK(hipSetDevice(p_[i].dev));

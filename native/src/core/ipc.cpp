@@ -36,6 +36,13 @@ extern "C" int mpx_ipc_open(const void *handle, void **base) {
     return MPX_OK;
 }
 
+// Same on an explicit device: for callers that map from a helper thread
+// (a deadline-bounded open), whose current device is not the rank's.
+extern "C" int mpx_ipc_open_dev(int device, const void *handle, void **base) {
+    MPX_RETURN_IF_HIP_ERROR(hipSetDevice(device));
+    return mpx_ipc_open(handle, base);
+}
+
 extern "C" int mpx_ipc_close(void *base) {
     MPX_CHECK_ARG(base, "null pointer");
     MPX_RETURN_IF_HIP_ERROR(hipIpcCloseMemHandle(base));

@@ -20,6 +20,7 @@
 // Pitches or widths that are not a multiple of the vector width use the
 // generic per-lane kernel below.
 #include "internal.hpp"
+#include "peer_sync.hpp"
 
 #include <type_traits>
 
@@ -178,30 +179,20 @@ __device__ __forceinline__ T dpp_shift(T v, int ctrl) {
 // an edge wave waits until the neighbour's counter is >= t — the neighbour has
 // finished iteration t-1, so (a) its edge row of u^(t) is written and (b) it
 // is done reading this rank's edge row of u^(t-1), the buffer this sweep
-// overwrites. After its stores, an edge wave releases them at system scope and
-// bumps this rank's edge-wave counter; the last one publishes counter value
-// t+1. Coherence without cache-maintenance fences (an L2 write-back or
-// invalidate per edge wave cost ~40 us per sweep): the rows a neighbour reads
-// are stored at system scope (write-through) and acknowledged before the
-// count goes up, and halo rows are loaded at system scope (never a stale
-// cached line). Interior waves never wait. Edge waves are dispatched first so the
+// overwrites. After its stores, an edge wave waits for their acknowledgement
+// and bumps this rank's edge-wave counter; the last one publishes counter
+// value t+1 with a system-scope RELEASE store (peer_sync.hpp: one L2
+// write-back per sweep, by that one wave). No per-wave cache maintenance (an
+// L2 write-back or invalidate per edge wave cost ~40 us per sweep): the rows
+// a neighbour reads are stored at system scope (write-through) and
+// acknowledged before the count goes up, and halo rows are loaded at system
+// scope (never a stale cached line), so the consumer needs no acquire fence
+// after its wait. Interior waves never wait. Edge waves are dispatched first so the
 // counter is published early in the sweep. Waits are bounded (pr.spin_limit):
 // a wave that gives up sets sync[kSyncErr] and the host raises.
 // ---------------------------------------------------------------------------
 constexpr int kSyncIter = 0, kSyncCtr = 32, kSyncErr = 64;  // uint32 slots, 128 B apart
-constexpr int kCpolSystem = 1 | 16;                          // gfx950 cache policy SC0 | SC1: system scope
-constexpr uint32_t kPeerSpinDefault = 1u << 22;             // ~seconds of s_sleep
-
-__device__ __forceinline__ void peer_wait(const uint32_t *flag, uint32_t target, uint32_t *err, uint32_t limit) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
-        if (++spins > limit) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(4);
-    }
-}
+constexpr int kCpolSystem = peer::kCpolSystem;               // gfx950 cache policy SC0 | SC1: system scope
 
 // Max over the wave of non-negative values through DPP (row_shr 1/2/4/8 within
 // each 16-lane row, then row_bcast 15/31 across rows; lanes with no source
@@ -270,11 +261,11 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
                 // after every edge wave of the sweep has finished)
                 it = __hip_atomic_load(pr.sync + kSyncIter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (rb == 0 && pr.up_flag) {
-                    peer_wait(pr.up_flag, it, pr.sync + kSyncErr, pr.spin_limit ? pr.spin_limit : kPeerSpinDefault);
+                    peer::wait_at_least(pr.up_flag, it, pr.sync + kSyncErr, pr.spin_limit);
                     up_row = static_cast<const T *>(pr.up_row[it & 1u]) + (int64_t)cvc * NV;
                 }
                 if (i1 == r1 && pr.dn_flag) {
-                    peer_wait(pr.dn_flag, it, pr.sync + kSyncErr, pr.spin_limit ? pr.spin_limit : kPeerSpinDefault);
+                    peer::wait_at_least(pr.dn_flag, it, pr.sync + kSyncErr, pr.spin_limit);
                     dn_row = static_cast<const T *>(pr.dn_row[it & 1u]) + (int64_t)cvc * NV;
                 }
             }
@@ -402,7 +393,9 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
                                                               __HIP_MEMORY_SCOPE_AGENT);
                     if (c + 1 == (uint32_t)n_edge) {  // last edge wave of this sweep
                         __hip_atomic_store(pr.sync + kSyncCtr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(pr.sync + kSyncIter, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        // release at system scope: every edge wave's write-through row
+                        // stores were acknowledged (waitcnt above, then the counter)
+                        peer::publish(pr.sync + kSyncIter, it + 1);
                     }
                 }
             }

@@ -1,0 +1,256 @@
+// One-sided halo transports between the ranks of a node (one process per
+// MI355X, neighbour slabs IPC-mapped and read over xGMI), beyond the fused
+// conv / Jacobi kernels:
+//
+//  * mpx_rows_checksum — start-up check of an IPC mapping THROUGH THE
+//    KERNELS' OWN LOAD PATH (16-byte buffer loads, default or system cache
+//    policy), compared with the owner's checksum of the same rows; replaces a
+//    hipMemcpy read-back, which goes through the copy engines instead;
+//  * mpx_peer_probe_run — start-up check of the device-signalled protocol: every
+//    rank writes a pattern into the rows it shares with the production store
+//    path, publishes a counter with the production release, and reads its
+//    neighbours' rows after the production wait — on real xGMI links before
+//    any timed or verified work trusts them (mismatch or timeout -> RCCL);
+//  * mpx_halo_fetch — the streaming convolution's halo exchange: publish this
+//    rank's step, wait (bounded) for each neighbour to reach it, copy their
+//    boundary rows into the local halo rows with system-scope loads. One tiny
+//    launch per step, no RCCL kernel, no host round trip.
+//
+// Reference: no multi-GPU code exists (/root/reference/
+// CMakeLists.txt:2 name only); this is the north-star halo tier.
+#include "peer_sync.hpp"
+
+namespace mpx {
+namespace {
+
+using peer::u32x4;
+
+constexpr int kSyncStep = 0, kSyncErr = 64, kSyncMismatch = 96;  // uint32 slots of a 512-B sync block
+
+// ---------------------------------------------------------------------------
+// checksum of nrows rows (row_bytes each, pitch_bytes apart): sum over 16-byte
+// chunks c of (word0 + 3*word1 + 5*word2 + 7*word3 + 1) * (global chunk + 1)
+// mod 2^64 — position-sensitive, identical on both sides of a mapping.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rows_checksum_kernel(const char *rows, uint32_t row_bytes, int nrows,
+                                                            int64_t pitch_bytes, int sys,
+                                                            unsigned long long *out) {
+    const int r = blockIdx.x;
+    if (r >= nrows) return;
+    const char *row = rows + (int64_t)r * pitch_bytes;
+    const uint32_t chunks = (row_bytes + 15) / 16;
+    unsigned long long acc = 0;
+    for (uint32_t c = threadIdx.x; c < chunks; c += 256) {
+        // out-of-range bytes of the last chunk read as 0 (buffer bounds check)
+        const u32x4 v = sys ? peer::load16_sys(row, c * 16, row_bytes) : peer::load16(row, c * 16, row_bytes);
+        const unsigned long long h = (unsigned long long)v.x + 3ull * v.y + 5ull * v.z + 7ull * v.w + 1ull;
+        acc += h * ((unsigned long long)r * chunks + c + 1);
+    }
+    atomicAdd(out, acc);
+}
+
+// ---------------------------------------------------------------------------
+// signalled probe
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t probe_word(int rank, int k, uint32_t i) {
+    uint32_t x = (uint32_t)(rank + 1) * 0x9E3779B1u ^ (uint32_t)(k + 1) * 0x85EBCA77u ^ i * 0xC2B2AE3Du;
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return x & 0x00FFFFFFu;  // exact in fp32 and fp64 when read as T
+}
+
+// V16: 16-byte system-scope accesses (the Jacobi peer path; rows 16-byte
+// aligned, row_bytes a multiple of 16), else 4-byte ones (any RGBA row).
+template <bool V16>
+__global__ __launch_bounds__(256) void peer_probe_kernel(mpx_peer_probe p) {
+    constexpr uint32_t kW = V16 ? 4 : 1;  // words per access
+    const uint32_t chunks = (uint32_t)(p.row_bytes / (4 * kW));
+    const uint32_t rb = (uint32_t)p.row_bytes;
+    // (a) this rank's shared rows, production store path (system-scope write-through)
+    for (int q = 0; q < 4; ++q) {
+        if (!p.own_rows[q]) continue;
+        const int k = q >> 1;  // buffer index: the pattern does not depend on top / bottom
+        for (uint32_t c = threadIdx.x; c < chunks; c += 256) {
+            if constexpr (V16) {
+                u32x4 v;
+                v.x = probe_word(p.rank, k, 4 * c);
+                v.y = probe_word(p.rank, k, 4 * c + 1);
+                v.z = probe_word(p.rank, k, 4 * c + 2);
+                v.w = probe_word(p.rank, k, 4 * c + 3);
+                peer::store16_sys(p.own_rows[q], c * 16, rb, v);
+            } else {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.own_rows[q], 0, rb, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(probe_word(p.rank, k, c), rs, c * 4, 0, peer::kCpolSystem);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // every wave's stores acknowledged before the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) peer::publish(p.sync + kSyncStep, p.magic);
+    // (b) wave 0 checks the upper neighbour, wave 1 the lower one
+    const int side = threadIdx.x >> 6;
+    if (side > 1 || !p.flag[side]) return;
+    const int lane = threadIdx.x & 63;
+    if (!peer::wait_at_least(p.flag[side], p.magic, p.sync + kSyncErr, p.spin_limit)) return;
+    const int nb = side == 0 ? p.rank - 1 : p.rank + 1;
+    uint32_t bad = 0;
+    for (int k = 0; k < 2; ++k) {
+        const void *row = p.nb_rows[side][k];
+        if (!row) continue;
+        for (uint32_t c = lane; c < chunks; c += 64) {
+            if constexpr (V16) {
+                const u32x4 v = peer::load16_sys(row, c * 16, rb);
+                bad += (v.x != probe_word(nb, k, 4 * c)) + (v.y != probe_word(nb, k, 4 * c + 1)) +
+                       (v.z != probe_word(nb, k, 4 * c + 2)) + (v.w != probe_word(nb, k, 4 * c + 3));
+            } else {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(row), 0, rb,
+                                                                                    0x00020000);
+                bad += __builtin_amdgcn_raw_buffer_load_b32(rs, c * 4, 0, peer::kCpolSystem) != probe_word(nb, k, c);
+            }
+        }
+    }
+    if (bad) atomicAdd(p.sync + kSyncMismatch, bad);
+}
+
+// ---------------------------------------------------------------------------
+// streaming halo fetch: block b serves side b (0 = rows above, 1 = rows below)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void halo_fetch_kernel(mpx_halo_fetch f) {
+    const int side = blockIdx.x;
+    if (threadIdx.x == 0) peer::publish(f.sync + kSyncStep, f.step);  // idempotent per block
+    if (!f.src[side]) return;  // block-uniform: global edge
+    __shared__ int s_ok;
+    if (threadIdx.x < 64) {  // one wave polls
+        const bool ok = peer::wait_at_least(f.flag[side], f.step, f.sync + kSyncErr, f.spin_limit);
+        if (threadIdx.x == 0) s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const uint32_t words = (uint32_t)(f.bytes[side] / 4);
+    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(f.src[side]), 0,
+                                                                         (int)f.bytes[side], 0x00020000);
+    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(f.dst[side], 0, (int)f.bytes[side],
+                                                                         0x00020000);
+    // 8 loads in flight per lane before the first store (xGMI latency, not bandwidth)
+    constexpr int kBatch = 8;
+    for (uint32_t w0 = 0; w0 < words; w0 += 256 * kBatch) {
+        uint32_t v[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b)
+            v[b] = __builtin_amdgcn_raw_buffer_load_b32(src, (w0 + b * 256 + threadIdx.x) * 4, 0, peer::kCpolSystem);
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b)
+            __builtin_amdgcn_raw_buffer_store_b32(v[b], dst, (w0 + b * 256 + threadIdx.x) * 4, 0, 0);
+    }
+}
+
+}  // namespace
+MPX_MODULE_ANCHOR(peer)
+}  // namespace mpx
+
+extern "C" int mpx_rows_checksum(const void *rows, int64_t row_bytes, int nrows, int64_t pitch_bytes, int sys,
+                                 unsigned long long *out, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(rows && out && nrows >= 0 && row_bytes > 0 && row_bytes < (int64_t)1 << 31 && pitch_bytes >= row_bytes,
+                  "bad arguments");
+    if (nrows == 0) return MPX_OK;
+    hipLaunchKernelGGL(rows_checksum_kernel, dim3(nrows), dim3(256), 0, as_stream(stream),
+                       static_cast<const char *>(rows), (uint32_t)row_bytes, nrows, pitch_bytes, sys, out);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
+extern "C" int mpx_peer_probe_run(const mpx_peer_probe *p, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(p && p->sync, "null probe descriptor");
+    MPX_CHECK_ARG(p->row_bytes > 0 && p->row_bytes % 4 == 0 && p->row_bytes < (int64_t)1 << 31,
+                  "probe rows must be a positive multiple of 4 bytes");
+    MPX_CHECK_ARG(p->magic > 0, "probe magic must be non-zero");
+    for (int s = 0; s < 2; ++s)
+        MPX_CHECK_ARG(!p->flag[s] == !p->nb_rows[s][0], "a neighbour needs both its rows and its flag");
+    bool v16 = p->row_bytes % 16 == 0;
+    for (const void *q : {(const void *)p->own_rows[0], (const void *)p->own_rows[1], (const void *)p->own_rows[2],
+                          (const void *)p->own_rows[3], p->nb_rows[0][0], p->nb_rows[0][1], p->nb_rows[1][0],
+                          p->nb_rows[1][1]}) {
+        MPX_CHECK_ARG(!q || (reinterpret_cast<uintptr_t>(q) & 3u) == 0, "probe rows must be 4-byte aligned");
+        v16 = v16 && (!q || aligned16(q));
+    }
+    if (v16)
+        hipLaunchKernelGGL(peer_probe_kernel<true>, dim3(1), dim3(256), 0, as_stream(stream), *p);
+    else
+        hipLaunchKernelGGL(peer_probe_kernel<false>, dim3(1), dim3(256), 0, as_stream(stream), *p);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
+extern "C" int mpx_halo_fetch_run(const mpx_halo_fetch *f, void *stream) {
+    using namespace mpx;
+    MPX_CHECK_ARG(f && f->sync && f->step > 0, "bad halo-fetch descriptor");
+    for (int s = 0; s < 2; ++s) {
+        MPX_CHECK_ARG(!f->src[s] == !f->flag[s] && (!f->src[s] || f->dst[s]), "a neighbour needs rows, flag and dst");
+        MPX_CHECK_ARG(!f->src[s] || (f->bytes[s] > 0 && f->bytes[s] % 4 == 0 && f->bytes[s] < (int64_t)1 << 31),
+                      "halo bytes must be a positive multiple of 4");
+    }
+    hipLaunchKernelGGL(halo_fetch_kernel, dim3(2), dim3(256), 0, as_stream(stream), *f);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
+// Sync-block allocation for the signalled transports: uncached device memory
+// (MTYPE UC: never held in any L2, so counters need no cache policy at all)
+// when this stack can export it over IPC, else fine-grained, else ordinary
+// coarse-grained memory (then the system-scope loads / stores carry the
+// protocol). *kind: 2 uncached, 1 fine-grained, 0 coarse-grained.
+extern "C" int mpx_sync_alloc(int64_t bytes, void **ptr, int *kind) {
+    using namespace mpx;
+    MPX_CHECK_ARG(ptr && kind && bytes > 0, "bad arguments");
+    const unsigned flags[3] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained, hipDeviceMallocDefault};
+    const int kinds[3] = {2, 1, 0};
+    const char *force = std::getenv("MPX_SYNC_MEM");  // "uncached" | "fine" | "coarse" (A/B)
+    for (int i = 0; i < 3; ++i) {
+        if (force && ((i == 0 && force[0] != 'u') || (i == 1 && force[0] != 'f') || (i == 2 && force[0] != 'c')))
+            continue;
+        void *p = nullptr;
+        if (hipExtMallocWithFlags(&p, (size_t)bytes, flags[i]) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        hipIpcMemHandle_t h;  // usable only if its neighbours can map it
+        if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(p);
+            continue;
+        }
+        MPX_RETURN_IF_HIP_ERROR(hipMemset(p, 0, (size_t)bytes));
+        *ptr = p;
+        *kind = kinds[i];
+        return MPX_OK;
+    }
+    set_error("mpx_sync_alloc: no exportable device allocation of %lld bytes", (long long)bytes);
+    return MPX_ERR_HIP;
+}
+
+extern "C" int mpx_sync_free(void *ptr) {
+    if (ptr) MPX_RETURN_IF_HIP_ERROR(hipFree(ptr));
+    return MPX_OK;
+}
+
+// Host access to single words of a sync block (synchronous; between kernels).
+extern "C" int mpx_sync_write(unsigned int *sync, int word, unsigned int value) {
+    MPX_CHECK_ARG(sync && word >= 0 && word < 128, "bad sync word");
+    MPX_RETURN_IF_HIP_ERROR(hipMemcpy(sync + word, &value, sizeof(value), hipMemcpyHostToDevice));
+    return MPX_OK;
+}
+
+extern "C" int mpx_sync_read(const unsigned int *sync, int word, unsigned int *value) {
+    MPX_CHECK_ARG(sync && value && word >= 0 && word < 128, "bad sync word");
+    MPX_RETURN_IF_HIP_ERROR(hipMemcpy(value, sync + word, sizeof(*value), hipMemcpyDeviceToHost));
+    return MPX_OK;
+}
+
+extern "C" int mpx_sync_clear(unsigned int *sync, int64_t bytes) {
+    MPX_CHECK_ARG(sync && bytes > 0, "bad sync block");
+    MPX_RETURN_IF_HIP_ERROR(hipMemset(sync, 0, (size_t)bytes));
+    return MPX_OK;
+}

@@ -731,6 +731,10 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                            dim3(std::max<int64_t>(1, std::min<int64_t>((n + 4095) / 4096, kNumCUs * 8))), dim3(256), 0,
                            s, x, n, mode, r.hist);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    } else {
+        // the give-up flag sort_ws_status reads: reduce-then-scan never waits,
+        // but the caller's workspace may hold anything (recycled allocations)
+        MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.err, 0, sizeof(uint32_t), s));
     }
     for (int p = 0; p < 4; ++p) {
         const uint32_t *src = (p & 1) ? r.tmp : x;

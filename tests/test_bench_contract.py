@@ -45,6 +45,22 @@ def test_bench_contract_two_ranks_cpu():
     assert rec["config"]["parallelism"].startswith("slab2")
     # value is the whole-job aggregate: N * size^2 * steps / time
     assert abs(rec["value"] - 2 * 96 * 96 / (rec["ms_per_step"] * 1e-3) / 1e9) < 1e-3 * max(1.0, rec["value"])
+    # streaming run: measured and verified N-rank == one device
+    assert rec["value_streaming"] > 0 and rec["verified_bit_exact_streaming"] is True
+    assert rec["verified_pixels_streaming"] == 6 * 2 * 96 * 96
+    assert abs(rec["value_streaming"] - 2 * 96 * 96 / (rec["ms_per_step_streaming"] * 1e-3) / 1e9) \
+        < 1e-3 * max(1.0, rec["value_streaming"])
+
+
+def test_bench_json_carries_no_hard_coded_ratio():
+    """every ratio in the JSON is computed in the run (no
+    literal same-method ratio), and vs_baseline says what it compares."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "vs_reference_same_method" not in src and "SAME_METHOD" not in src
+    rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2", "--no-stream"])
+    assert "vs_reference_same_method" not in rec and "value_streaming" not in rec
+    assert "estimate" in rec["vs_baseline_note"]
+    assert abs(rec["vs_baseline"] - rec["value"] / 4.4) < 0.01 + 1e-3 * rec["vs_baseline"]
 
 
 def test_bench_contract_single_process_cpu():
@@ -60,6 +76,20 @@ def test_bench_jacobi_two_ranks_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["scaling"] == "strong" and rec["residual"] is not None and rec["value"] > 0
+    assert rec["verified"] is True  # gathered 2-rank field == one-device run
+
+
+def test_bench_jacobi_catches_injected_halo_corruption():
+    """a silently corrupted halo value on one rank must fail the
+    N-rank == one-device check (exit 3 from the rank, non-zero from torchrun)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tools", "bench_jacobi.py"), "--device", "cpu",
+           "--size", "64", "--iters", "12", "--warmup", "2", "--check-every", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="1", MPX_FAULT_INJECT="halo:1:5"))
+    assert r.returncode != 0
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["verified"] is False
 
 
 def test_bench_self_launches_ranks_cpu():

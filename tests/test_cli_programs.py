@@ -212,15 +212,23 @@ def test_lab2_gpu_multi_part_matches_cpu(op, tmp_path):
     ref, got = tmp_path / "ref.data", tmp_path / "got.data"
     assert run("labs/lab2/src/cpu_omp_exe", f"{src}\n{ref}", env={"MPX_LAB2_OP": op}).returncode == 0
     r = run("labs/lab2/src/to_plot_hip_exe", f"0\n0\n0\n0\n{src}\n{got}", env={"MPX_LAB2_OP": op, "MPX_NGPUS": "3",
-                                                                           "MPX_WARMUP": "2"})
+                                                                           "MPX_WARMUP": "2", "MPX_ALLOW_SHARED": "1"})
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("HIP execution time: <")
     assert got.read_bytes() == ref.read_bytes()
 
 
 @pytest.mark.gpu
+def test_multi_part_refuses_missing_devices():
+    """VERDICT r2 #8: MPX_NGPUS=N on fewer devices must not report an N-GPU time."""
+    r = run("labs/lab1/src/to_plot_hip_exe", "0\n0\n5\n1 2 3 4 5\n5 4 3 2 1", env={"MPX_NGPUS": "64"})
+    assert r.returncode == 2 and "MPX_ALLOW_SHARED" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
 def test_lab1_gpu_multi_part():
-    r = run("labs/lab1/src/to_plot_hip_exe", "0\n0\n5\n1 2 3 4 5\n5 4 3 2 1", env={"MPX_NGPUS": "3"})
+    r = run("labs/lab1/src/to_plot_hip_exe", "0\n0\n5\n1 2 3 4 5\n5 4 3 2 1",
+            env={"MPX_NGPUS": "3", "MPX_ALLOW_SHARED": "1"})
     assert r.returncode == 0, r.stderr
     assert r.stdout.split("\n", 1)[1] == ("-4.0000000000e+00 -2.0000000000e+00 0.0000000000e+00 "
                                           "2.0000000000e+00 4.0000000000e+00 ")
@@ -234,6 +242,6 @@ def test_lab3_gpu_multi_part_matches_cpu(path, tmp_path):
     ref, got = tmp_path / "ref.data", tmp_path / "got.data"
     assert run("labs/lab3/src/cpu_omp_exe", f"{src}\n{ref}\n{classes}").returncode == 0
     r = run("labs/lab3/src/to_plot_hip_exe", f"0\n0\n{src}\n{got}\n{classes}",
-            env={"MPX_NGPUS": "5", "MPX_LAB3_PATH": path})
+            env={"MPX_NGPUS": "5", "MPX_LAB3_PATH": path, "MPX_ALLOW_SHARED": "1"})
     assert r.returncode == 0, r.stderr
     assert got.read_bytes() == ref.read_bytes()

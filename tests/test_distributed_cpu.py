@@ -70,6 +70,24 @@ def conv_worker(ctx, h, w, filt, overlap, outdir):
         torch.save(got, os.path.join(outdir, f"conv_{filt}.pt"))
 
 
+def stream_worker(ctx, h, w, filt, steps):
+    """Streaming conv (input = previous step's output): N ranks == one device
+    running the same frame sequence on the whole image; then a reload."""
+    from cuda_mpi_openmp_amd.models.edge import stream_reference
+
+    det = SlabEdgeDetector(ctx, h, w, filt, stream=True)
+    s = det.slab
+    for seed, k in ((11, steps), (12, steps + 1)):
+        full = _img(h, w, seed)
+        det.load(full[s.row0:s.row0 + s.rows])
+        for _ in range(k):
+            det.step()
+        got = parallel.gather_slabs(det.stream_out.contiguous(), s, ctx)
+        if ctx.rank == 0:
+            assert torch.equal(got, stream_reference(full, filt, k)), f"streaming conv differs ({filt}, {k} steps)"
+    det.close()
+
+
 def jacobi_worker(ctx, rows, cols, iters, outdir, tag):
     sol = SlabJacobi(ctx, rows, cols, check_every=5)
     sol.set_boundary(top=1.0, left=0.5)
@@ -198,6 +216,11 @@ def test_all_workloads_decomposed_uneven(world):
 @pytest.mark.parametrize("filt", ["sobel5", "roberts", "sobel3"])
 def test_slab_conv_equals_single(world, filt, tmp_path):
     run_world(world, "conv_worker", 37, 29, filt, True, str(tmp_path))
+
+
+@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (8, "sobel5_dense")])
+def test_slab_conv_stream_equals_one_device(world, filt):
+    run_world(world, "stream_worker", 8 * 5 + 5, 21, filt, 4)
 
 
 @pytest.mark.parametrize("mode", [False, "pipeline"])

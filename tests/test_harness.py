@@ -78,9 +78,9 @@ def _copy_lab(tmp_path, lab):
     return dst
 
 
-def _run_test(args, cwd):
+def _run_test(args, cwd, env=None):
     return subprocess.run([sys.executable, os.path.join(ROOT, "run_test.py"), *args], cwd=cwd, capture_output=True,
-                          text=True, timeout=600)
+                          text=True, timeout=600, env=dict(os.environ, **(env or {})))
 
 
 def test_harness_lab2_cpu_binaries(tmp_path):
@@ -185,10 +185,40 @@ def test_harness_lab2_gpu_n_gpus_warmup(tmp_path):
     lab = _copy_lab(tmp_path, "lab2")
     r = _run_test(["--binary_path_cuda", str(lab / "src" / "to_plot_hip_exe"), "--k_times", "2", "--kernel_sizes",
                    json.dumps([[[0, 0], [0, 0]]]), "--n_gpus", "2", "--warmup", "2", "--synthetic", "640x480"],
-                  tmp_path)
+                  tmp_path, env={"MPX_ALLOW_SHARED": "1"})  # the one-GPU box rehearses 2 parts on one device
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     df = pd.read_csv(lab / "src" / "stats_to_plot_hip_exe.csv")
     assert df["test_verification_result"].all() and (df["n_gpus"] == 2).all()
+    assert (df["devices_used"] == 1).all()  # ...and the CSV says so
+
+
+def test_harness_refuses_n_gpus_beyond_visible(tmp_path):
+    """--n_gpus N with fewer visible GPUs refuses to run (exit
+    2) instead of writing an N-GPU row measured on fewer devices."""
+    from cuda_mpi_openmp_amd.parallel.launch import visible_devices
+
+    lab = _copy_lab(tmp_path, "lab2")
+    n = max(2, visible_devices() + 1)
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--k_times", "1", "--kernel_sizes",
+                   "[[null, null]]", "--n_gpus", str(n)], tmp_path, env={"MPX_ALLOW_SHARED": "0"})
+    assert r.returncode == 2 and "refusing" in r.stderr, r.stderr[-2000:]
+    assert not list((lab / "src").glob("stats_*.csv"))
+
+
+def test_visible_devices_from_sysfs(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the KFD topology (no HIP runtime)."""
+    from cuda_mpi_openmp_amd.parallel import launch
+
+    for i, ver in enumerate([0, 90500, 90500, 0, 90500]):  # CPU nodes report 0
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {ver}\nsimd_count 8\n")
+    assert launch._kfd_gpu_count(str(tmp_path)) == 3
+    assert launch._kfd_gpu_count(str(tmp_path / "missing")) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert launch._visible_filter(3) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert launch._visible_filter(3) == 0
 
 
 @pytest.mark.parametrize("elem_type", ["int", "float", "uchar"])

@@ -268,3 +268,23 @@ def test_gpu_radix_variants(gpu, variant, kind, n):
     _native.check(L.mpx_sort_variant(d.data_ptr(), n, dt, ws.data_ptr(), nb, variant, _native.stream_of(d)))
     assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
     _native.check(L.mpx_sort_ws_status(ws.data_ptr(), n, dt))  # no look-back wait gave up
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 2, 3])
+def test_gpu_sort_ws_status_ignores_stale_workspace(gpu, variant):
+    """A recycled workspace full of 0xff bytes must not make mpx_sort_ws_status
+    report a look-back give-up after a reduce-then-scan sort (which never
+    waits): every schedule clears the flag it reads."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    n = (1 << 18) + 1001  # above the onesweep crossover: AUTO picks reduce-then-scan
+    a = random_array("int", n, seed=77)
+    d = torch.from_numpy(a.copy()).to(gpu)
+    nb = int(L.mpx_sort_workspace_bytes(n, 0))
+    ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=gpu)
+    _native.check(L.mpx_sort_variant(d.data_ptr(), n, 0, ws.data_ptr(), nb, variant, _native.stream_of(d)))
+    torch.cuda.synchronize()
+    assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
+    _native.check(L.mpx_sort_ws_status(ws.data_ptr(), n, 0))
