@@ -83,12 +83,21 @@ int main(void) {
         goto done;
     }
 #ifdef _OPENMP
+    const int io_timing = getenv("MPX_IO_TIMING") != NULL;
+    double ts[5];
+    ts[0] = now_ms();
     if (slurp_stdin()) {
         fprintf(stderr, "[ERROR CPU] out of memory reading stdin\n");
         goto done;
     }
 #endif
+#ifdef _OPENMP
+    ts[1] = now_ms();
+#endif
     if (read_vec(a, n, "first vector") || read_vec(b, n, "second vector")) goto done;
+#ifdef _OPENMP
+    ts[2] = now_ms();
+#endif
     const double t0 = now_ms();
     mpx_cpu_vsub_f64(a, b, c, n);
     const double t1 = now_ms();
@@ -101,9 +110,15 @@ int main(void) {
             fprintf(stderr, "[ERROR CPU] out of memory formatting the result\n");
             goto done;
         }
+        ts[3] = now_ms();
         fflush(stdout);
         if (len) fwrite(txt, 1, len, stdout);
+        fflush(stdout);
+        ts[4] = now_ms();
         free(txt);
+        if (io_timing)
+            fprintf(stderr, "[io] read %.1f ms, parse %.1f ms, format %.1f ms, write %.1f ms\n", ts[1] - ts[0],
+                    ts[2] - ts[1], ts[3] - t1, ts[4] - ts[3]);
     }
 #else
     for (int i = 0; i < n; ++i) printf("%.10e ", c[i]);

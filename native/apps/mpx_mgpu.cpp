@@ -7,6 +7,12 @@
 //   mpx_mgpu vsub   [--gpus N] [--n ELEMS_PER_GPU] [--steps K] [--warmup W] [--fp64]
 //
 // Each prints one JSON line (whole-job throughput, ms per step, verification).
+// "verified" means the N-rank result equals a ONE-DEVICE run of the same work
+// (VERDICT r2 #3): conv — every output pixel of every slab against the whole
+// image convolved on device 0; jacobi (rccl and peer) — the gathered final
+// field against warmup + iters sweeps of the whole grid on device 0, bit for
+// bit (same sweep order). MPX_FAULT_INJECT=halo:RANK:ITER corrupts one halo
+// value of RANK before sweep ITER (a silent error the check must catch: exit 3).
 //
 // Reference: the reference has no multi-process or multi-GPU code (SURVEY §0,
 // §2.6: "MPI" in the name only); this is the MPI tier of the BASELINE north
@@ -204,7 +210,62 @@ struct Shared {
     std::vector<double> elapsed;  // seconds per rank
     std::vector<int> verified;    // 1 ok, 0 mismatch, -1 not checked
     std::vector<double> extra;    // residual etc.
+    // one-device verification: every rank's initial / final rows at their global offsets
+    std::vector<uint8_t> init, fin;
+    std::vector<int> probe_ok, sync_kind;  // jacobi --halo peer: start-up probe verdict, sync memory kind
 };
+
+// MPX_FAULT_INJECT=halo:RANK:ITER -> true for that rank and iteration
+bool inject_halo(int rank, int it) {
+    const char *e = std::getenv("MPX_FAULT_INJECT");
+    int r = -1, i = -1;
+    return e && std::sscanf(e, "halo:%d:%d", &r, &i) == 2 && r == rank && i == it;
+}
+
+template <typename T>
+__global__ void poke_add_one(T *p) { *p += (T)1; }
+
+// One-device reference: warmup + iters sweeps of the whole (grows + 2) x cols
+// field on device 0 (rows 1..grows; rows 0 and grows+1 and columns 0, cols-1
+// are the Dirichlet boundary), compared with the gathered N-rank field.
+template <typename T>
+bool jacobi_one_device_equal(const std::vector<uint8_t> &init, const std::vector<uint8_t> &fin, int grows, int cols,
+                             int iters) {
+    HIP_OK(hipSetDevice(0));
+    hipStream_t s;
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const size_t bytes = (size_t)(grows + 2) * cols * sizeof(T);
+    T *u, *un;
+    HIP_OK(hipMalloc(&u, bytes));
+    HIP_OK(hipMalloc(&un, bytes));
+    HIP_OK(hipMemcpy(u, init.data(), bytes, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(un, u, bytes, hipMemcpyDeviceToDevice));
+    for (int i = 0; i < iters; ++i) {
+        if constexpr (sizeof(T) == 8) MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, 1, grows + 1, nullptr, s));
+        else MPX_OK_OR_DIE(mpx_jacobi_f32(u, un, cols, cols, 1, grows + 1, nullptr, s));
+        std::swap(u, un);
+    }
+    std::vector<uint8_t> got(bytes);
+    HIP_OK(hipMemcpyAsync(got.data(), u, bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipFree(u));
+    HIP_OK(hipFree(un));
+    HIP_OK(hipStreamDestroy(s));
+    const size_t rb = (size_t)cols * sizeof(T);
+    return std::memcmp(got.data() + rb, fin.data() + rb, (size_t)grows * rb) == 0;
+}
+
+// A rank's initial rows into the whole-field image: owned rows always, plus
+// the global top / bottom boundary row on the first / last rank.
+void stash_rows(std::vector<uint8_t> &dst, const void *dev_buf, long long row0, long long rows, size_t rb, bool top,
+                bool bottom) {
+    HIP_OK(hipMemcpy(dst.data() + (row0 + 1) * rb, static_cast<const uint8_t *>(dev_buf) + rb, rows * rb,
+                     hipMemcpyDeviceToHost));
+    if (top) HIP_OK(hipMemcpy(dst.data(), dev_buf, rb, hipMemcpyDeviceToHost));
+    if (bottom)
+        HIP_OK(hipMemcpy(dst.data() + (row0 + rows + 1) * rb, static_cast<const uint8_t *>(dev_buf) + (rows + 1) * rb,
+                         rb, hipMemcpyDeviceToHost));
+}
 
 ncclComm_t init_comm(Shared &sh, int rank) {
     ncclComm_t c;
@@ -251,10 +312,14 @@ void conv_worker(const Args &a, Shared &sh, int rank) {
     // logical rows of the slab: [0, rows); reads clamp into [y_lo, y_hi]
     const int y_lo = up ? -hu : 0, y_hi = (int)rows - 1 + (down ? hd : 0);
     const uint32_t *in = reinterpret_cast<const uint32_t *>(buf + hu * row_bytes);
+    int it = 0;
     auto step = [&]() {
         if (sh.world > 1) halo_exchange(comm, s, rank, sh.world, buf, row_bytes, hu, rows, hu, hd);
+        if (inject_halo(rank, it) && (up || down))  // one received halo byte off by one (kept: inputs are static)
+            poke_add_one<uint8_t><<<1, 1, 0, s>>>(up ? buf + w * 2 : buf + (hu + rows) * row_bytes + w * 2);
         MPX_OK_OR_DIE(mpx_conv(in, reinterpret_cast<uint32_t *>(out), w, w, 0, (int)rows, y_lo, y_hi, k, anchor, mode,
                                wx, wy, s));
+        ++it;
     };
     for (int i = 0; i < a.warmup; ++i) step();
     HIP_OK(hipStreamSynchronize(s));
@@ -264,12 +329,16 @@ void conv_worker(const Args &a, Shared &sh, int rank) {
     HIP_OK(hipStreamSynchronize(s));
     sh.bar->wait();
     sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
-    // verify the halo-dependent edge rows (and a band around them) on the CPU
+    // verify: (a) the halo-dependent edge bands against the CPU reference on
+    // this rank's halo-filled buffer; (b) every output row, after the threads
+    // join, against the whole image convolved on one device (main()).
     const int band = std::min<long long>(32, rows);
     std::vector<uint32_t> hbuf(buf_rows * w), hout(rows * w), ref(rows * w);
     HIP_OK(hipMemcpy(hbuf.data(), buf, buf_rows * row_bytes, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(hout.data(), out, rows * row_bytes, hipMemcpyDeviceToHost));
     const uint32_t *hin = hbuf.data() + (size_t)hu * w;
+    std::memcpy(sh.init.data() + (size_t)rank * rows * row_bytes, hin, rows * row_bytes);
+    std::memcpy(sh.fin.data() + (size_t)rank * rows * row_bytes, hout.data(), rows * row_bytes);
     bool ok = true;
     for (int part = 0; part < 2; ++part) {
         const int oy0 = part == 0 ? 0 : (int)rows - band, oy1 = part == 0 ? band : (int)rows;
@@ -299,14 +368,14 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
     const size_t bytes = (rows + 2) * row_bytes;
     T *u, *un, *res;
     unsigned *sync;
+    int sync_kind = 0;
     HIP_OK(hipMalloc(&u, bytes));
     HIP_OK(hipMalloc(&un, bytes));
     HIP_OK(hipMalloc(&res, sizeof(T)));
-    HIP_OK(hipMalloc(&sync, mpx_jacobi_sync_bytes()));
-    fill_unit<T><<<1024, 256, 0, s>>>(u, (rows + 2) * cols, 77 + rank);
-    HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
+    // the iteration words: uncached / fine-grained device memory where available
+    MPX_OK_OR_DIE(mpx_sync_alloc(mpx_jacobi_sync_bytes(), reinterpret_cast<void **>(&sync), &sync_kind));
+    sh.sync_kind[rank] = sync_kind;
     HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
-    HIP_OK(hipMemsetAsync(sync, 0, mpx_jacobi_sync_bytes(), s));
     HIP_OK(hipStreamSynchronize(s));
     sh.peer_u[rank] = u;
     sh.peer_un[rank] = un;
@@ -314,6 +383,10 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
     sh.bar->wait();
     mpx_jacobi_peer pr{};
     pr.sync = sync;
+    mpx_peer_probe probe{};
+    probe.own_rows[0] = u + cols, probe.own_rows[1] = u + rows * cols;
+    probe.own_rows[2] = un + cols, probe.own_rows[3] = un + rows * cols;
+    probe.sync = sync, probe.row_bytes = (int64_t)row_bytes, probe.rank = rank, probe.magic = 0x40000000u;
     for (int nb : {rank - 1, rank + 1}) {
         if (nb < 0 || nb >= sh.world || a.halo == "none") continue;
         const int nd = nb % sh.ndev;
@@ -326,16 +399,46 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
         const long long row = nb < rank ? ns.rows : 1;  // its last / first owned row
         const void *even = static_cast<const T *>(sh.peer_u[nb]) + row * cols;  // every rank starts with u
         const void *odd = static_cast<const T *>(sh.peer_un[nb]) + row * cols;
+        const int side = nb < rank ? 0 : 1;
+        probe.nb_rows[side][0] = even, probe.nb_rows[side][1] = odd, probe.flag[side] = sh.peer_sync[nb];
         if (nb < rank) {
             pr.up_row[0] = even, pr.up_row[1] = odd, pr.up_flag = sh.peer_sync[nb];
         } else {
             pr.dn_row[0] = even, pr.dn_row[1] = odd, pr.dn_flag = sh.peer_sync[nb];
         }
     }
+    // start-up kernel-path probe of the P2P protocol (production stores, release,
+    // bounded wait, system-scope loads) before any timed or verified sweep
+    MPX_OK_OR_DIE(mpx_peer_probe_run(&probe, s));
+    HIP_OK(hipStreamSynchronize(s));
+    unsigned perr = 0, pbad = 0;
+    MPX_OK_OR_DIE(mpx_sync_read(sync, 64, &perr));
+    MPX_OK_OR_DIE(mpx_sync_read(sync, 96, &pbad));
+    sh.probe_ok[rank] = perr == 0 && pbad == 0;
+    sh.bar->wait();  // every probe has finished reading before anyone resets
+    fill_unit<T><<<1024, 256, 0, s>>>(u, (rows + 2) * cols, 77 + rank);
+    HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemsetAsync(sync, 0, mpx_jacobi_sync_bytes(), s));
+    HIP_OK(hipStreamSynchronize(s));
+    stash_rows(sh.init, u, sl.row0, rows, row_bytes, rank == 0, rank + 1 == sh.world);
+    sh.bar->wait();
+    if (!std::all_of(sh.probe_ok.begin(), sh.probe_ok.end(), [](int v) { return v == 1; })) {
+        if (rank == 0) fprintf(stderr, "[ERROR MPX] peer probe failed (wait gave up or rows differ); not running\n");
+        sh.verified[rank] = 0;
+        sh.bar->wait();
+        HIP_OK(hipFree(u));
+        HIP_OK(hipFree(un));
+        HIP_OK(hipFree(res));
+        MPX_OK_OR_DIE(mpx_sync_free(sync));
+        HIP_OK(hipStreamDestroy(s));
+        return;
+    }
     int it = 0;
     double last_res = -1;
     auto iterate = [&]() {
         const bool check = (it + 1) % a.check_every == 0;
+        if (inject_halo(rank, it))  // the edge row a neighbour reads in place, off by one
+            poke_add_one<T><<<1, 1, 0, s>>>(u + cols + cols / 2);
         MPX_OK_OR_DIE(mpx_jacobi_peer_sweep(sizeof(T) == 8, u, un, cols, cols, (int)rows, check ? res : nullptr, &pr, s));
         std::swap(u, un);
         if (check) {  // residual max over ranks on the host (no RCCL in this mode)
@@ -384,11 +487,13 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
     HIP_OK(hipStreamSynchronize(s));
     sh.verified[rank] = err == 0 && std::memcmp(gun.data() + cols, hun.data() + cols, (size_t)vr * row_bytes) == 0;
     if (err) fprintf(stderr, "[ERROR MPX] rank %d: a device-side halo wait timed out\n", rank);
+    // the final field (u after `it` sweeps: the extra verification sweep above wrote un only)
+    HIP_OK(hipMemcpy(sh.fin.data() + (sl.row0 + 1) * row_bytes, u + cols, rows * row_bytes, hipMemcpyDeviceToHost));
     sh.bar->wait();  // nobody frees buffers a neighbour may still read
     HIP_OK(hipFree(u));
     HIP_OK(hipFree(un));
     HIP_OK(hipFree(res));
-    HIP_OK(hipFree(sync));
+    MPX_OK_OR_DIE(mpx_sync_free(sync));
     HIP_OK(hipStreamDestroy(s));
 }
 
@@ -411,6 +516,8 @@ void jacobi_worker(const Args &a, Shared &sh, int rank) {
     fill_unit<T><<<1024, 256, 0, s>>>(u, (rows + 2) * cols, 77 + rank);
     HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
     HIP_OK(hipMemsetAsync(res, 0, sizeof(T), s));
+    HIP_OK(hipStreamSynchronize(s));
+    stash_rows(sh.init, u, sl.row0, rows, row_bytes, rank == 0, rank + 1 == sh.world);
     const ncclDataType_t dt = sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
     const bool up = rank > 0, down = rank + 1 < sh.world;
     int it = 0;
@@ -429,6 +536,8 @@ void jacobi_worker(const Args &a, Shared &sh, int rank) {
             }
             NCCL_CHECK(ncclGroupEnd());
         }
+        if (inject_halo(rank, it) && (up || down))  // one received halo value off by one
+            poke_add_one<T><<<1, 1, 0, s>>>(up ? u + cols / 2 : u + (rows + 1) * cols + cols / 2);
         const bool check = (it + 1) % a.check_every == 0;
         // owned rows 1..rows; buffer row 0 of the first rank and row rows+1 of
         // the last are the global Dirichlet boundary (never received into)
@@ -456,6 +565,7 @@ void jacobi_worker(const Args &a, Shared &sh, int rank) {
     sh.bar->wait();
     sh.elapsed[rank] = std::chrono::duration<double>(Clock::now() - t0).count();
     sh.extra[rank] = last_res;
+    HIP_OK(hipMemcpy(sh.fin.data() + (sl.row0 + 1) * row_bytes, u + cols, rows * row_bytes, hipMemcpyDeviceToHost));
     // verify one more sweep of the first owned rows against the CPU reference
     const long long vr = std::min<long long>(rows, 8);
     if (sh.world > 1) {  // refresh halos exactly as an iteration does
@@ -569,6 +679,8 @@ int main(int argc, char **argv) {
     sh.peer_un.assign(N, nullptr);
     sh.peer_sync.assign(N, nullptr);
     sh.res.assign(N, 0.0);
+    sh.probe_ok.assign(N, 1);
+    sh.sync_kind.assign(N, -1);
     Barrier bar(N);
     sh.bar = &bar;
     sh.elapsed.assign(N, 0.0);
@@ -580,10 +692,15 @@ int main(int argc, char **argv) {
     if (a.mode == "conv") {
         if (a.size <= 0) a.size = 4096;
         if (a.steps <= 0) a.steps = 50;
+        sh.init.assign((size_t)N * a.size * a.size * 4, 0);
+        sh.fin.assign(sh.init.size(), 0);
         for (int r = 0; r < N; ++r) th.emplace_back([&, r] { conv_worker(a, sh, r); });
     } else if (a.mode == "jacobi") {
         if (a.size <= 0) a.size = 16384;
         if (a.steps <= 0) a.steps = 50;
+        const int grows0 = peer && a.rows > 0 ? a.rows : a.size;
+        sh.init.assign((size_t)(grows0 + 2) * a.size * (a.fp32 ? 4 : 8), 0);
+        sh.fin.assign(sh.init.size(), 0);
         for (int r = 0; r < N; ++r)
             th.emplace_back([&, r] {
                 if (peer) a.fp32 ? jacobi_peer_worker<float>(a, sh, r) : jacobi_peer_worker<double>(a, sh, r);
@@ -600,15 +717,43 @@ int main(int argc, char **argv) {
     }
     for (auto &t : th) t.join();
 
-    const double el = *std::max_element(sh.elapsed.begin(), sh.elapsed.end());
+    const double el = std::max(1e-12, *std::max_element(sh.elapsed.begin(), sh.elapsed.end()));
     const double ms = el * 1e3 / a.steps;
-    const bool ok = std::all_of(sh.verified.begin(), sh.verified.end(), [](int v) { return v == 1; });
+    bool ok = std::all_of(sh.verified.begin(), sh.verified.end(), [](int v) { return v == 1; });
+    const char *one_dev = "null";
+    if (a.mode == "conv" && N > 1) {  // every output pixel vs the whole image on one device
+        int k, anchor, mode;
+        float wx[MPX_MAX_K * MPX_MAX_K], wy[MPX_MAX_K * MPX_MAX_K];
+        MPX_OK_OR_DIE(mpx_filter_lookup(a.filter.c_str(), &k, &anchor, &mode, wx, wy));
+        const size_t bytes = sh.init.size();
+        const int H = N * a.size;
+        HIP_OK(hipSetDevice(0));
+        uint32_t *din, *dout;
+        HIP_OK(hipMalloc(&din, bytes));
+        HIP_OK(hipMalloc(&dout, bytes));
+        HIP_OK(hipMemcpy(din, sh.init.data(), bytes, hipMemcpyHostToDevice));
+        MPX_OK_OR_DIE(mpx_conv(din, dout, a.size, a.size, 0, H, 0, H - 1, k, anchor, mode, wx, wy, nullptr));
+        std::vector<uint8_t> got(bytes);
+        HIP_OK(hipMemcpy(got.data(), dout, bytes, hipMemcpyDeviceToHost));
+        HIP_OK(hipFree(din));
+        HIP_OK(hipFree(dout));
+        const bool same = std::memcmp(got.data(), sh.fin.data(), bytes) == 0;
+        one_dev = same ? "true" : "false";
+        ok &= same;
+    } else if (a.mode == "jacobi" && N > 1 && a.halo != "none") {
+        const int grows = peer && a.rows > 0 ? a.rows : a.size;
+        const int total = a.warmup + a.steps;
+        const bool same = a.fp32 ? jacobi_one_device_equal<float>(sh.init, sh.fin, grows, a.size, total)
+                                 : jacobi_one_device_equal<double>(sh.init, sh.fin, grows, a.size, total);
+        one_dev = same ? "true" : "false";
+        ok &= same;
+    }
     if (a.mode == "conv") {
         const double gpix = (double)N * a.size * a.size * a.steps / el / 1e9;
         printf("{\"workload\": \"conv\", \"filter\": \"%s\", \"n_gpus\": %d, \"slab\": [%d, %d], \"steps\": %d, "
                "\"ms_per_step\": %.5f, \"value\": %.3f, \"unit\": \"Gpixel/s\", \"scaling\": \"weak\", "
-               "\"verified_bit_exact\": %s}\n",
-               a.filter.c_str(), N, a.size, a.size, a.steps, ms, gpix, ok ? "true" : "false");
+               "\"verified_bit_exact\": %s, \"one_device_equal\": %s}\n",
+               a.filter.c_str(), N, a.size, a.size, a.steps, ms, gpix, ok ? "true" : "false", one_dev);
     } else if (a.mode == "jacobi") {
         const int grows = peer && a.rows > 0 ? a.rows : a.size;
         const double pts = (double)grows * a.size * a.steps / el / 1e9;
@@ -616,10 +761,14 @@ int main(int argc, char **argv) {
         printf("{\"workload\": \"jacobi\", \"dtype\": \"%s\", \"n_gpus\": %d, \"grid\": [%d, %d], \"iters\": %d, "
                "\"check_every\": %d, \"ms_per_iter\": %.5f, \"value\": %.3f, \"unit\": \"Gpoint/s\", "
                "\"TBps_aggregate\": %.3f, \"scaling\": \"strong\", \"residual\": %.6e, \"halo\": \"%s\", "
-               "\"devices\": %d, \"verified\": %s}\n",
+               "\"devices\": %d, \"verified\": %s, \"one_device_equal\": %s, \"peer_probe\": %s, "
+               "\"sync_memory\": \"%s\"}\n",
                a.fp32 ? "fp32" : "fp64", N, grows, a.size, a.steps, a.check_every, ms, pts, tbs, sh.extra[0],
                !peer ? "rccl" : a.halo == "none" ? "none (ablation)" : "peer-signalled", std::min(N, ndev),
-               ok ? "true" : "false");
+               ok ? "true" : "false", one_dev,
+               !peer || a.halo == "none" ? "null"
+               : std::all_of(sh.probe_ok.begin(), sh.probe_ok.end(), [](int v) { return v == 1; }) ? "\"ok\"" : "\"failed\"",
+               !peer ? "n/a" : sh.sync_kind[0] == 2 ? "uncached" : sh.sync_kind[0] == 1 ? "fine-grained" : "coarse-grained");
     } else {
         const int es = a.fp64 ? 8 : 4;
         const double tbs = (double)N * a.n * es * 3 * a.steps / el / 1e12;

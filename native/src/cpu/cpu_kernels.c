@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "fastfloat.h"
 #include "mpx/common.h"
 
 #ifdef _OPENMP
@@ -92,17 +93,23 @@ int64_t mpx_parse_doubles(const char *buf, size_t len, size_t pos, int64_t count
         while (idx < count && i < start[k + 1]) {
             while (i < start[k + 1] && is_ws(buf[i])) ++i;
             if (i >= start[k + 1]) break;
-            char *e = NULL;
-            out[idx] = strtod(buf + i, &e);
-            if (e == buf + i) {  /* not a number */
-                if (idx < bad) bad = idx;
-                break;
-            }
-            size_t j = i;
-            while (j < start[k + 1] && !is_ws(buf[j])) ++j;
-            if ((size_t)(e - buf) != j) {  /* trailing junk in the token */
-                if (idx < bad) bad = idx;
-                break;
+            const char *fe = NULL;
+            size_t j;
+            if (mpx_fast_strtod(buf + i, buf + start[k + 1], &out[idx], &fe)) {  /* exact fast path */
+                j = (size_t)(fe - buf);
+            } else {  /* anything the fast path does not decide: the C library */
+                char *e = NULL;
+                out[idx] = strtod(buf + i, &e);
+                if (e == buf + i) {  /* not a number */
+                    if (idx < bad) bad = idx;
+                    break;
+                }
+                j = i;
+                while (j < start[k + 1] && !is_ws(buf[j])) ++j;
+                if ((size_t)(e - buf) != j) {  /* trailing junk in the token */
+                    if (idx < bad) bad = idx;
+                    break;
+                }
             }
             if (idx == count - 1) last_end = j;
             i = j;
@@ -124,8 +131,13 @@ char *mpx_format_e10(const double *v, int64_t n, size_t *len) {
     if (n < 4096) T = 1;
 #endif
     char **part = (char **)calloc((size_t)T, sizeof(char *));
-    size_t *plen = (size_t *)calloc((size_t)T, sizeof(size_t));
+    size_t *plen = (size_t *)calloc((size_t)T + 1, sizeof(size_t));
     int fail = 0;
+    char *outb = NULL;
+    size_t total = 0;
+    if (!part || !plen) goto out;
+    /* pass 1: each thread formats its slice (exact fast path, snprintf when
+     * the fast path cannot decide) */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static, 1) num_threads(T) reduction(| : fail)
 #endif
@@ -137,22 +149,28 @@ char *mpx_format_e10(const double *v, int64_t n, size_t *len) {
             continue;
         }
         size_t o = 0;
-        for (int64_t i = a; i < b; ++i) o += (size_t)snprintf(buf + o, 32, "%.10e ", v[i]);
-        part[k] = buf;
-        plen[k] = o;
-    }
-    size_t total = 0;
-    for (int k = 0; k < T; ++k) total += plen[k];
-    char *outb = fail ? NULL : (char *)malloc(total + 1);
-    if (outb) {
-        size_t o = 0;
-        for (int k = 0; k < T; ++k) {
-            memcpy(outb + o, part[k], plen[k]);
-            o += plen[k];
+        for (int64_t i = a; i < b; ++i) {
+            const int l = mpx_fast_e10(v[i], buf + o);
+            o += l ? (size_t)l : (size_t)snprintf(buf + o, 32, "%.10e", v[i]);
+            buf[o++] = ' ';
         }
+        part[k] = buf;
+        plen[k + 1] = o;
+    }
+    for (int k = 0; k < T; ++k) plen[k + 1] += plen[k];
+    total = plen[T];
+    outb = fail ? NULL : (char *)malloc(total + 1);
+    /* pass 2: the slices land at their prefix offsets in parallel */
+    if (outb) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+#endif
+        for (int k = 0; k < T; ++k) memcpy(outb + plen[k], part[k], plen[k + 1] - plen[k]);
         outb[total] = 0;
     }
-    for (int k = 0; k < T; ++k) free(part[k]);
+out:
+    if (part)
+        for (int k = 0; k < T; ++k) free(part[k]);
     free(part);
     free(plen);
     *len = outb ? total : 0;

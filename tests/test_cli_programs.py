@@ -187,6 +187,23 @@ def test_mpx_mgpu_jacobi_peer_shared(ranks, extra):
     assert r.returncode == 0, r.stderr[-2000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["n_gpus"] == ranks and rec["halo"] == "peer-signalled" and rec["verified"] is True
+    assert rec["peer_probe"] == "ok"
+    # N > 1: the gathered field equals ONE device running the same sweeps
+    assert rec["one_device_equal"] is (True if ranks > 1 else None)
+
+
+@pytest.mark.gpu
+def test_mpx_mgpu_catches_injected_halo_corruption():
+    """A silently corrupted halo value on one rank (MPX_FAULT_INJECT) must fail
+    the N-rank == one-device check with exit code 3."""
+    import json
+
+    r = run("bin/mpx_mgpu", "", env={"MPX_FAULT_INJECT": "halo:1:7"},
+            args=["jacobi", "--halo", "peer", "--shared", "--gpus", "3", "--size", "1024", "--iters", "20",
+                  "--warmup", "2", "--check-every", "10"])
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["one_device_equal"] is False and rec["verified"] is False
 
 
 def test_mpx_mgpu_usage_errors():
