@@ -12,7 +12,7 @@ import torch
 from .. import _native
 from .edge import check_image
 
-PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3, "mfma64": 4}
+PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3, "mfma64": 4, "mfma8": 5}
 PATH_NAMES = {v: k for k, v in PATHS.items()}
 MAX_CLASSES = 32
 
@@ -47,6 +47,8 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``fast``   — fp32 packed-VALU distances;
       * ``mfma``   — fp32 MFMA distance GEMM (v_mfma_f32_32x32x2f32);
       * ``mfma64`` — fp64 MFMA distance GEMM (v_mfma_f64_16x16x4_f64);
+      * ``mfma8``  — exact int8 MFMA distance GEMM (v_mfma_i32_32x32x16_i8,
+        16-bit fixed-point weights in two int8 limbs, int32 keys);
       * ``auto``   — ``fast`` (measured fastest at every nc on MI355X: the f32
         MFMA shares the VALU's fp32 datapath on gfx950).
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a

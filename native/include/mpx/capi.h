@@ -122,6 +122,11 @@ int mpx_classify_ex(uint32_t *img, int64_t npix, int nc, const double *mu, const
 /* Host-side plan: the path `path` resolves to for these statistics (DIRECT when
  * the fp32 decision cannot be proven) and the fp32 decision margin. <0 = error. */
 int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin);
+/* MFMA8 integer weights as the kernel uses them (CPU emulation in the tests):
+ * a, b: 32 x 16 int8 limbs per class and slot; c: 32 accumulator constants;
+ * *t2: decision margin in key units. MPX_ERR_UNSUPPORTED when no bound exists. */
+int mpx_classify_i8_params(int nc, const double *mu, const double *inv, int8_t *a, int8_t *b, int32_t *c,
+                           int32_t *t2);
 
 /* ---------------- native RCCL tier (inter-GPU transport) ---------------- */
 /*

@@ -51,7 +51,8 @@ enum mpx_classify_path {
     MPX_CLS_MFMA = 1,   /* fp32 MFMA distance GEMM, proven margin + exact fallback  */
     MPX_CLS_AUTO = 2,   /* FAST, or DIRECT when the fp32 margin cannot be proven    */
     MPX_CLS_FAST = 3,   /* fp32 packed-VALU distances, proven margin + fallback     */
-    MPX_CLS_MFMA64 = 4  /* fp64 MFMA distance GEMM, proven margin + exact fallback  */
+    MPX_CLS_MFMA64 = 4, /* fp64 MFMA distance GEMM, proven margin + exact fallback  */
+    MPX_CLS_MFMA8 = 5   /* exact int8 MFMA distance GEMM (int32 keys), proven margin */
 };
 
 /* lab5 element types (binary fixtures lab5/data/{int10,float10,uchar10}). */

@@ -36,6 +36,7 @@
 //     med3(best, key, second). A bias folded into the constant weight makes
 //     every computed value positive, so unsigned key order is value order.
 #include <algorithm>
+#include <utility>
 #include <cstdlib>
 
 #include "internal.hpp"
@@ -495,6 +496,164 @@ __global__ __launch_bounds__(256) void classify_mfma64_kernel(uint32_t *__restri
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// MFMA8: the distance GEMM in exact int8 x int8 -> int32 on
+// v_mfma_i32_32x32x16_i8 (BASELINE config 4 "MFMA
+// distance-GEMM").
+//   Features (K = 16, every one an exact int8): the six centred products
+//   P = q_i q_j (|P| <= 2^14) split as P = 256 h + l with h = (P + 128) >> 8 in
+//   [-64, 64] (byte 1 of P + 128) and l in [-128, 127] (byte 0 of P), the three
+//   centred channels q in [-128, 127], one zero slot; the constant term rides
+//   in the MFMA's accumulator input.
+//     half-wave 0 (k 0..7):  h(rr gg bb rg rb gb), r, g
+//     half-wave 1 (k 8..15): l(rr gg bb rg rb gb), b, 0
+//   Weights: the slot weights V (256 w for h slots, w for l and linear slots)
+//   as integers v = round(V / u) in 16 bits, split v = 256 a + b over two
+//   int8 GEMMs; the class constant round(w9 / u) is the accumulator input of
+//   the b GEMM. The int32 key of (pixel, class) is
+//       ((D_a << 8) + D_b) << 5 | class     (|.| < 2^31, checked on the host)
+//   — exact integer arithmetic, so the only error is the weight rounding,
+//   u/2 per unit of |feature|: the host bounds it (plus the reference chain's
+//   own error) and a pixel is decided only when its second-best key exceeds
+//   the best by more than 2 max_c tol_c / u; every other pixel is deferred to
+//   the exact fp64 chain at the end of the block (all lanes busy).
+//   A (weights): lane l holds A[class l & 31][k = 8 (l >> 5) .. +7] (loaded once)
+//   B (features): lane l holds B[k = 8 (l >> 5) .. +7][pixel l & 31]
+//   D: lane l, reg r holds class (r & 3) + 8 (r >> 2) + 4 (l >> 5), pixel l & 31
+// Per (pixel, class) the VALU spends 4 instructions (shift-add, shift-or tag,
+// med3, min) against fast32's ~9.
+// ---------------------------------------------------------------------------
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+struct I8Params {
+    uint64_t a[MPX_MAX_CLASSES][2];  // hi limbs: [class][half] = 8 int8 weights of k = 8 half .. +7
+    uint64_t b[MPX_MAX_CLASSES][2];  // lo limbs
+    int32_t c[MPX_MAX_CLASSES];      // round(w9 / u); padded classes: 2^26 - 64 (never the argmin)
+    int32_t T2;                      // decision margin in key units (key >> 5)
+};
+
+constexpr int kAmb8Cap = 2048;
+
+// (a << s) + b in one v_lshl_add_u32 (the compiler splits the shift-by-5 form
+// into shift + or + add chains)
+__device__ __forceinline__ int32_t lshl_add(int32_t a, int s, int32_t b) {
+    int32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
+    return r;
+}
+
+// (a << s) + K with K an inline constant (the class tag)
+template <int K>
+__device__ __forceinline__ int32_t lshl_add_k(int32_t a, int s) {
+    int32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "i"(K));
+    return r;
+}
+
+__device__ __forceinline__ int32_t imed3(int32_t a, int32_t b, int32_t c) {
+    int32_t r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int NREG, int RR>
+__device__ __forceinline__ void rank_reg(const i32x16 &da, const i32x16 &db, int32_t &B, int32_t &S) {
+    if constexpr (RR < NREG) {
+        const int32_t key = lshl_add(db[RR], 5, lshl_add_k<(RR & 3) + 8 * (RR >> 2)>(da[RR], 13));
+        S = imed3(B, key, S);
+        B = min(B, key);
+    }
+}
+
+template <int NREG, int... R>
+__device__ __forceinline__ void rank_regs(const i32x16 &da, const i32x16 &db, int32_t &B, int32_t &S,
+                                          std::integer_sequence<int, R...>) {
+    (rank_reg<NREG, R>(da, db, B, S), ...);
+}
+
+template <int NREG>
+__global__ __launch_bounds__(256) void classify_mfma8_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
+                                                             ClassParams cp, I8Params ip, uint32_t *amb) {
+    __shared__ int64_t s_amb[kAmb8Cap];
+    __shared__ uint32_t s_ambpx[kAmb8Cap];
+    __shared__ uint32_t s_namb;
+    if (threadIdx.x == 0) s_namb = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const long wa = (long)ip.a[col][h], wb = (long)ip.b[col][h];
+    i32x16 cinit;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cinit[r] = ip.c[(r & 3) + 8 * (r >> 2) + 4 * h];
+    // half 0 packs byte 1 of P + 128 (the h limbs), half 1 byte 0 of P (the l limbs)
+    const int add = h ? 0 : 128;
+    const uint32_t sel = h ? 0u : 1u;
+    const uint32_t selA = sel | ((4u + sel) << 8) | (0x0Cu << 16) | (0x0Cu << 24);  // [x.s, y.s, 0, 0]
+    const uint32_t selB = 0x0Cu | (0x0Cu << 8) | (sel << 16) | ((4u + sel) << 24);   // [0, 0, x.s, y.s]
+    const uint32_t selD = 0x0Cu | (0x0Cu << 8) | (0u << 16) | ((h ? 0x0Cu : 4u) << 24);  // [0, 0, x6, g | 0]
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    int64_t ch = wave;
+    uint4 qn = ch < nchunks ? v[ch * 32 + col] : uint4{};
+    for (; ch < nchunks; ch += nwaves) {
+        const uint4 q = qn;
+        if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        int32_t rb[4], rs[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int p = (int)(px[m] ^ 0x80808080u);  // bytes - 128, sign-extended below
+            const int r = __builtin_amdgcn_sbfe(p, 0, 8), g = __builtin_amdgcn_sbfe(p, 8, 8),
+                      b = __builtin_amdgcn_sbfe(p, 16, 8);
+            const uint32_t P0 = (uint32_t)(r * r + add), P1 = (uint32_t)(g * g + add), P2 = (uint32_t)(b * b + add);
+            const uint32_t P3 = (uint32_t)(r * g + add), P4 = (uint32_t)(r * b + add), P5 = (uint32_t)(g * b + add);
+            const uint32_t x6 = (uint32_t)(h ? b : r);
+            const uint32_t d0 = __builtin_amdgcn_perm(P1, P0, selA) | __builtin_amdgcn_perm(P3, P2, selB);
+            const uint32_t d1 = __builtin_amdgcn_perm(P5, P4, selA) | __builtin_amdgcn_perm((uint32_t)g, x6, selD);
+            const long feat = (long)(((uint64_t)d1 << 32) | d0);
+            const i32x16 da = __builtin_amdgcn_mfma_i32_32x32x16_i8(wa, feat, i32x16{}, 0, 0, 0);
+            const i32x16 db = __builtin_amdgcn_mfma_i32_32x32x16_i8(wb, feat, cinit, 0, 0, 0);
+            int32_t B = INT32_MAX, S = INT32_MAX;
+            // key = ((da << 8) + db) << 5 | tag as two v_lshl_add_u32:
+            // (da << 13) + tag first, then (db << 5) + that
+            rank_regs<NREG>(da, db, B, S, std::make_integer_sequence<int, 16>{});
+            B |= 4 * h;  // row tags (r & 3) + 8 (r >> 2) never set bit 2
+            S |= 4 * h;
+            const auto sb = __builtin_amdgcn_permlane32_swap((uint32_t)B, (uint32_t)B, false, false);
+            const auto ss = __builtin_amdgcn_permlane32_swap((uint32_t)S, (uint32_t)S, false, false);
+            const int32_t B0 = (int32_t)sb[0], B1 = (int32_t)sb[1], S0 = (int32_t)ss[0], S1 = (int32_t)ss[1];
+            rb[m] = min(B0, B1);
+            rs[m] = min(max(B0, B1), min(S0, S1));
+        }
+        if (h == 0) {
+            uint4 o;
+            uint32_t *op = &o.x;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                op[m] = (px[m] & 0x00ffffffu) | (((uint32_t)rb[m] & 31u) << 24);
+                // exact integers: the tag bits are below the shift
+                if (__builtin_expect((rs[m] >> 5) - (rb[m] >> 5) <= ip.T2, 0)) {
+                    if (amb) atomicAdd(amb, 1u);
+                    const uint32_t slot = atomicAdd(&s_namb, 1u);
+                    if (slot < (uint32_t)kAmb8Cap) {
+                        s_amb[slot] = (ch * 32 + col) * 4 + m;
+                        s_ambpx[slot] = px[m];
+                    } else {
+                        op[m] = classify_direct(px[m], nc, cp);
+                    }
+                }
+            }
+            v[ch * 32 + col] = o;
+        }
+    }
+    __syncthreads();
+    const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
+    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
+}
+
 // ---------------------------------------------------------------------------
 // Host: expanded fp32 weights and the rigorous decision margin.
 // ---------------------------------------------------------------------------
@@ -631,6 +790,87 @@ bool build_fast64(int nc, const double *mu, const double *inv, Fast64Params &fp)
     return true;
 }
 
+
+// Integer weights for MFMA8 (see the kernel): slot weights V_s as
+// v_s = round(V_s / u) with |v_s| <= 32639 (two int8 limbs), the constant as
+// c = round(w9 / u) in the accumulator; u is doubled until every key fits
+// int32 after the 5-bit class tag (|sum_s Fmax_s |v_s|| + |c| < 2^26). The
+// decision bound per class: u/2 per unit of feature magnitude (weight
+// rounding; the int32 arithmetic is exact) + u/2 (constant) + the reference
+// chain's error; T2 = ceil(2 max_c tol_c / u) + 1 in key units.
+constexpr int kSlots = 16;
+// slot -> (expanded weight index, scale, max |feature|)
+constexpr int kSlotW[kSlots] = {0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3, 4, 5, 8, -1};
+constexpr ld kSlotScale[kSlots] = {256, 256, 256, 256, 256, 256, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0};
+constexpr ld kSlotFmax[kSlots] = {64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 128, 128, 128, 128, 128, 0};
+
+bool build_i8(int nc, const double *mu, const double *inv, I8Params &ip) {
+    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
+    if (!expand_classes(nc, mu, inv, w, refb, psd)) return false;
+    ld vmax = 0, mag = 0;
+    for (int c = 0; c < nc; ++c)
+        for (int s = 0; s < kSlots; ++s)
+            if (kSlotW[s] >= 0) {
+                vmax = std::fmax(vmax, std::fabs(w[c][kSlotW[s]] * kSlotScale[s]));
+                mag = std::fmax(mag, std::fabs(w[c][kSlotW[s]]) * kPhiMax[kSlotW[s]]);
+            }
+    if (!(vmax > 0) || !(mag < 1e30L)) return false;
+    ld u = vmax / 32639;
+    long long v[MPX_MAX_CLASSES][kSlots], cc[MPX_MAX_CLASSES];
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 60) return false;
+        bool fits = true;
+        for (int c = 0; c < nc && fits; ++c) {
+            ld tot = 0;
+            for (int s = 0; s < kSlots; ++s) {
+                v[c][s] = kSlotW[s] >= 0 ? std::llround(w[c][kSlotW[s]] * kSlotScale[s] / u) : 0;
+                if (std::llabs(v[c][s]) > 32639) fits = false;
+                tot += kSlotFmax[s] * (ld)std::llabs(v[c][s]);
+            }
+            const ld cw = w[c][9] / u;
+            if (!(std::fabs(cw) < (ld)(1 << 26))) {
+                fits = false;
+                break;
+            }
+            cc[c] = std::llround(cw);
+            tot += (ld)std::llabs(cc[c]);
+            if (!(tot < (ld)(1 << 26) - 64)) fits = false;  // key = ((D_a << 8) + D_b) << 5 | tag
+        }
+        if (fits) break;
+        u *= 2;
+    }
+    ld tmax = 0;
+    for (int c = 0; c < nc; ++c) {
+        ld fsum = 0;
+        for (int s = 0; s < kSlots; ++s) fsum += kSlotFmax[s];
+        // weight rounding + constant rounding + reference chain + long-double slack
+        const ld t = (u / 2 * fsum + u / 2 + refb[c] + psd[c] + 1e-15L * mag * 16) * 1.001L;
+        tmax = std::fmax(tmax, t);
+    }
+    const ld t2 = std::ceil(2 * tmax / u) + 1;
+    if (!(t2 < (ld)(1 << 24))) return false;  // nothing would ever be decided
+    ip.T2 = (int32_t)t2;
+    for (int c = 0; c < MPX_MAX_CLASSES; ++c) {
+        for (int hf = 0; hf < 2; ++hf) {
+            uint64_t pa = 0, pb = 0;
+            for (int j = 0; j < 8; ++j) {
+                const int s = 8 * hf + j;
+                long long a8 = 0, b8 = 0;
+                if (c < nc) {
+                    const long long x = v[c][s];
+                    a8 = (x + 128) >> 8;  // floor: x = 256 a + b with b in [-128, 127]
+                    b8 = x - 256 * a8;
+                }
+                pa |= (uint64_t)(uint8_t)(int8_t)a8 << (8 * j);
+                pb |= (uint64_t)(uint8_t)(int8_t)b8 << (8 * j);
+            }
+            ip.a[c][hf] = pa;
+            ip.b[c][hf] = pb;
+        }
+        ip.c[c] = c < nc ? (int32_t)cc[c] : (1 << 26) - 64;  // above every real key: never the argmin
+    }
+    return true;
+}
 }  // namespace
 
 // AUTO: FAST32, DIRECT when the fp32 decision cannot be proven for these
@@ -652,7 +892,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
     MPX_CHECK_ARG(grid >= 0 && block >= 0 && block <= 1024, "bad launch geometry");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA64, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA8, "bad path");
     if (npix == 0) return MPX_OK;
     MPX_CHECK_ARG(img, "null image");
     ClassParams cp{};
@@ -661,11 +901,29 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     hipStream_t s = as_stream(stream);
     FastParams fp;
     Fast64Params fp64;
+    I8Params ip8;
     const bool fast_ok = path != MPX_CLS_DIRECT && aligned16(img) &&
-                         (path == MPX_CLS_MFMA64 ? build_fast64(nc, mu, inv, fp64) : build_fast(nc, mu, inv, fp));
+                         (path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
+                          : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
+                                                  : build_fast(nc, mu, inv, fp));
     const int chosen = classify_choose(nc, path, fast_ok);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
-    if (chosen == MPX_CLS_MFMA64) {
+    if (chosen == MPX_CLS_MFMA8) {
+        const int64_t nchunks = npix / 128;
+        if (nchunks > 0) {
+            const int64_t blocks = (nchunks + 3) / 4;
+            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            if (nc <= 8)
+                hipLaunchKernelGGL(classify_mfma8_kernel<4>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+            else if (nc <= 16)
+                hipLaunchKernelGGL(classify_mfma8_kernel<8>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+            else
+                hipLaunchKernelGGL(classify_mfma8_kernel<16>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8,
+                                   amb);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nchunks * 128;
+        }
+    } else if (chosen == MPX_CLS_MFMA64) {
         const int64_t nchunks = npix / 64;
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;
@@ -738,11 +996,15 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 int classify_plan_impl(int nc, const double *mu, const double *inv, int path, float *margin) {
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA64, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA8, "bad path");
     FastParams fp;
     Fast64Params fp64;
+    I8Params ip8;
     bool ok = false;
-    if (path == MPX_CLS_MFMA64) {
+    if (path == MPX_CLS_MFMA8) {
+        ok = build_i8(nc, mu, inv, ip8);
+        if (margin) *margin = ok ? (float)ip8.T2 : 0.0f;  // in key units
+    } else if (path == MPX_CLS_MFMA64) {
         ok = build_fast64(nc, mu, inv, fp64);
         if (margin) *margin = ok ? (float)fp64.T2 : 0.0f;
     } else {
@@ -764,6 +1026,25 @@ extern "C" int mpx_classify(uint32_t *img, int64_t npix, int nc, const double *m
 extern "C" int mpx_classify_ex(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid,
                                int block, int path, uint32_t *ambiguous, void *stream) {
     return mpx::classify_impl(img, npix, nc, mu, inv, grid, block, path, ambiguous, stream);
+}
+
+// Host-side export of the MFMA8 integer weights (tests emulate the kernel's
+// exact integer arithmetic on the CPU): a, b = [32][16] int8 limbs by slot,
+// c = [32] accumulator constants, *t2 = decision margin in key units.
+extern "C" int mpx_classify_i8_params(int nc, const double *mu, const double *inv, int8_t *a, int8_t *b, int32_t *c,
+                                      int32_t *t2) {
+    MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES && mu && inv && a && b && c && t2, "bad arguments");
+    mpx::I8Params ip;
+    if (!mpx::build_i8(nc, mu, inv, ip)) return MPX_ERR_UNSUPPORTED;
+    for (int k = 0; k < MPX_MAX_CLASSES; ++k) {
+        for (int s = 0; s < 16; ++s) {
+            a[16 * k + s] = (int8_t)(uint8_t)(ip.a[k][s / 8] >> (8 * (s % 8)));
+            b[16 * k + s] = (int8_t)(uint8_t)(ip.b[k][s / 8] >> (8 * (s % 8)));
+        }
+        c[k] = ip.c[k];
+    }
+    *t2 = ip.T2;
+    return MPX_OK;
 }
 
 extern "C" int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin) {

@@ -127,7 +127,7 @@ def test_lab2_gpu_ground_truth(name, geom, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["direct", "mfma", "mfma64", "auto"])
+@pytest.mark.parametrize("path", ["direct", "mfma", "mfma64", "mfma8", "auto"])
 def test_lab3_gpu_ground_truth(path, tmp_path):
     src = write_hex_as_data(os.path.join(LAB3_DATA, "test_01_lab3.txt"), tmp_path / "in.data")
     out = tmp_path / "out.data"

@@ -63,7 +63,7 @@ def lab3_8192():
 
 
 @pytest.mark.parametrize("nc", [4, 16, 32])
-@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "auto"])
+@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8", "auto"])
 def test_classify_8192_every_pixel(gpu, lab3_8192, nc, path):
     img, ref = lab3_8192
     mu, inv, cls = ref[nc]

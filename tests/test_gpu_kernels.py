@@ -172,7 +172,7 @@ def test_classify_ground_truth(gpu):
         assert img_to_bytes(d) == gt, path
 
 
-CLS_PATHS = ("direct", "fast", "mfma", "mfma64", "auto")
+CLS_PATHS = ("direct", "fast", "mfma", "mfma64", "mfma8", "auto")
 
 
 def _random_classes(img, nc, npts, seed):
@@ -261,7 +261,7 @@ def test_classify_random_pixels_and_fallback_rate(gpu, path):
         assert amb.item() == 0
 
 
-@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64"])
+@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8"])
 def test_classify_exact_ties_all_fall_back(gpu, path):
     """Duplicated classes tie exactly on every pixel: every pixel must take the
     fp64 chain and keep the lowest class index (reference strict '<')."""
@@ -298,7 +298,7 @@ def test_classify_near_ties_fall_back_exactly(gpu):
     mu, inv = ops.class_stats(img, [pts, pts, pts[:-1]])
     cpu = img.clone()
     ops.classify_(cpu, mu, inv)
-    for path in ("fast", "mfma", "mfma64"):
+    for path in ("fast", "mfma", "mfma64", "mfma8"):
         d = img.to(gpu)
         ops.classify_(d, mu, inv, path=path)
         assert torch.equal(d.cpu(), cpu), path

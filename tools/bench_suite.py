@@ -95,7 +95,7 @@ def bench_lab3(dev, size=8192):
         mu, inv = ops.class_stats(host, pts)
         ref = host.clone()
         cpu = cpu_time_ms(lambda: ops.classify_(ref, mu, inv))
-        for path in ("direct", "fast", "mfma", "mfma64", "auto"):
+        for path in ("direct", "fast", "mfma", "mfma64", "mfma8", "auto"):
             work = img.clone()
             amb = torch.zeros(1, dtype=torch.int32, device=dev)
             ops.classify_(work, mu, inv, path=path, ambiguous=amb)

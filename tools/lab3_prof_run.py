@@ -12,7 +12,7 @@ dev = torch.device("cuda:0")
 size, nc = 8192, int(sys.argv[1]) if len(sys.argv) > 1 else 32
 img = torch.randint(0, 256, (size, size, 4), dtype=torch.uint8, device=dev)
 mu, inv = ops.class_stats(img.cpu(), class_points_for(size, size, nc, 64, seed=nc))
-for path in ("direct", "fast", "mfma", "mfma64"):
+for path in ("direct", "fast", "mfma", "mfma64", "mfma8"):
     for _ in range(2):
         ops.classify_(img, mu, inv, path=path)
 torch.cuda.synchronize()
