@@ -600,9 +600,11 @@ class StreamHaloLink:
     ping-pong input buffers, each (buffer_rows, ...) with the owned rows at
     ``slab.own_offset``). Step k (1-based) reads buffer (k-1) % 2: the fetch
     kernel publishes k, waits until each neighbour published k (it finished
-    step k-1, so its rows of this buffer are written and it no longer reads
-    ours of the other buffer), then copies the neighbours' boundary rows into
-    this rank's halo rows. Built by :func:`try_stream_halo`."""
+    step k-1, so its rows of this buffer are written, and it finished its
+    fetch of step k-1, so it no longer reads ours of the buffer this step
+    overwrites — a one-sided window waits on the side it does not read from
+    for exactly this), then copies the neighbours' boundary rows into this
+    rank's halo rows. Built by :func:`try_stream_halo`."""
 
     def __init__(self, ctx: DistContext, slab: Slab, bufs: List[torch.Tensor], sync: SyncBlock, every: list):
         self.ctx = ctx
@@ -630,18 +632,23 @@ class StreamHaloLink:
             raise
         self._descs: List[_HaloFetchDesc] = []
         s, rb = slab, self.row_bytes
+        any_halo = s.halo_up > 0 or s.halo_down > 0
         for k in range(2):  # one descriptor per buffer parity; only `step` changes
             d = _HaloFetchDesc()
-            if "up" in self._nb and s.halo_up:
+            if "up" in self._nb and any_halo:
                 p0, p1, ps, rows, off = self._nb["up"]
-                src = (p0, p1)[k] + (off + rows - s.halo_up) * rb  # its last halo_up owned rows
-                d.src[0], d.dst[0], d.bytes[0], d.flag[0] = src, bufs[k].data_ptr() + (s.own_offset - s.halo_up) * rb, \
-                    s.halo_up * rb, ps
-            if "dn" in self._nb and s.halo_down:
+                d.flag[0] = ps  # waited on even without rows to copy (it may read ours)
+                if s.halo_up:
+                    d.src[0] = (p0, p1)[k] + (off + rows - s.halo_up) * rb  # its last halo_up owned rows
+                    d.dst[0] = bufs[k].data_ptr() + (s.own_offset - s.halo_up) * rb
+                    d.bytes[0] = s.halo_up * rb
+            if "dn" in self._nb and any_halo:
                 p0, p1, ps, rows, off = self._nb["dn"]
-                src = (p0, p1)[k] + off * rb  # its first halo_down owned rows
-                d.src[1], d.dst[1], d.bytes[1], d.flag[1] = src, bufs[k].data_ptr() + (s.own_offset + s.rows) * rb, \
-                    s.halo_down * rb, ps
+                d.flag[1] = ps
+                if s.halo_down:
+                    d.src[1] = (p0, p1)[k] + off * rb  # its first halo_down owned rows
+                    d.dst[1] = bufs[k].data_ptr() + (s.own_offset + s.rows) * rb
+                    d.bytes[1] = s.halo_down * rb
             d.sync = sync.ptr
             d.spin_limit = int(os.environ.get("MPX_PEER_SPIN_LIMIT", "0"))
             self._descs.append(d)

@@ -194,8 +194,10 @@ typedef struct mpx_peer_probe {
 } mpx_peer_probe;
 int mpx_peer_probe_run(const mpx_peer_probe *p, void *stream);
 /* Streaming halo fetch: publish sync[0] = step (release), then per side s with a
- * neighbour: wait flag[s] >= step (bounded), copy bytes[s] from src[s] (its
- * boundary rows, system-scope loads) to dst[s] (this rank's halo rows). */
+ * neighbour (flag[s] != NULL): wait flag[s] >= step (bounded), and when src[s]
+ * is set copy bytes[s] from it (its boundary rows, system-scope loads) to dst[s]
+ * (this rank's halo rows). A side without rows to copy still waits: the
+ * neighbour reads this rank's rows (write-after-read order). */
 typedef struct mpx_halo_fetch {
     const void *src[2];
     void *dst[2];

@@ -535,33 +535,27 @@ struct I8Params {
 
 constexpr int kAmb8Cap = 2048;
 
-// (a << s) + b in one v_lshl_add_u32 (the compiler splits the shift-by-5 form
-// into shift + or + add chains)
-__device__ __forceinline__ int32_t lshl_add(int32_t a, int s, int32_t b) {
-    int32_t r;
-    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
-    return r;
-}
-
-// (a << s) + K with K an inline constant (the class tag)
-template <int K>
-__device__ __forceinline__ int32_t lshl_add_k(int32_t a, int s) {
-    int32_t r;
-    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "i"(K));
-    return r;
-}
-
 __device__ __forceinline__ int32_t imed3(int32_t a, int32_t b, int32_t c) {
     int32_t r;
     asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
+// The MFMA results are read by compiler-visible instructions only: the
+// hazard recognizer does not see inline-asm reads of an MFMA destination and
+// would not pad them (a read right after the MFMA sees stale registers). The
+// empty asm between the two v_lshl_add_u32 only stops the compiler from
+// re-associating them into a shift + or + add chain (5 instead of 4 VALU).
 template <int NREG, int RR>
 __device__ __forceinline__ void rank_reg(const i32x16 &da, const i32x16 &db, int32_t &B, int32_t &S) {
     if constexpr (RR < NREG) {
-        const int32_t key = lshl_add(db[RR], 5, lshl_add_k<(RR & 3) + 8 * (RR >> 2)>(da[RR], 13));
-        S = imed3(B, key, S);
+        uint32_t x = ((uint32_t)da[RR] << 13) + (uint32_t)((RR & 3) + 8 * (RR >> 2));
+        asm volatile("" : "+v"(x));
+        const int32_t key = (int32_t)(((uint32_t)db[RR] << 5) + x);
+        // med3(B, key, S) in the form the backend selects as v_med3_i32 (an
+        // inline-asm med3 may not be ordered after an in-flight MFMA's
+        // writeback to a reused dead accumulator register)
+        S = max(min(B, key), min(max(B, key), S));
         B = min(B, key);
     }
 }

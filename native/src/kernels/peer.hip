@@ -12,9 +12,11 @@
 //    neighbours' rows after the production wait — on real xGMI links before
 //    any timed or verified work trusts them (mismatch or timeout -> RCCL);
 //  * mpx_halo_fetch — the streaming convolution's halo exchange: publish this
-//    rank's step, wait (bounded) for each neighbour to reach it, copy their
-//    boundary rows into the local halo rows with system-scope loads. One tiny
-//    launch per step, no RCCL kernel, no host round trip.
+//    rank's step, wait (bounded) for each neighbour to reach it (read-after-
+//    write on the rows this rank copies, write-after-read on the rows the
+//    neighbour copies from this rank), copy their boundary rows into the local
+//    halo rows with system-scope loads. One tiny launch per step, no RCCL
+//    kernel, no host round trip.
 //
 // Reference: no multi-GPU code exists (/root/reference/
 // CMakeLists.txt:2 name only); this is the north-star halo tier.
@@ -119,14 +121,18 @@ __global__ __launch_bounds__(256) void peer_probe_kernel(mpx_peer_probe p) {
 __global__ __launch_bounds__(256) void halo_fetch_kernel(mpx_halo_fetch f) {
     const int side = blockIdx.x;
     if (threadIdx.x == 0) peer::publish(f.sync + kSyncStep, f.step);  // idempotent per block
-    if (!f.src[side]) return;  // block-uniform: global edge
+    if (!f.flag[side]) return;  // block-uniform: global edge
+    // wait even when no rows are copied from this side (one-sided windows such
+    // as Roberts): the neighbour READS this rank's rows, and its reaching
+    // `step` means it finished the fetch of step - 1, so the buffer this
+    // step's convolution overwrites is no longer being read (write-after-read)
     __shared__ int s_ok;
     if (threadIdx.x < 64) {  // one wave polls
         const bool ok = peer::wait_at_least(f.flag[side], f.step, f.sync + kSyncErr, f.spin_limit);
         if (threadIdx.x == 0) s_ok = ok;
     }
     __syncthreads();
-    if (!s_ok) return;
+    if (!s_ok || !f.src[side]) return;
     const uint32_t words = (uint32_t)(f.bytes[side] / 4);
     const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(f.src[side]), 0,
                                                                          (int)f.bytes[side], 0x00020000);
@@ -188,7 +194,7 @@ extern "C" int mpx_halo_fetch_run(const mpx_halo_fetch *f, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(f && f->sync && f->step > 0, "bad halo-fetch descriptor");
     for (int s = 0; s < 2; ++s) {
-        MPX_CHECK_ARG(!f->src[s] == !f->flag[s] && (!f->src[s] || f->dst[s]), "a neighbour needs rows, flag and dst");
+        MPX_CHECK_ARG((!f->src[s] || (f->flag[s] && f->dst[s])), "copied rows need the neighbour's flag and a dst");
         MPX_CHECK_ARG(!f->src[s] || (f->bytes[s] > 0 && f->bytes[s] % 4 == 0 && f->bytes[s] < (int64_t)1 << 31),
                       "halo bytes must be a positive multiple of 4");
     }
