@@ -49,8 +49,9 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``mfma64`` — fp64 MFMA distance GEMM (v_mfma_f64_16x16x4_f64);
       * ``mfma8``  — exact int8 MFMA distance GEMM (v_mfma_i32_32x32x16_i8,
         16-bit fixed-point weights in two int8 limbs, int32 keys);
-      * ``auto``   — ``fast`` (measured fastest at every nc on MI355X: the f32
-        MFMA shares the VALU's fp32 datapath on gfx950).
+      * ``auto``   — ``mfma8`` from 24 classes (1.28x ``fast`` at nc = 32 on
+        MI355X), else ``fast`` (the f32 MFMA shares the VALU's fp32 datapath
+        on gfx950; the int8 path's fixed feature cost loses below ~16 classes).
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes

@@ -252,7 +252,16 @@ bool jacobi_one_device_equal(const std::vector<uint8_t> &init, const std::vector
     HIP_OK(hipFree(un));
     HIP_OK(hipStreamDestroy(s));
     const size_t rb = (size_t)cols * sizeof(T);
-    return std::memcmp(got.data() + rb, fin.data() + rb, (size_t)grows * rb) == 0;
+    for (int r = 1; r <= grows; ++r)
+        if (std::memcmp(got.data() + r * rb, fin.data() + r * rb, rb) != 0) {
+            const T *g = reinterpret_cast<const T *>(got.data() + r * rb), *f = reinterpret_cast<const T *>(fin.data() + r * rb);
+            int j = 0;
+            while (j < cols && g[j] == f[j]) ++j;
+            fprintf(stderr, "[mpx_mgpu] one-device mismatch: first at row %d col %d (one device %.17g, N ranks %.17g)\n", r, j,
+                    (double)g[j], (double)f[j]);
+            return false;
+        }
+    return true;
 }
 
 // A rank's initial rows into the whole-field image: owned rows always, plus
@@ -487,6 +496,7 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
     HIP_OK(hipStreamSynchronize(s));
     sh.verified[rank] = err == 0 && std::memcmp(gun.data() + cols, hun.data() + cols, (size_t)vr * row_bytes) == 0;
     if (err) fprintf(stderr, "[ERROR MPX] rank %d: a device-side halo wait timed out\n", rank);
+    if (!sh.verified[rank]) fprintf(stderr, "[mpx_mgpu] rank %d: the extra-sweep check against the CPU failed\n", rank);
     // the final field (u after `it` sweeps: the extra verification sweep above wrote un only)
     HIP_OK(hipMemcpy(sh.fin.data() + (sl.row0 + 1) * row_bytes, u + cols, rows * row_bytes, hipMemcpyDeviceToHost));
     sh.bar->wait();  // nobody frees buffers a neighbour may still read

@@ -867,8 +867,9 @@ bool build_i8(int nc, const double *mu, const double *inv, I8Params &ip) {
 }
 }  // namespace
 
-// AUTO: FAST32, DIRECT when the fp32 decision cannot be proven for these
-// statistics. Measured on MI355X (profiles/lab3_classify.md): the f32 MFMA and
+// AUTO: MFMA8 from kAutoMfma8MinClasses classes, else FAST32; DIRECT when no
+// decision bound can be proven for these statistics. Measured on MI355X
+// (profiles/lab3_classify.md): the f32 MFMA and
 // the f32 VALU share one datapath on gfx950 — SQ_VALU_MFMA_BUSY_CYCLES and the
 // VALU issue cycles ADD UP to the kernel time — so the distance GEMM cannot hide
 // the ranking work behind the matrix core, and FAST32 is as fast or faster at
@@ -878,6 +879,23 @@ int classify_choose(int nc, int path, bool fast_ok) {
     if (path == MPX_CLS_DIRECT || !fast_ok) return MPX_CLS_DIRECT;
     if (path == MPX_CLS_AUTO) return MPX_CLS_FAST;
     return path;
+}
+
+// AUTO above this class count runs MFMA8 (its statistics permitting): same
+// box, 8192^2, µs (profiles/lab3_classify.md): nc 4 fast 130 / mfma8 256,
+// nc 16 360 / 352 (parity), nc 32 633 / 494.
+constexpr int kAutoMfma8MinClasses = 24;
+
+// The path AUTO (or an explicit path) resolves to for these statistics, with
+// the parameters it needs built; DIRECT when no fp32 / int bound exists.
+int classify_resolve(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
+                     Fast64Params &fp64, I8Params &ip8) {
+    if (path == MPX_CLS_DIRECT || !aligned) return MPX_CLS_DIRECT;
+    if (path == MPX_CLS_AUTO && nc >= kAutoMfma8MinClasses && build_i8(nc, mu, inv, ip8)) return MPX_CLS_MFMA8;
+    const bool ok = path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
+                    : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
+                                            : build_fast(nc, mu, inv, fp);
+    return classify_choose(nc, path, ok);
 }
 
 int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid, int block,
@@ -896,11 +914,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     FastParams fp;
     Fast64Params fp64;
     I8Params ip8;
-    const bool fast_ok = path != MPX_CLS_DIRECT && aligned16(img) &&
-                         (path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
-                          : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
-                                                  : build_fast(nc, mu, inv, fp));
-    const int chosen = classify_choose(nc, path, fast_ok);
+    const int chosen = classify_resolve(nc, mu, inv, path, aligned16(img), fp, fp64, ip8);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
     if (chosen == MPX_CLS_MFMA8) {
         const int64_t nchunks = npix / 128;
@@ -994,18 +1008,13 @@ int classify_plan_impl(int nc, const double *mu, const double *inv, int path, fl
     FastParams fp;
     Fast64Params fp64;
     I8Params ip8;
-    bool ok = false;
-    if (path == MPX_CLS_MFMA8) {
-        ok = build_i8(nc, mu, inv, ip8);
-        if (margin) *margin = ok ? (float)ip8.T2 : 0.0f;  // in key units
-    } else if (path == MPX_CLS_MFMA64) {
-        ok = build_fast64(nc, mu, inv, fp64);
-        if (margin) *margin = ok ? (float)fp64.T2 : 0.0f;
-    } else {
-        ok = path != MPX_CLS_DIRECT && build_fast(nc, mu, inv, fp);
-        if (margin) *margin = ok ? fp.T2 : 0.0f;
-    }
-    return classify_choose(nc, path, ok);
+    const int chosen = classify_resolve(nc, mu, inv, path, true, fp, fp64, ip8);
+    if (margin)
+        *margin = chosen == MPX_CLS_MFMA8    ? (float)ip8.T2  // in key units
+                  : chosen == MPX_CLS_MFMA64 ? (float)fp64.T2
+                  : chosen == MPX_CLS_DIRECT ? 0.0f
+                                             : fp.T2;
+    return chosen;
 }
 
 MPX_MODULE_ANCHOR(classify)

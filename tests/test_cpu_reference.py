@@ -146,6 +146,10 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
     mu20, inv20 = stats(20)
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
+    # from 24 classes AUTO runs the exact int8-MFMA distance GEMM (margin in key units)
+    mu28, inv28 = stats(28)
+    path28, margin28 = ops.classify_plan(mu28, inv28, "auto")
+    assert path28 == "mfma8" and margin28 >= 1
     assert ops.classify_plan(mu20, inv20, "mfma")[0] == "mfma"
     # fp64 GEMM: same validation, a bound ~2^29 x tighter than the fp32 one
     path64, margin64 = ops.classify_plan(mu20, inv20, "mfma64")

@@ -14,9 +14,9 @@ def test_scale_driver_cpu_dry_run(tmp_path):
     data = json.load(open(tmp_path / "scaling.json"))
     runs = {(x["name"], x["n"]): x for x in data["runs"]}
     one, two = runs[("conv/peer", 1)], runs[("conv/rccl", 2)]
-    assert one["status"] == "ok" and one["efficiency"] == 1.0
-    assert two["status"] == "ok" and two["n_reported"] == 2 and two["verified"] is True
-    assert two["efficiency"] is not None and two["world_size_seen"]["torch_distributed"] == 2
+    assert one["status"] == "ok" and one["efficiency"] == 1.0, one
+    assert two["status"] == "ok" and two["n_reported"] == 2 and two["verified"] is True, two
+    assert two["efficiency"] is not None and two["world_size_seen"]["torch_distributed"] == 2, two
     assert runs[("conv/peer", 2)]["status"] == "skipped" and runs[("conv/peer", 2)]["reason"]
     assert (tmp_path / "scaling.csv").exists() and (tmp_path / "scaling.png").exists()
 

@@ -157,6 +157,11 @@ def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
         r["efficiency"] = None
         if r["status"] != "ok" or b is None:
             continue
+        if r is b:  # the baseline itself, whatever its rounding
+            r["efficiency"] = 1.0
+            if rehearse:
+                r["retained"] = 1.0
+            continue
         if r["kind"] == "weak" and r.get("value") is not None and b.get("value"):
             r["efficiency"] = round(r["value"] / (r["n"] * b["value"]), 4)
             if rehearse:
