@@ -23,6 +23,7 @@ CSER      := -O0 -ffp-contract=off -Wall -Wno-unknown-pragmas $(WERROR) -std=gnu
 
 B         := build
 PYLIB     := cuda_mpi_openmp_amd/_lib/libmpx.so
+TUNELIB   := cuda_mpi_openmp_amd/_lib/libmpx_tune.so
 ALIB      := $(B)/libmpx.a
 
 HIP_SRCS  := $(wildcard native/src/kernels/*.hip)
@@ -37,9 +38,11 @@ GPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/to_plot_hip_exe labs/lab$(L)/s
 CPU_APPS  := $(foreach L,1 2 3 5,labs/lab$(L)/src/cpu_exe labs/lab$(L)/src/cpu_omp_exe)
 MISC_APPS := labs/lab3/src/read_input_exe bin/gpu_info bin/hw1 bin/hw2 bin/mpx_mgpu
 
-.PHONY: all lib apps tools clean
-all: lib apps
+.PHONY: all lib apps tools tune clean
+all: lib apps tune
 lib: $(PYLIB) $(ALIB)
+# tuning-only kernel variants / probes (tools/kbench.py), linked against libmpx
+tune: $(TUNELIB)
 apps: $(GPU_APPS) $(CPU_APPS) $(MISC_APPS)
 
 $(B):
@@ -53,7 +56,7 @@ $(B)/k_%.o: native/src/kernels/%.hip $(HDRS) | $(B)
 
 # the lab2 kernels keep scalar v_fmac chains: SLP packing into v_pk_fma_f32 costs
 # hazard NOPs and ~40 VGPRs (8 -> 4 waves per SIMD) for no extra FLOP rate
-$(B)/k_edge.o $(B)/k_edge_roberts.o $(B)/k_edge_variants.o: HIPFLAGS += -fno-slp-vectorize
+$(B)/k_edge.o $(B)/k_edge_roberts.o $(B)/t_edge_variants.o: HIPFLAGS += -fno-slp-vectorize
 # MFMA accumulators straight into VGPRs (unified file on gfx950): no v_accvgpr_read per result
 $(B)/k_classify.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
@@ -72,6 +75,12 @@ $(B)/cpu_kernels.o: native/src/cpu/cpu_kernels.c $(HDRS) | $(LABS)
 
 $(PYLIB): $(LIB_OBJS) | $(B)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(LIB_OBJS) -lgomp -lm -ldl
+
+$(B)/t_%.o: native/tune/%.hip $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(TUNELIB): $(B)/t_edge_variants.o $(PYLIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $< -L$(dir $(PYLIB)) -lmpx -Wl,-rpath,'$$ORIGIN'
 
 $(ALIB): $(LIB_OBJS) | $(B)
 	rm -f $@ && ar rcs $@ $(LIB_OBJS)
@@ -108,7 +117,7 @@ bin/hw2: native/apps/hw2_bubble_sort.c | $(B)
 
 # ---- stand-alone measurement tools (not part of `all`) ----
 tools: bin/mfma_valu_overlap
-bin/mfma_valu_overlap: tools/mfma_valu_overlap.hip | $(B)
+bin/mfma_valu_overlap: tools/experiments/mfma_valu_overlap.hip | $(B)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 # ---- host-only sanitizer builds of the CPU references ----
@@ -140,4 +149,4 @@ build/san/hw2: native/apps/hw2_bubble_sort.c | build/san
 	$(CC) $(SAN) -Wall -std=gnu11 $< -o $@
 
 clean:
-	rm -rf $(B) bin $(PYLIB) $(GPU_APPS) $(CPU_APPS) labs/lab3/src/read_input_exe
+	rm -rf $(B) bin $(PYLIB) $(TUNELIB) $(GPU_APPS) $(CPU_APPS) labs/lab3/src/read_input_exe

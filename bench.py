@@ -64,6 +64,11 @@ BASELINE_NOTE = ("estimate: A6000 Roberts 2x2 on a ~0.78 Mpx image, one cold lau
                  "same-methodology comparison is in profiles/harness_vs_baseline.md")
 
 
+def _sig(v: float) -> float:
+    """Six significant digits (a tiny CPU dry run must not round to 0)."""
+    return float(f"{v:.6g}")
+
+
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=1)
@@ -222,7 +227,7 @@ def run(args) -> int:
     if ctx.rank == 0:
         rec = {
             "metric": BASELINE_METRIC,
-            "value": round(value, 3),
+            "value": _sig(value),
             "unit": "Gpixel/s",
             "n_gpus": n,
             "steps": args.steps,
@@ -259,7 +264,7 @@ def run(args) -> int:
             "device": str(torch.cuda.get_device_name(ctx.device)) if ctx.device.type == "cuda" else "cpu",
         }
         if warm is not None:
-            rec["value_warm_cache"] = round(pixels / warm / 1e9, 3)
+            rec["value_warm_cache"] = _sig(pixels / warm / 1e9)
             rec["ms_per_step_warm_cache"] = round(warm * 1e3 / max(1, args.steps), 5)
         if stream_rec is not None:
             rec.update(stream_rec)
@@ -307,7 +312,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     elapsed = max(per_rank)
     for d in sdets:
         d.check_stream()
-    rec = {"value_streaming": round(n * args.size * args.size * args.steps / elapsed / 1e9, 3),
+    rec = {"value_streaming": _sig(n * args.size * args.size * args.steps / elapsed / 1e9),
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
            "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
            "transport_streaming": sdets[0].transport if n > 1 else None}

@@ -61,9 +61,6 @@ _SIGNATURES = {
     "mpx_ipc_open_dev": (c_int, [c_int, c_vp, ctypes.POINTER(c_vp)]),
     "mpx_ipc_close": (c_int, [c_vp]),
     "mpx_memcpy_d2d": (c_int, [c_vp, c_vp, c_i64, c_vp]),
-    "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
-    "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_int, c_vp]),
-    "mpx_strip_copy_probe": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "mpx_filter_lookup": (c_int, [c_char_p, _ip, _ip, _ip, _fp, _fp]),
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
@@ -115,6 +112,17 @@ _SIGNATURES = {
     "mpx_sync_clear": (c_int, [c_vp, c_i64]),
 }
 
+# tuning-only entry points (kernel variants, copy probes, the exhaustive
+# fast-sqrt self-test): libmpx_tune.so, built from native/tune/ and loaded only
+# by tools/kbench.py and its tests, never by the production paths
+TUNE_PATH = _PKG_DIR / "_lib" / "libmpx_tune.so"
+_TUNE_SIGNATURES = {
+    "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
+    "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_int, c_vp]),
+    "mpx_strip_copy_probe": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+}
+_tune = None
+
 
 class MpxError(RuntimeError):
     """A libmpx entry point returned a non-zero status."""
@@ -151,6 +159,23 @@ def lib(auto_build: bool = True) -> ctypes.CDLL:
             fn.argtypes = args
         _lib = handle
         return _lib
+
+
+def tune_lib() -> ctypes.CDLL:
+    """The tuning library (after libmpx, whose error state and runtime it shares)."""
+    global _tune
+    lib()
+    with _lock:
+        if _tune is None:
+            if not TUNE_PATH.exists():
+                raise MpxError(f"{TUNE_PATH} not built; run `make tune`")
+            handle = ctypes.CDLL(str(TUNE_PATH), mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in _TUNE_SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _tune = handle
+    return _tune
 
 
 def available() -> bool:

@@ -24,6 +24,7 @@ from typing import Any, Dict, List, Optional
 
 import pandas as pd
 
+from ..utils.plots import annotated_bars, median_groups, metadata_note
 from .core import RunRecord, print_stats, run_binary
 
 
@@ -133,37 +134,10 @@ class Tester:
                 print(f"[Speedup] CPU median {cpu:.5f} ms / {self.gpu_label}_{ks} median {med:.5f} ms = "
                       f"{cpu / med:.1f}x")
 
-    def plot(self, df: pd.DataFrame) -> str:
-        import matplotlib
-
-        matplotlib.use("Agg")
-        import matplotlib.pyplot as plt
-
-        d = df.copy()
-        d["kernel_size"] = d["kernel_size"].apply(_kernel_key)
-        grouped = (d.groupby(["device", "kernel_size"])
-                   .agg(median_time=("time_kernel_exe_ms", "median"), sample_count=("time_kernel_exe_ms", "size"))
-                   .reset_index())
-        grouped["label"] = [dev if dev == "CPU" else f"{dev}_{ks}"
-                            for dev, ks in zip(grouped["device"], grouped["kernel_size"])]
-        legend = ""
-        for col in self.metadata_columns2plot:
-            if col in d.columns:
-                legend += f"{col}: [" + ", \n".join(map(str, d[col].unique())) + "]\n"
-        legend += "\nSample Count by Group:\n" + "".join(
-            f"{lab}: {n} samples\n" for lab, n in zip(grouped["label"], grouped["sample_count"]))
-        fig, ax = plt.subplots(figsize=(16, 6))
-        bars = ax.bar(grouped["label"], grouped["median_time"], color="skyblue")
-        for bar, med in zip(bars, grouped["median_time"]):
-            ax.text(bar.get_x() + bar.get_width() / 2, bar.get_height() + 5e-5, f"{med:.5f}", ha="center",
-                    va="bottom")
-        plt.text(1.02, 0.95, legend, transform=ax.transAxes, fontsize=10, verticalalignment="top",
-                 bbox=dict(facecolor="white", alpha=0.5))
-        ax.set_xlabel("Device and Kernel Size")
-        ax.set_ylabel("Median Execution Time (ms)")
-        ax.set_title("Median Execution Time by Device and Kernel Size")
-        plt.tight_layout()
-        path = os.path.join(self.dir2save, "median_execution_time.png")
-        plt.savefig(path, dpi=300, bbox_inches="tight")
-        plt.close(fig)
-        return path
+    def plot(self, df: pd.DataFrame) -> Optional[str]:
+        """``median_execution_time.png`` next to the GPU binary (utils/plots.py)."""
+        groups = median_groups(df, self.gpu_label)
+        return annotated_bars(groups["label"], groups["median_ms"], os.path.join(self.dir2save, "median_execution_time.png"),
+                              note=metadata_note(df, self.metadata_columns2plot, groups),
+                              xlabel="Device and Kernel Size", ylabel="Median Execution Time (ms)",
+                              title="Median Execution Time by Device and Kernel Size")

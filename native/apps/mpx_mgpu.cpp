@@ -252,16 +252,27 @@ bool jacobi_one_device_equal(const std::vector<uint8_t> &init, const std::vector
     HIP_OK(hipFree(un));
     HIP_OK(hipStreamDestroy(s));
     const size_t rb = (size_t)cols * sizeof(T);
-    for (int r = 1; r <= grows; ++r)
-        if (std::memcmp(got.data() + r * rb, fin.data() + r * rb, rb) != 0) {
-            const T *g = reinterpret_cast<const T *>(got.data() + r * rb), *f = reinterpret_cast<const T *>(fin.data() + r * rb);
-            int j = 0;
-            while (j < cols && g[j] == f[j]) ++j;
-            fprintf(stderr, "[mpx_mgpu] one-device mismatch: first at row %d col %d (one device %.17g, N ranks %.17g)\n", r, j,
-                    (double)g[j], (double)f[j]);
-            return false;
-        }
-    return true;
+    long long bad = 0;
+    int r_lo = -1, r_hi = -1, c_lo = cols, c_hi = -1;
+    double dmax = 0;
+    for (int r = 1; r <= grows; ++r) {
+        if (std::memcmp(got.data() + r * rb, fin.data() + r * rb, rb) == 0) continue;
+        const T *g = reinterpret_cast<const T *>(got.data() + r * rb), *f = reinterpret_cast<const T *>(fin.data() + r * rb);
+        for (int j = 0; j < cols; ++j)
+            if (g[j] != f[j]) {
+                if (!bad)
+                    fprintf(stderr, "[mpx_mgpu] one-device mismatch: first at row %d col %d (one device %.17g, N ranks %.17g)\n",
+                            r, j, (double)g[j], (double)f[j]);
+                ++bad;
+                r_lo = r_lo < 0 ? r : r_lo, r_hi = r;
+                c_lo = std::min(c_lo, j), c_hi = std::max(c_hi, j);
+                dmax = std::max(dmax, std::fabs((double)g[j] - (double)f[j]));
+            }
+    }
+    if (bad)
+        fprintf(stderr, "[mpx_mgpu] one-device mismatch: %lld elements, rows %d..%d, cols %d..%d, max |diff| %.3g\n", bad,
+                r_lo, r_hi, c_lo, c_hi, dmax);
+    return bad == 0;
 }
 
 // A rank's initial rows into the whole-field image: owned rows always, plus

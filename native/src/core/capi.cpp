@@ -32,15 +32,13 @@ const void *module_anchor_jacobi();
 const void *module_anchor_classify();
 const void *module_anchor_edge();
 const void *module_anchor_edge_roberts();
-const void *module_anchor_edge_variants();
 const void *module_anchor_sort();
 }  // namespace mpx
 
 extern "C" int mpx_preload_modules(void) {
     const void *anchors[] = {mpx::module_anchor_vsub(),         mpx::module_anchor_jacobi(),
                              mpx::module_anchor_classify(),     mpx::module_anchor_edge(),
-                             mpx::module_anchor_edge_roberts(), mpx::module_anchor_edge_variants(),
-                             mpx::module_anchor_sort()};
+                             mpx::module_anchor_edge_roberts(), mpx::module_anchor_sort()};
     for (const void *k : anchors) {
         hipFuncAttributes attr;
         MPX_RETURN_IF_HIP_ERROR(hipFuncGetAttributes(&attr, k));

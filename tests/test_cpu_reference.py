@@ -162,3 +162,14 @@ def test_classify_plan_routes():
     bad = inv.copy()
     bad[0] = np.diag([1e-3, -1e-3, 1e-3])
     assert ops.classify_plan(mu, bad, "auto")[0] == "direct"
+
+
+def test_production_library_exports_no_tuning_entry_points():
+    """Kernel variants, copy probes and the exhaustive self-test live in
+    libmpx_tune.so (native/tune/, tools/kbench.py); libmpx.so has none."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    for name in ("mpx_conv_variant", "mpx_strip_copy_probe", "mpx_selftest_fast_sqrt"):
+        assert not hasattr(L, name), name
+        assert hasattr(_native.tune_lib(), name), name

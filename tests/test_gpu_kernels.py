@@ -353,7 +353,7 @@ def test_fast_sqrt_exhaustive(gpu, capsys):
     v_sqrt_f32 truncation would get wrong (the reason the margin exists)."""
     from cuda_mpi_openmp_amd import _native
 
-    L = _native.lib()
+    L = _native.tune_lib()  # the self-test entry point lives in the tuning library
     counts = []
     for raw in (0, 1):
         bad = torch.zeros(1, dtype=torch.int64, device=gpu)
@@ -375,7 +375,7 @@ def test_conv_alternating_segments_exact(gpu, hw, seg):
 
     from cuda_mpi_openmp_amd import _native
 
-    L = _native.lib()
+    L = _native.tune_lib()
     f = ops.get_filter("sobel5")
     wx, wy = f.c_taps()
     img = smooth_img(*hw, seed=hw[0] + seg)

@@ -8,9 +8,16 @@
 #   O=...             bash tools/gpu.sh bench [bench.py args...]    # one JSON line -> $O/bench.json
 #   O=...             bash tools/gpu.sh prof NAME -- CMD...         # rocprofv3 kernel trace + stats
 #   O=...             bash tools/gpu.sh pmc NAME "C1 C2 ..." -- CMD...   # one counter pass
+#   O=...             bash tools/gpu.sh profile NAME -- CMD...      # trace + the standard counter groups
+#   O=...             bash tools/gpu.sh ab NAME LIB ROUNDS -- CMD...  # CMD alternately on libmpx / LIB
+#   O=...             bash tools/gpu.sh mgpu [ARGS...]              # native runtime: N-rank == one-device
 #   O=...             bash tools/gpu.sh jpeer [N...]                # device-signalled Jacobi: peer vs no-exchange
 #   O=...             bash tools/gpu.sh run NAME SECONDS CMD...     # any command, logged, time-bounded
 #   O=...             bash tools/gpu.sh checkpoint                  # tests + smoke + bench
+#
+# Counter groups respect the per-block limits (<= 8 SQ, 4 TCC, 2 GRBM per pass);
+# FETCH_SIZE / WRITE_SIZE get passes of their own. tools/pmc_median.py merges
+# the passes (median per kernel); tools/prof_summary.py writes the tables.
 set -o pipefail
 O=${O:-gpurun_out/scratch}
 mkdir -p "$O"
@@ -43,6 +50,31 @@ case "$cmd" in
     timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/$name" -o "$name" -- "$@" > "$O/$name.log" 2>&1 \
         || fail "pmc $name" $? "$O/$name.log"
     echo "pmc $name done" ;;
+  profile)
+    name=$1; shift; [ "$1" = "--" ] && shift
+    bash "$0" prof "$name" -- "$@" || exit $?
+    i=0
+    for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+               "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+               "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU" "FETCH_SIZE" "WRITE_SIZE" \
+               "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
+               "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
+      i=$((i + 1))
+      bash "$0" pmc "$name.pmc$i" "$grp" -- "$@" || exit $?
+    done ;;
+  ab)
+    name=$1; lib=$2; rounds=$3; shift 3; [ "$1" = "--" ] && shift
+    for r in $(seq 1 "$rounds"); do
+      timeout -k 10 300 "$@" > "$O/$name.a$r.log" 2>&1 || fail "ab $name a$r" $? "$O/$name.a$r.log"
+      MPX_LIB_PATH="$lib" timeout -k 10 300 "$@" > "$O/$name.b$r.log" 2>&1 || fail "ab $name b$r" $? "$O/$name.b$r.log"
+    done
+    echo "ab $name: $rounds rounds in $O/$name.{a,b}N.log" ;;
+  mgpu)
+    args=("$@"); [ ${#args[@]} -eq 0 ] && args=(jacobi --halo peer --shared --gpus 2 --size 4096)
+    timeout -k 10 200 bin/mpx_mgpu "${args[@]}" > "$O/mgpu.json" 2> "$O/mgpu.err"; rc=$?
+    echo "mpx_mgpu ${args[*]}: rc=$rc $(grep -o '"verified": [a-z]*\|"one_device_equal": [a-z]*' "$O/mgpu.json" | tr '\n' ' ')"
+    head -c 900 "$O/mgpu.err"
+    [ $rc -eq 0 ] || [ $rc -eq 3 ] || exit $rc ;;
   jpeer)
     ns=("$@"); [ ${#ns[@]} -eq 0 ] && ns=(2 4)
     for n in "${ns[@]}"; do
@@ -63,5 +95,5 @@ case "$cmd" in
   checkpoint)
     bash "$0" tests && bash "$0" smoke && bash "$0" bench ;;
   *)
-    sed -n 2,14p "$0"; exit 2 ;;
+    sed -n 2,21p "$0"; exit 2 ;;
 esac

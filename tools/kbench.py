@@ -41,6 +41,7 @@ def main():
     p.add_argument("--only", default="", help="run only the variants whose name contains this string")
     args = p.parse_args()
     L = _native.lib()
+    T = _native.tune_lib()  # variants / probes live in libmpx_tune.so
     dev = torch.device("cuda:0")
     n = args.size
     # --rotate R: R independent (input, output) pairs cycled launch by launch,
@@ -62,7 +63,7 @@ def main():
 
     # exhaustive fast-sqrt equivalence check
     bad = torch.zeros(1, dtype=torch.int64, device=dev)
-    _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), 0, 0))
+    _native.check(T.mpx_selftest_fast_sqrt(bad.data_ptr(), 0, 0))
     torch.cuda.synchronize()
     print(json.dumps({"fast_sqrt_selftest_mismatches": int(bad.item())}), flush=True)
 
@@ -73,7 +74,7 @@ def main():
         ref = ops.conv(img, f)
 
         def mk(kind, p1, p2, fast, wx=wx, wy=wy, k=k):
-            return lambda: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, k, kind, p1, p2, fast,
+            return lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, k, kind, p1, p2, fast,
                                                             wx, wy, 0))
 
         for seg in (8, 16, 32, 64):
@@ -89,40 +90,40 @@ def main():
     sref = ops.conv(img, fs5)
     for seg in (0, 16, 32, 48):  # alternating segment direction (production MAG2 order candidate)
         variants[f"sobel5-sep/wave-const/seg{seg}/alt"] = (
-            (lambda seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 2000, 1,
+            (lambda seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 2000, 1,
                                                               swx, swy, 0))), sref)
     for seg in (0, 8, 20, 24):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
-                (lambda kind=kind, seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5,
+                (lambda kind=kind, seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5,
                                                                              kind, seg, 0, 1, swx, swy, 0))), sref)
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
-            (lambda seg=seg: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 1000, 1,
+            (lambda seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 1000, 1,
                                                               swx, swy, 0))), sref)
     for seg, per in ((0, 0), (0, 2000), (24, 2000), (0, 18000), (0, 34000), (0, 66000), (0, 162000),
                      (20, 34000), (24, 34000), (12, 34000),
                      (0, 10000), (0, 10005), (0, 11005), (24, 10000)):
         # 18000: no apron loads — a cost probe whose strip edges are wrong (no reference check)
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
-            (lambda seg=seg, per=per: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
+            (lambda seg=seg, per=per: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
                                                                        per, 1, swx, swy, 0))), None if per == 18000 else sref)
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
     variants["sobel5-sep/stores-nt"] = (
-        (lambda: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, 3, 1, swx, swy, 0))),
+        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, 3, 1, swx, swy, 0))),
         sref)
     for p2, nm in ((0, "buffer"), (1, "global"), (2, "global-nt")):  # row-load A/B
         variants[f"sobel5-sep/loads-{nm}"] = (
-            (lambda p2=p2: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, p2, 1,
+            (lambda p2=p2: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, p2, 1,
                                                             swx, swy, 0))), sref)
         variants[f"roberts/loads-{nm}"] = (
-            (lambda p2=p2: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 2, 7, 0, p2, 1,
+            (lambda p2=p2: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 2, 7, 0, p2, 1,
                                                             rwx, rwy, 0))), rref)
     for pf in (4, 8, 12):  # prefetch ring depth (D = 5 / 10 / 15 rows)
         for seg in (0, 16, 24, 32, 40):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
-                (lambda seg=seg, pf=pf: _native.check(L.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg,
+                (lambda seg=seg, pf=pf: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg,
                                                                          pf, 1, swx, swy, 0))), sref)
     for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
         f = ops.get_filter(fname)
@@ -131,19 +132,19 @@ def main():
     variants["copy/torch"] = ((lambda: O().copy_(I())), img)
     for v, d, seg in ((2, 4, 8), (2, 4, 24), (2, 8, 24), (4, 4, 8), (4, 4, 24), (4, 8, 24), (4, 2, 24), (4, 4, 48)):
         variants[f"copy/strip-v{v}-d{d}-seg{seg}"] = (
-            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
+            (lambda v=v, d=d, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
                                                                             seg, 0))), img)
     for v, d, seg in ((2, 104, 8), (2, 104, 24), (4, 104, 8), (4, 104, 24), (4, 104, 64)):  # 16 waves per block
         variants[f"copy/strip-v{v}-d{d - 100}-seg{seg}-wpb16"] = (
-            (lambda v=v, d=d, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
+            (lambda v=v, d=d, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
                                                                             seg, 0))), img)
     for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
         variants[f"copy/linear-{nm}"] = (
-            (lambda d=d: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
+            (lambda d=d: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
     for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26)] + [(16, 0), (16, 4)]:
         if True:  # row bands, 16-B vector per thread (ref None: XOR of rows, no reference)
             variants[f"copy/band-seg{seg}-f{fl}"] = (
-                (lambda fl=fl, seg=seg: _native.check(L.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
+                (lambda fl=fl, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
                                                                               fl, seg, 0))), None)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):

@@ -159,6 +159,8 @@ def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
             continue
         if r is b:  # the baseline itself, whatever its rounding
             r["efficiency"] = 1.0
+            if r["kind"] == "strong":
+                r["speedup"] = 1.0
             if rehearse:
                 r["retained"] = 1.0
             continue
@@ -174,41 +176,10 @@ def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
 
 
 def plot(rows: List[dict], path: str, title: str) -> Optional[str]:
-    try:
-        import matplotlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from cuda_mpi_openmp_amd.utils.plots import scaling_figure
 
-        matplotlib.use("Agg")
-        import matplotlib.pyplot as plt
-    except Exception:  # noqa: BLE001
-        return None
-    fig, (ax1, ax2) = plt.subplots(1, 2, figsize=(13, 5))
-    ns = sorted({r["n"] for r in rows})
-    for name in sorted({r["name"] for r in rows if r["kind"] == "weak"}):
-        pts = [(r["n"], r["value"]) for r in rows if r["name"] == name and r["status"] == "ok" and r.get("value")]
-        b = [v for n, v in pts if n == 1]
-        if pts and b:  # workloads have different units: plot throughput relative to one rank
-            ax1.plot([n for n, _ in pts], [v / b[0] for _, v in pts], marker="o", label=name)
-    ax1.plot(ns, ns, ls=":", color="gray", label="ideal")
-    ax1.set_xlabel("GPUs")
-    ax1.set_ylabel("whole-job throughput / 1-rank throughput")
-    ax1.set_title("weak scaling (dotted: ideal)")
-    ax1.set_xticks(ns)
-    ax1.legend(fontsize=8)
-    for name in sorted({r["name"] for r in rows if r["kind"] == "strong"}):
-        pts = [(r["n"], r["speedup"]) for r in rows if r["name"] == name and r.get("speedup")]
-        if pts:
-            ax2.plot(*zip(*pts), marker="o", label=name)
-    ax2.plot(ns, ns, ls=":", color="gray", label="ideal")
-    ax2.set_xlabel("GPUs")
-    ax2.set_ylabel("speedup vs 1 GPU")
-    ax2.set_title("strong scaling: Jacobi 16384^2 fp64")
-    ax2.set_xticks(ns)
-    ax2.legend(fontsize=8)
-    fig.suptitle(title)
-    fig.tight_layout()
-    fig.savefig(path, dpi=150)
-    plt.close(fig)
-    return path
+    return scaling_figure(rows, path, title)
 
 
 def main(argv=None) -> int:
