@@ -238,8 +238,11 @@ bool jacobi_one_device_equal(const std::vector<uint8_t> &init, const std::vector
     T *u, *un;
     HIP_OK(hipMalloc(&u, bytes));
     HIP_OK(hipMalloc(&un, bytes));
-    HIP_OK(hipMemcpy(u, init.data(), bytes, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(un, u, bytes, hipMemcpyDeviceToDevice));
+    // on s, not the null stream: s is non-blocking, and a pageable hipMemcpy
+    // may return before its last DMA chunk has landed (the kernels below would
+    // read a partly copied field)
+    HIP_OK(hipMemcpyAsync(u, init.data(), bytes, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(un, u, bytes, hipMemcpyDeviceToDevice, s));
     for (int i = 0; i < iters; ++i) {
         if constexpr (sizeof(T) == 8) MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, 1, grows + 1, nullptr, s));
         else MPX_OK_OR_DIE(mpx_jacobi_f32(u, un, cols, cols, 1, grows + 1, nullptr, s));
@@ -272,6 +275,24 @@ bool jacobi_one_device_equal(const std::vector<uint8_t> &init, const std::vector
     if (bad)
         fprintf(stderr, "[mpx_mgpu] one-device mismatch: %lld elements, rows %d..%d, cols %d..%d, max |diff| %.3g\n", bad,
                 r_lo, r_hi, c_lo, c_hi, dmax);
+    if (bad && std::getenv("MPX_MGPU_CPU_REF")) {  // arbiter: the same sweeps on the CPU
+        std::vector<T> a(bytes / sizeof(T)), b;
+        std::memcpy(a.data(), init.data(), bytes);
+        b = a;
+        for (int i = 0; i < iters; ++i) {
+            if constexpr (sizeof(T) == 8) mpx_cpu_jacobi_f64(a.data(), b.data(), cols, cols, 1, grows + 1);
+            else cpu_sweep_f32(a.data(), b.data(), cols, 1, grows + 1);
+            std::swap(a, b);
+        }
+        const size_t n = (size_t)(grows + 2) * cols;
+        size_t d1 = 0, dn = 0;
+        for (size_t k = (size_t)cols; k < n - cols; ++k) {
+            d1 += a[k] != reinterpret_cast<const T *>(got.data())[k];
+            dn += a[k] != reinterpret_cast<const T *>(fin.data())[k];
+        }
+        fprintf(stderr, "[mpx_mgpu] CPU arbiter: one-device differs from the CPU in %zu elements, N ranks in %zu\n", d1,
+                dn);
+    }
     return bad == 0;
 }
 
@@ -488,13 +509,14 @@ void jacobi_peer_worker(const Args &a, Shared &sh, int rank) {
     // then one sweep of the first owned rows against the CPU reference
     if (rank > 0 && a.halo != "none") {  // the upper neighbour's current u: swapped `it` times like ours
         const T *nb_u = static_cast<const T *>(it % 2 ? sh.peer_un[rank - 1] : sh.peer_u[rank - 1]);
-        HIP_OK(hipMemcpy(u, nb_u + Slab(grows, sh.world, rank - 1).rows * cols, row_bytes, hipMemcpyDefault));
+        HIP_OK(hipMemcpyAsync(u, nb_u + Slab(grows, sh.world, rank - 1).rows * cols, row_bytes, hipMemcpyDefault, s));
     }
     // rows 1..vr need row vr + 1: stay clear of the lower halo row (not pulled)
     const long long vr = std::max<long long>(
         1, std::min<long long>(rank + 1 < sh.world && a.halo != "none" ? rows - 1 : rows, 8));
     std::vector<T> hu_((vr + 2) * cols), hun((vr + 2) * cols), gun((vr + 2) * cols);
-    HIP_OK(hipMemcpy(hu_.data(), u, (vr + 2) * row_bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpyAsync(hu_.data(), u, (vr + 2) * row_bytes, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
     hun = hu_;
     if constexpr (sizeof(T) == 8) {
         MPX_OK_OR_DIE(mpx_jacobi_f64(u, un, cols, cols, 1, (int)vr + 1, nullptr, s));

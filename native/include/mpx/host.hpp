@@ -222,6 +222,10 @@ class Parts {
         const TimingPolicy pol = TimingPolicy::from_env();
         for (int i = 0; i < size(); ++i) {
             use(i);
+            // the parts' streams are non-blocking: a pageable hipMemcpy that
+            // filled the inputs may return before its last DMA chunk lands, and
+            // nothing orders it before this stream's kernels — drain the device
+            HIP_CHECK(hipDeviceSynchronize());
             init_stream_queue(p_[i].stream);
         }
         for (int w = 0; w < pol.warmups; ++w) {
