@@ -86,11 +86,16 @@ $(ALIB): $(LIB_OBJS) | $(B)
 	rm -f $@ && ar rcs $@ $(LIB_OBJS)
 
 # ---- GPU programs: two personalities from one source ----
-labs/lab%/src/to_plot_hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS) | $(LABS)
-	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
+# linked against libmpx.so (one copy of the kernels on disk, not one per
+# program); found through the build tree's absolute path (tests copy a lab to
+# a scratch directory) and, relocated, next to the repository layout
+LIBDIR    := $(abspath $(dir $(PYLIB)))
+SOLINK    := -L$(LIBDIR) -lmpx -Wl,-rpath,$(LIBDIR)
+labs/lab%/src/to_plot_hip_exe: native/apps/lab%_gpu.cpp $(PYLIB) $(HDRS) | $(LABS)
+	$(HIPCC) $(HIPFLAGS) $< $(SOLINK) -Wl,-rpath,'$$ORIGIN/../../../cuda_mpi_openmp_amd/_lib' -lgomp -lm -ldl -o $@
 
-labs/lab%/src/hip_exe: native/apps/lab%_gpu.cpp $(ALIB) $(HDRS) | $(LABS)
-	$(HIPCC) $(HIPFLAGS) -DMPX_SUBMISSION $< -x none $(ALIB) -lgomp -lm -ldl -o $@
+labs/lab%/src/hip_exe: native/apps/lab%_gpu.cpp $(PYLIB) $(HDRS) | $(LABS)
+	$(HIPCC) $(HIPFLAGS) -DMPX_SUBMISSION $< $(SOLINK) -Wl,-rpath,'$$ORIGIN/../../../cuda_mpi_openmp_amd/_lib' -lgomp -lm -ldl -o $@
 
 # ---- CPU references: serial -O0 (published methodology) and OpenMP -O3 ----
 labs/lab%/src/cpu_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $(HDRS) | $(LABS)
@@ -102,12 +107,12 @@ labs/lab%/src/cpu_omp_exe: native/apps/lab%_cpu.c native/src/cpu/cpu_kernels.c $
 labs/lab3/src/read_input_exe: native/apps/lab3_read_input.c | $(LABS)
 	$(CC) $(CSER) $< -o $@
 
-bin/gpu_info: native/apps/gpu_info.cpp $(ALIB) $(HDRS) | $(B)
-	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -lgomp -lm -ldl -o $@
+bin/gpu_info: native/apps/gpu_info.cpp $(PYLIB) $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) $< $(SOLINK) -Wl,-rpath,'$$ORIGIN/../cuda_mpi_openmp_amd/_lib' -lgomp -lm -ldl -o $@
 
 # native multi-GPU runtime: links /opt/rocm's RCCL directly (no torch in this process)
-bin/mpx_mgpu: native/apps/mpx_mgpu.cpp $(ALIB) $(HDRS) | $(B)
-	$(HIPCC) $(HIPFLAGS) $< -x none $(ALIB) -L$(ROCM)/lib -lrccl -lgomp -lm -ldl -lpthread -Wl,-rpath,$(ROCM)/lib -o $@
+bin/mpx_mgpu: native/apps/mpx_mgpu.cpp $(PYLIB) $(HDRS) | $(B)
+	$(HIPCC) $(HIPFLAGS) $< $(SOLINK) -Wl,-rpath,'$$ORIGIN/../cuda_mpi_openmp_amd/_lib' -L$(ROCM)/lib -lrccl -lgomp -lm -ldl -lpthread -Wl,-rpath,$(ROCM)/lib -o $@
 
 bin/hw1: native/apps/hw1_quadratic.c | $(B)
 	$(CC) $(CSER) $< -lm -o $@

@@ -93,6 +93,8 @@ _SIGNATURES = {
     "mpx_cpu_vsub_f64": (None, [c_vp, c_vp, c_vp, c_i64]),
     "mpx_cpu_vsub_f32": (None, [c_vp, c_vp, c_vp, c_i64]),
     "mpx_cpu_roberts": (None, [c_vp, c_vp, c_int, c_int]),
+    "mpx_cpu_roberts_rgb": (None, [c_vp, c_vp, c_int, c_int]),
+    "mpx_roberts_rgb": (c_int, [c_vp, c_vp, c_int, c_int, c_vp]),
     "mpx_cpu_conv": (None, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp]),
     "mpx_cpu_classify": (None, [c_vp, c_i64, c_int, _dp, _dp]),
     "mpx_cpu_jacobi_f64": (ctypes.c_double, [c_vp, c_vp, c_int, c_int, c_int, c_int]),

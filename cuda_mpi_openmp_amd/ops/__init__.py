@@ -3,7 +3,7 @@ OpenMP C references (CPU tensors) of libmpx."""
 
 from .classify import class_stats, classify_
 from .classify import plan as classify_plan
-from .edge import ConvLauncher, conv, conv_rows, roberts
+from .edge import ConvLauncher, conv, conv_rows, roberts, roberts_rgb
 from .filters import Filter, get_filter, list_filters
 from .sort import sort_
 from .stencil import jacobi_sweep
@@ -17,6 +17,7 @@ __all__ = [
     "ConvLauncher",
     "conv_rows",
     "roberts",
+    "roberts_rgb",
     "Filter",
     "get_filter",
     "list_filters",

@@ -43,6 +43,27 @@ def roberts(img: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
+def roberts_rgb(img: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-channel Roberts cross with the L1 magnitude: each colour channel
+    becomes min(255, |c(x,y) - c(x+1,y+1)| + |c(x+1,y) - c(x,y+1)|),
+    clamp-to-edge, alpha kept. The operator of the reference's extra lab2
+    samples (``/root/reference/lab2/test_data/lenna{,_out}.data``, carried in
+    ``labs/lab2/test_data``): byte-exact there; no reference program computes
+    it."""
+    h, w = check_image(img)
+    if out is None:
+        out = torch.empty_like(img)
+    check_image(out, "out")
+    if out.data_ptr() == img.data_ptr():
+        raise ValueError("roberts_rgb: in-place is not supported")
+    L = _native.lib()
+    if img.is_cuda:
+        _native.check(L.mpx_roberts_rgb(img.data_ptr(), out.data_ptr(), w, h, _native.stream_of(img)))
+    else:
+        L.mpx_cpu_roberts_rgb(img.data_ptr(), out.data_ptr(), w, h)
+    return out
+
+
 def _conv_args(src: torch.Tensor, out: torch.Tensor, filt: Filter, src_row0: int, out_row0: int, oy0: int,
                oy1: int, y_lo: int, y_hi: int) -> tuple:
     hs, w = check_image(src, "src")

@@ -40,6 +40,17 @@ def roberts(img: torch.Tensor) -> torch.Tensor:
     return _gray(g, img.cpu()[..., 3])
 
 
+def roberts_rgb(img: torch.Tensor) -> torch.Tensor:
+    """Per-channel Roberts cross, L1 magnitude, saturated; alpha kept."""
+    x = img.cpu().to(torch.int32)
+    xd = torch.cat([x[1:], x[-1:]], dim=0)
+    xr = torch.cat([x[:, 1:], x[:, -1:]], dim=1)
+    xdr = torch.cat([xd[:, 1:], xd[:, -1:]], dim=1)
+    g = ((x - xdr).abs() + (xr - xd).abs()).clamp(max=255)
+    g[..., 3] = x[..., 3]
+    return g.to(torch.uint8)
+
+
 def conv(img: torch.Tensor, filt: Filter) -> torch.Tensor:
     y = luma(img.cpu())
     up, down = filt.anchor, filt.k - 1 - filt.anchor

@@ -55,6 +55,9 @@ int mpx_vsub_f32(const float *a, const float *b, float *c, int64_t n, int grid, 
  * (reference lab2/src/to_plot.cu:57-64,106). Each thread owns 4 pixels of a row. */
 int mpx_roberts(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by, int gx, int gy,
                 void *stream);
+/* Per-channel Roberts cross, L1 magnitude, saturated to 255, alpha kept (the
+ * operator of the reference's lab2/test_data samples; mpx_cpu_roberts_rgb). */
+int mpx_roberts_rgb(const uint32_t *in, uint32_t *out, int w, int h, void *stream);
 
 /* ---------------- lab2 generalisation: KxK convolution on luminance ---------------- */
 /*
@@ -270,6 +273,7 @@ int mpx_cpu_threads(void);
 void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n);
 void mpx_cpu_vsub_f32(const float *a, const float *b, float *c, int64_t n);
 void mpx_cpu_roberts(const uint32_t *in, uint32_t *out, int w, int h);
+void mpx_cpu_roberts_rgb(const uint32_t *in, uint32_t *out, int w, int h);
 void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
                   int y_hi, int k, int anchor, int mode, const float *wx, const float *wy);
 void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv);

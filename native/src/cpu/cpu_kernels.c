@@ -212,6 +212,33 @@ void mpx_cpu_roberts(const uint32_t *in, uint32_t *out, int w, int h) {
     }
 }
 
+/* Per-channel Roberts cross, L1 magnitude: every colour channel c of
+ * pixel (x, y) becomes min(255, |c(x,y) - c(x+1,y+1)| + |c(x+1,y) - c(x,y+1)|)
+ * with clamp-to-edge neighbours, alpha kept. The operator behind the
+ * reference's lab2/test_data/lenna_out.data (byte-exact on all 512 x 512
+ * pixels; no reference program computes it). Integer arithmetic. */
+void mpx_cpu_roberts_rgb(const uint32_t *in, uint32_t *out, int w, int h) {
+    int y;
+#pragma omp parallel for schedule(static)
+    for (y = 0; y < h; ++y) {
+        const int y1 = y + 1 < h ? y + 1 : h - 1;
+        for (int x = 0; x < w; ++x) {
+            const int x1 = x + 1 < w ? x + 1 : w - 1;
+            const uint32_t a = in[(int64_t)y * w + x], b = in[(int64_t)y * w + x1];
+            const uint32_t c = in[(int64_t)y1 * w + x], d = in[(int64_t)y1 * w + x1];
+            uint32_t o = a & 0xff000000u;
+            for (int ch = 0; ch < 24; ch += 8) {
+                const int va = (int)((a >> ch) & 255u), vb = (int)((b >> ch) & 255u);
+                const int vc = (int)((c >> ch) & 255u), vd = (int)((d >> ch) & 255u);
+                int g = abs(va - vd) + abs(vb - vc);
+                g = g > 255 ? 255 : g;
+                o |= (uint32_t)g << ch;
+            }
+            out[(int64_t)y * w + x] = o;
+        }
+    }
+}
+
 static inline float conv_finish(int mode, float gx, float gy) {
     if (mode == MPX_CONV_MAG2) {
         const float a = gx * gx;

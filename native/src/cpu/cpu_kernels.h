@@ -22,6 +22,7 @@ int mpx_cpu_threads(void);
 void mpx_cpu_vsub_f64(const double *a, const double *b, double *c, int64_t n);
 void mpx_cpu_vsub_f32(const float *a, const float *b, float *c, int64_t n);
 void mpx_cpu_roberts(const uint32_t *in, uint32_t *out, int w, int h);
+void mpx_cpu_roberts_rgb(const uint32_t *in, uint32_t *out, int w, int h);
 void mpx_cpu_conv(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo,
                   int y_hi, int k, int anchor, int mode, const float *wx, const float *wy);
 void mpx_cpu_classify(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv);

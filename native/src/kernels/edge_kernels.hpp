@@ -585,6 +585,7 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
     // scheduler sinks prefetches towards their first use (lower register
     // pressure), which turns the ring back into load-then-wait.
     const int iy_last = ye - 1 + (K - 1 - A);  // last input row (upward walk: input row 0)
+    const int i_last = ye - ys + K - 2;          // the walk's last input row index
     auto load_row = [&](int i) -> uint2 {
         const int gy = mpx_clampi(up ? iy_last - i : iy0 + i, y_lo, y_hi);
         // wave-uniform row source select (scalar): own slab or a neighbour's
@@ -600,10 +601,12 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
         } else if constexpr (VEC) {  // w even: the pair is entirely inside, left or right (BUFLD 1, 3)
             // buffer load: the row base lives in the (scalar) descriptor and the
             // lane's byte offset is loop-invariant — no per-row address VALU
+            // (the ring's loads past the walk's last input row are never
+            // consumed: out-of-range offset, dropped by the hardware)
             const __amdgpu_buffer_rsrc_t rrow = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0,
                                                                                   w * 4, 0x00020000);
             typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-            const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rrow, cc * 4, 0, 0);
+            const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rrow, i <= i_last ? cc * 4 : 0x7ffffff0, 0, 0);
             r = make_uint2(v.x, v.y);
         } else {
             r = make_uint2(row[mpx_clampi(cin, 0, w - 1)], row[mpx_clampi(cin + 1, 0, w - 1)]);
@@ -827,21 +830,27 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const uint32_t *src = gy < 0 ? rs.up : (gy >= rs.own_rows ? rs.dn : in);
         return src + (int64_t)gy * pitch;
     };
+    // the prefetch ring runs D rows past the walk's last input row (nrows + K - 2);
+    // those loads are never consumed: their offsets go out of range, so the
+    // hardware drops them instead of fetching a neighbour segment's rows
+    const int i_last = ye - ys + K - 2;
     auto load_row = [&](int i, u32x2_t &ap) -> u32x4_t {
-        const uint32_t *row = row_ptr(i);
+        const uint32_t *row = row_ptr(min(i, i_last));
         const __amdgpu_buffer_rsrc_t rr =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, w * 4, 0x00020000);
+        const bool live = i <= i_last;  // wave-uniform
+        const int qo = live ? cc * 4 : kDrop, ao = live ? ap_off : kDrop;
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
         // non-temporal; bit 6: every row does (probes)
         if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
-            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, (OPT & 64) ? 2 : 0);
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, (OPT & 64) ? 2 : 0);
         } else if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
-            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 2);
-            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, (OPT & 128) ? 0 : 2);
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 2);
+            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ao, 0, (OPT & 128) ? 0 : 2);
         } else {
-            q = __builtin_amdgcn_raw_buffer_load_b128(rr, cc * 4, 0, 0);
-            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ap_off, 0, 0);
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 0);
+            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ao, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         return q;

@@ -233,6 +233,59 @@ int roberts_impl(const uint32_t *in, uint32_t *out, int w, int h, int bx, int by
     return MPX_OK;
 }
 
+// Per-channel Roberts cross, L1 magnitude (mpx_cpu_roberts_rgb; the operator
+// of the reference's lab2/test_data samples). Byte-exact integer math. One
+// thread per aligned 16-B quad of 4 pixels (w % 4 == 0) or per pixel (VEC 1):
+// the quad, the pixel right of it, and the same from the row below (clamped).
+__device__ __forceinline__ uint32_t roberts_rgb_px(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    uint32_t o = a & 0xff000000u;
+#pragma unroll
+    for (int ch = 0; ch < 24; ch += 8) {
+        const int va = (int)__builtin_amdgcn_ubfe(a, ch, 8), vb = (int)__builtin_amdgcn_ubfe(b, ch, 8);
+        const int vc = (int)__builtin_amdgcn_ubfe(c, ch, 8), vd = (int)__builtin_amdgcn_ubfe(d, ch, 8);
+        o |= (uint32_t)min(abs(va - vd) + abs(vb - vc), 255) << ch;
+    }
+    return o;
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void roberts_rgb_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                          int w, int h) {
+    const int per_row = w / VEC;
+    const int64_t total = (int64_t)per_row * h;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(t / per_row), x = (int)(t - (int64_t)y * per_row) * VEC;
+        const int y1 = min(y + 1, h - 1), xr = min(x + VEC, w - 1);
+        const uint32_t *r0 = in + (int64_t)y * w, *r1 = in + (int64_t)y1 * w;
+        if constexpr (VEC == 4) {
+            const uint4 q0 = *reinterpret_cast<const uint4 *>(r0 + x), q1 = *reinterpret_cast<const uint4 *>(r1 + x);
+            const uint32_t e0 = r0[xr], e1 = r1[xr];
+            uint4 o;
+            o.x = roberts_rgb_px(q0.x, q0.y, q1.x, q1.y);
+            o.y = roberts_rgb_px(q0.y, q0.z, q1.y, q1.z);
+            o.z = roberts_rgb_px(q0.z, q0.w, q1.z, q1.w);
+            o.w = roberts_rgb_px(q0.w, e0, q1.w, e1);
+            *reinterpret_cast<uint4 *>(out + (int64_t)y * w + x) = o;
+        } else {
+            out[(int64_t)y * w + x] = roberts_rgb_px(r0[x], r0[xr], r1[x], r1[xr]);
+        }
+    }
+}
+
+int roberts_rgb_impl(const uint32_t *in, uint32_t *out, int w, int h, void *stream) {
+    MPX_CHECK_ARG(in && out && w > 0 && h > 0, "bad image");
+    MPX_CHECK_ARG(in != out, "in-place is not supported (neighbours are read after the write)");
+    const bool vec = w % 4 == 0 && aligned16(in) && aligned16(out);
+    const int64_t work = (int64_t)w * h / (vec ? 4 : 1);
+    const int grid = (int)std::min<int64_t>((work + 255) / 256, (int64_t)kNumCUs * 16);
+    if (vec)
+        hipLaunchKernelGGL(roberts_rgb_kernel<4>, dim3(grid), dim3(256), 0, as_stream(stream), in, out, w, h);
+    else
+        hipLaunchKernelGGL(roberts_rgb_kernel<1>, dim3(grid), dim3(256), 0, as_stream(stream), in, out, w, h);
+    MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    return MPX_OK;
+}
+
 MPX_MODULE_ANCHOR(edge_roberts)
 
 }  // namespace mpx
@@ -242,3 +295,6 @@ extern "C" int mpx_roberts(const uint32_t *in, uint32_t *out, int w, int h, int 
     return mpx::roberts_impl(in, out, w, h, bx, by, gx, gy, stream);
 }
 
+extern "C" int mpx_roberts_rgb(const uint32_t *in, uint32_t *out, int w, int h, void *stream) {
+    return mpx::roberts_rgb_impl(in, out, w, h, stream);
+}

@@ -354,6 +354,26 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// The same peer mask on the VALU: one ballot per digit bit, each lane keeping
+// the lanes whose bit agrees with its own, m &= ~(ballot ^ own) (one
+// v_bitop3_b32 per 32-bit half on gfx950): 8 x (bfe + cmp + 2 bitop3) VALU
+// per 64 keys and no LDS. The LDS table costs 3 random-address LDS ops per 64
+// keys whose bank conflicts (a half-wave's 32 lanes land on 16 even banks)
+// were ~21 of the scatter's ~35 extra LDS cycles per slice
+// (profiles/lab5_sort.md); the VALU had room (51.6M instructions in ~190 us).
+// `key` is the whole key: bit `shift + b` is digit bit b.
+__device__ __forceinline__ uint64_t match_digit_valu(uint32_t key, int shift) {
+    uint32_t lo = ~0u, hi = ~0u;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint32_t own = (uint32_t)__builtin_amdgcn_sbfe((int)key, shift + b, 1);  // 0 or ~0
+        const uint64_t B = __ballot(own != 0u);
+        lo &= ~((uint32_t)B ^ own);
+        hi &= ~((uint32_t)(B >> 32) ^ own);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Digit pass. LOOKBACK (onesweep): the tile id comes from an atomic counter
 // and the global digit offsets from decoupled look-back over `status`.
 // !LOOKBACK (reduce-then-scan): the tile id is the XCD-remapped block id and
@@ -525,6 +545,9 @@ __device__ __forceinline__ uint32_t scan256_excl_lds(uint32_t v, uint32_t *s_wsu
 // are LDS-only so the prefetch stays in flight across them.
 constexpr int kPersistBlocksPerCU = 2;
 
+// VALU_MATCH: peer masks from ballots (match_digit_valu, production) or from
+// the LDS table (match_digit_lds, the round-2 form: tuning variant 4).
+template <bool VALU_MATCH>
 __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift, int in_mode, int out_mode,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
@@ -557,7 +580,7 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + tile] : 0u;
         for (int i = t; i < kRWaves * 256; i += kRThreads) {
             (&s_cnt[0][0])[i] = 0;
-            reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
+            if (!VALU_MATCH) reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
         }
         lds_barrier();
         uint32_t key[kRPer], rank[kRPer];
@@ -572,7 +595,9 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int g = 0; g < kRPer; g += kRG) {
             uint64_t m[kRG];
 #pragma unroll
-            for (int e = 0; e < kRG; ++e) m[e] = match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
+            for (int e = 0; e < kRG; ++e)
+                m[e] = VALU_MATCH ? match_digit_valu(key[g + e], shift)
+                                  : match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
             uint32_t old[kRG], pre[kRG];
 #pragma unroll
             for (int e = 0; e < kRG; ++e) {
@@ -652,8 +677,66 @@ __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *
     cnt[(size_t)t * ntiles + tile] = c;
 }
 
-// reduce-then-scan, step 2: one block per digit turns its row of tile counts
-// into exclusive offsets in place and records the digit total
+// reduce-then-scan, step 2 (production): one 1024-thread block per digit
+// turns its row of tile counts into exclusive offsets in place and records
+// the digit total. 8192 counts per round (2^26 keys: one round); a thread owns
+// 8 consecutive counts, read from LDS as two 16-byte pieces. The 256-thread
+// form below took 15.3 us per pass at 2^26 in two dependent rounds.
+constexpr int kScanThreads = 1024;
+__device__ __forceinline__ uint32_t scan1024_excl(uint32_t v, uint32_t *s_wsum) {
+    const int t = threadIdx.x, lane = t & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wsum[t >> 6] = x;
+    __syncthreads();
+    uint32_t add = 0;
+    for (int w = 0; w < (t >> 6); ++w) add += s_wsum[w];
+    __syncthreads();  // s_wsum may be reused by the caller
+    return x - v + add;
+}
+
+__global__ __launch_bounds__(kScanThreads) void radix_scan1024_kernel(uint32_t *__restrict__ cnt, int ntiles,
+                                                                      uint32_t *__restrict__ tot) {
+    constexpr int kChunk = kScanThreads * 8;
+    __shared__ uint4 v4[kChunk / 4];
+    __shared__ uint32_t s_wsum[kScanThreads / 64];
+    uint32_t *v = reinterpret_cast<uint32_t *>(v4);
+    const int t = threadIdx.x;
+    uint32_t *row = cnt + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < ntiles; c0 += kChunk) {
+        const int m = min(kChunk, ntiles - c0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = t + k * kScanThreads;
+            v[i] = i < m ? row[c0 + i] : 0u;
+        }
+        __syncthreads();
+        const uint4 a = v4[2 * t], b = v4[2 * t + 1];
+        const uint32_t own = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+        uint32_t run = carry + scan1024_excl(own, s_wsum);
+        uint4 ea, eb;
+        ea.x = run, run += a.x, ea.y = run, run += a.y, ea.z = run, run += a.z, ea.w = run, run += a.w;
+        eb.x = run, run += b.x, eb.y = run, run += b.y, eb.z = run, run += b.z, eb.w = run, run += b.w;
+        v4[2 * t] = ea, v4[2 * t + 1] = eb;
+        if (t == kScanThreads - 1) s_wsum[0] = run;  // carry for the next round
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = t + k * kScanThreads;
+            if (i < m) row[c0 + i] = v[i];
+        }
+        carry = s_wsum[0];
+        __syncthreads();
+    }
+    if (t == 0) tot[blockIdx.x] = carry;
+}
+
+// the round-2 scan (256 threads, 4096 counts per round): tuning variant 4
 __global__ __launch_bounds__(256) void radix_scan_kernel(uint32_t *__restrict__ cnt, int ntiles,
                                                          uint32_t *__restrict__ tot) {
     constexpr int kChunk = 256 * 16;
@@ -714,7 +797,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 
 // Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan
 // (one tile per block), 3 = reduce-then-scan with the persistent prefetching
-// scatter.
+// scatter (ballot peer masks, 1024-thread scan), 4 = variant 3 as in round 2
+// (LDS-table peer masks, 256-thread scan; same-process A/B).
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
@@ -749,12 +833,20 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             hipLaunchKernelGGL(radix_count_kernel, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src, n, 8 * p,
                                in_mode, r.status, ntiles);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            hipLaunchKernelGGL(radix_scan_kernel, dim3(256), dim3(256), 0, s, r.status, ntiles, r.hist);
+            if (variant == 4)
+                hipLaunchKernelGGL(radix_scan_kernel, dim3(256), dim3(256), 0, s, r.status, ntiles, r.hist);
+            else
+                hipLaunchKernelGGL(radix_scan1024_kernel, dim3(256), dim3(kScanThreads), 0, s, r.status, ntiles,
+                                   r.hist);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            if (variant == 3) {
+            if (variant >= 3) {
                 const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
-                hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src, dst, n,
-                                   8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
+                if (variant == 3)
+                    hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
+                                       dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
+                else
+                    hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
+                                       dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
             } else {
                 hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst,
                                    n, 8 * p, in_mode, out_mode, r.hist, r.status, r.ctr, r.err, ntiles);
@@ -903,11 +995,11 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream);
 }
 
-// Tuning entry (tools/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
+// Tuning entry (tools/experiments/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
 // (decoupled look-back), 2 = reduce-then-scan, 3 = reduce-then-scan with the
 // persistent scatter.
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 3) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 4) return MPX_ERR_ARG;
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }

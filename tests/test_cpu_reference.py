@@ -173,3 +173,28 @@ def test_production_library_exports_no_tuning_entry_points():
     for name in ("mpx_conv_variant", "mpx_strip_copy_probe", "mpx_selftest_fast_sqrt"):
         assert not hasattr(L, name), name
         assert hasattr(_native.tune_lib(), name), name
+
+
+LAB2_SAMPLES = os.path.join(os.path.dirname(LAB2_DATA), "test_data")
+
+
+def _sample(name):
+    with open(os.path.join(LAB2_SAMPLES, name), "rb") as f:
+        return bytes_to_img(f.read())
+
+
+def test_roberts_rgb_pins_reference_sample():
+    """The reference's extra lab2 sample (lenna -> lenna_out, 512 x 512) is
+    per-channel Roberts with the L1 magnitude: byte-exact, native CPU path and
+    torch reference. (world_map_processed_test.data is a constant (27, 30,
+    27) image no operator of the input produces: not carried, parity
+    unpinned.)"""
+    src, want = _sample("lenna.data"), _sample("lenna_out.data")
+    assert torch.equal(ref.roberts_rgb(src), want)
+    assert torch.equal(ops.roberts_rgb(src), want)
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (1, 7), (5, 1), (33, 47), (64, 64)])
+def test_roberts_rgb_cpu_matches_torch(hw):
+    img = rand_img(*hw, seed=hw[0] * 100 + hw[1])
+    assert torch.equal(ops.roberts_rgb(img), ref.roberts_rgb(img))

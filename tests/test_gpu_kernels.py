@@ -384,3 +384,22 @@ def test_conv_alternating_segments_exact(gpu, hw, seg):
     _native.check(L.mpx_conv_variant(d.data_ptr(), out.data_ptr(), hw[1], hw[0], 5, 3, seg, 2000, 1, wx, wy, 0))
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ops.conv(img, f))
+
+
+def test_roberts_rgb_gpu_pins_reference_sample(gpu):
+    """Per-channel Roberts (L1) on the device: byte-exact against the
+    reference's lenna_out.data sample."""
+    d = os.path.join(os.path.dirname(LAB2_DATA), "test_data")
+    with open(os.path.join(d, "lenna.data"), "rb") as f:
+        src = bytes_to_img(f.read())
+    with open(os.path.join(d, "lenna_out.data"), "rb") as f:
+        want = bytes_to_img(f.read())
+    assert torch.equal(ops.roberts_rgb(src.to(gpu)).cpu(), want)
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (3, 5), (17, 64), (130, 257), (1024, 1000), (4096, 4096)])
+def test_roberts_rgb_gpu_matches_cpu(gpu, hw):
+    """Both launch forms (16-B quads when w % 4 == 0, per pixel otherwise),
+    image edges included, against the native CPU reference."""
+    img = rand_img(*hw, seed=hw[0] + hw[1])
+    assert torch.equal(ops.roberts_rgb(img.to(gpu)).cpu(), ops.roberts_rgb(img))
