@@ -18,6 +18,10 @@ def test_scale_driver_cpu_dry_run(tmp_path):
     assert two["status"] == "ok" and two["n_reported"] == 2 and two["verified"] is True, two
     assert two["efficiency"] is not None and two["world_size_seen"]["torch_distributed"] == 2, two
     assert runs[("conv/peer", 2)]["status"] == "skipped" and runs[("conv/peer", 2)]["reason"]
+    # the streaming conv (bench.py value_streaming) is its own curve, verified N-rank == one-device
+    st1, st2 = runs[("conv-stream/peer", 1)], runs[("conv-stream/rccl", 2)]
+    assert st1["status"] == "ok" and st1["efficiency"] == 1.0 and st1["verified"] is True, st1
+    assert st2["status"] == "ok" and st2["verified"] is True and st2["efficiency"] is not None, st2
     assert (tmp_path / "scaling.csv").exists() and (tmp_path / "scaling.png").exists()
 
 

@@ -227,8 +227,24 @@ def main(argv=None) -> int:
                     else:
                         row["stderr_tail"] = res.get("stderr_tail")
                 rows.append(row)
-                print(json.dumps({k: row.get(k) for k in ("name", "n", "status", "value", "unit", "ms", "transport",
-                                                           "reason")}), flush=True)
+                # bench.py's streaming conv (each step convolves the previous
+                # output: halos with a real inter-rank dependency) as its own curve
+                rec = res["record"] if not job["skip"] and res["status"] == "ok" else {}
+                if job["name"].startswith("conv/") and (job["skip"] or rec.get("value_streaming") is not None):
+                    srow = {"name": job["name"].replace("conv/", "conv-stream/"), "kind": "weak", "n": n,
+                            "cmd": row["cmd"], "status": row["status"]}
+                    if job["skip"]:
+                        srow["reason"] = job["skip"]
+                    else:
+                        srow.update(value=float(rec["value_streaming"]), unit=rec.get("unit"),
+                                    ms=rec.get("ms_per_step_streaming"), n_reported=rec.get("n_gpus"),
+                                    transport=rec.get("transport_streaming"),
+                                    world_size_seen=rec.get("world_size_seen"),
+                                    verified=rec.get("verified_bit_exact_streaming"), wall_s=row.get("wall_s"))
+                    rows.append(srow)
+                for r in rows[-2:] if rows[-1] is not row else [row]:
+                    print(json.dumps({k: r.get(k) for k in ("name", "n", "status", "value", "unit", "ms", "transport",
+                                                             "reason")}), flush=True)
     efficiencies(rows, a.rehearse)
     meta = {"devices_visible": ndev, "device": a.device, "rehearse": a.rehearse, "gpus": ns,
             "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
