@@ -547,7 +547,10 @@ constexpr int kPersistBlocksPerCU = 2;
 
 // VALU_MATCH: peer masks from ballots (match_digit_valu, production) or from
 // the LDS table (match_digit_lds, the round-2 form: tuning variant 4).
-template <bool VALU_MATCH>
+// REV: walk each XCD's tile range from its end (tuning variant 5): the count
+// kernel that just read this pass's input finished with the range ends, so
+// those tiles are the likeliest to still sit in the 256 MB MALL.
+template <bool VALU_MATCH, bool REV = false>
 __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift, int in_mode, int out_mode,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
@@ -559,8 +562,10 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     uint64_t *tbl = reinterpret_cast<uint64_t *>(s_keys) + w * 256;
     const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
     const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
-    int tile = (int)((int64_t)ntiles * xcd / kNumXCDs) + (int)blockIdx.x / kNumXCDs;
+    const int t0 = (int)((int64_t)ntiles * xcd / kNumXCDs);
+    int tile = t0 + (int)blockIdx.x / kNumXCDs;
     if (tile >= t1) return;  // block-uniform
+    auto phys = [&](int tl) { return REV ? t0 + t1 - 1 - tl : tl; };  // walk position -> tile
     // digit bases of the whole array (the same for every tile of the pass)
     const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);
 
@@ -573,11 +578,12 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             dst[e] = i < n ? in[i] : 0u;
         }
     };
-    load_tile(raw, tile);
+    load_tile(raw, phys(tile));
     for (; tile < t1; tile += per) {
-        const int64_t tile0 = (int64_t)tile * kRTile;
-        if (tile + per < t1) load_tile(nxt, tile + per);  // in flight under this tile's work
-        const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + tile] : 0u;
+        const int ptile = phys(tile);
+        const int64_t tile0 = (int64_t)ptile * kRTile;
+        if (tile + per < t1) load_tile(nxt, phys(tile + per));  // in flight under this tile's work
+        const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
         for (int i = t; i < kRWaves * 256; i += kRThreads) {
             (&s_cnt[0][0])[i] = 0;
             if (!VALU_MATCH) reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
@@ -653,23 +659,52 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 // 4-byte stores into whole lines
 constexpr int kCThreads = 256;
 constexpr int kCPer = kRTile / kCThreads;  // 32 keys per thread
+// VEC (16-B aligned input, whole tile in range): counting ignores order, so
+// each lane reads 16-B pieces (8 loads of 1 KiB per wave instead of 32 of
+// 256 B); the partial last tile keeps the 4-B form.
+template <bool VEC>
+__device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in, int64_t n, int shift, int mode,
+                                                int tile, uint32_t *hw) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int kWaveKeys = kRTile / (kCThreads / 64);  // 2048 contiguous keys per wave
+    if constexpr (VEC) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(in + (int64_t)tile * kRTile + w * kWaveKeys) + lane;
+        uint4 q[kCPer / 4];
+#pragma unroll
+        for (int e = 0; e < kCPer / 4; ++e) q[e] = src[e * 64];
+#pragma unroll
+        for (int e = 0; e < kCPer / 4; ++e) {
+            atomicAdd(&hw[(to_key(q[e].x, mode) >> shift) & 255u], 1u);
+            atomicAdd(&hw[(to_key(q[e].y, mode) >> shift) & 255u], 1u);
+            atomicAdd(&hw[(to_key(q[e].z, mode) >> shift) & 255u], 1u);
+            atomicAdd(&hw[(to_key(q[e].w, mode) >> shift) & 255u], 1u);
+        }
+    } else {
+        const int64_t base = (int64_t)tile * kRTile + w * kWaveKeys + lane;
+        uint32_t key[kCPer];
+#pragma unroll
+        for (int e = 0; e < kCPer; ++e) {
+            const int64_t i = base + e * 64;
+            key[e] = i < n ? in[i] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < kCPer; ++e)
+            if (base + e * 64 < n) atomicAdd(&hw[(to_key(key[e], mode) >> shift) & 255u], 1u);
+    }
+}
+
 __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *__restrict__ in, int64_t n, int shift,
                                                                 int mode, uint32_t *__restrict__ cnt, int ntiles) {
     __shared__ uint32_t h[kCThreads / 64][256];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int t = threadIdx.x, w = t >> 6;
     for (int i = t; i < (kCThreads / 64) * 256; i += kCThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t base = (int64_t)tile * kRTile + w * (kRTile / (kCThreads / 64)) + lane;
-    uint32_t key[kCPer];
-#pragma unroll
-    for (int e = 0; e < kCPer; ++e) {
-        const int64_t i = base + e * 64;
-        key[e] = i < n ? in[i] : 0u;
-    }
-#pragma unroll
-    for (int e = 0; e < kCPer; ++e)
-        if (base + e * 64 < n) atomicAdd(&h[w][(to_key(key[e], mode) >> shift) & 255u], 1u);
+    // block-uniform: whole tile in range and the input 16-B aligned
+    if (((int64_t)tile + 1) * kRTile <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0)
+        count_tile_keys<true>(in, n, shift, mode, tile, h[w]);
+    else
+        count_tile_keys<false>(in, n, shift, mode, tile, h[w]);
     __syncthreads();
     uint32_t c = 0;
 #pragma unroll
@@ -798,7 +833,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan
 // (one tile per block), 3 = reduce-then-scan with the persistent prefetching
 // scatter (ballot peer masks, 1024-thread scan), 4 = variant 3 as in round 2
-// (LDS-table peer masks, 256-thread scan; same-process A/B).
+// (LDS-table peer masks, 256-thread scan; same-process A/B), 5 = variant 3
+// walking each XCD's tiles from the end (MALL reuse probe).
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
@@ -844,6 +880,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 if (variant == 3)
                     hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
                                        dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
+                else if (variant == 5)
+                    hipLaunchKernelGGL((radix_scatter_kernel<true, true>), dim3((unsigned)blocks), dim3(kRThreads), 0,
+                                       s, src, dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
                 else
                     hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
                                        dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
@@ -1000,6 +1039,6 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // persistent scatter.
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 4) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 5) return MPX_ERR_ARG;
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }
