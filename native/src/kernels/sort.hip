@@ -19,8 +19,10 @@
 //         the tile in LDS in digit order and writes it out in runs per digit;
 //       - larger n, reduce-then-scan: per pass a count kernel (per-tile digit
 //         counts), a scan kernel (per-tile offsets and digit totals) and a
-//         persistent scatter kernel (2 blocks per CU walking XCD-local tiles,
-//         next tile prefetched while this one is ranked as above). It
+//         persistent scatter kernel (radix_scatter_lean_kernel: 2 blocks per
+//         CU walking XCD-local tiles, next tile prefetched while this one is
+//         ranked as above, buffer loads / stores, one counter add per
+//         distinct digit). It
 //         re-reads each tile once more but never waits on a look-back chain,
 //         whose cross-XCD round trips bound onesweep at large n.
 //     The key transform rides on the first pass's loads and the inverse on
@@ -653,6 +655,219 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
+// exclusive scan over the 64 lanes of one wave (no LDS barrier)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t to_key_t(uint32_t v) { return to_key(v, MODE); }
+template <int MODE>
+__device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, MODE); }
+
+// Lean persistent scatter (production, variants 6 / 7). The same schedule and
+// ranking as radix_scatter_kernel<false> (LDS peer-mask table), with the
+// per-key VALU cut — the round-3 counters put the scatter on its VALU pipe
+// (51.6M VALU per pass with the LDS table, 85.3M with ballots; 4 cycles each
+// per SIMD ~ 88 / 145 us of a 190 / 214 us pass):
+//   * key loads and output stores are buffer instructions: one lane offset
+//     register, the 16 slices in the instruction's immediate field, the tile
+//     in the scalar offset, and the array bound in the descriptor (pads and
+//     past-the-end stores are dropped by the hardware, no 64-bit address or
+//     compare per key);
+//   * the key transform is a template parameter (only the first pass reads
+//     raw int32 / float32, only the last writes them);
+//   * a slice's digit counter is read before its lowest lane adds the peer
+//     count (ds_add, no return): a wave's LDS operations execute in program
+//     order, so the read returns the count of the slices before it, and
+//     lanes_below(peer mask) the rank among its peers — no find-first-bit or
+//     bpermute;
+//   * two register sets ping-pong between the tile being ranked and the tile
+//     being prefetched (no per-tile register copies).
+// BPC blocks per CU (2: 4 waves per SIMD; 3 blocks = 6 waves per SIMD fit the
+// LDS but not the registers: 80 VGPRs spill 280 B per lane).
+template <int IN_MODE, int OUT_MODE, int BPC, bool ONEWAVE>
+__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC * 2))) void radix_scatter_lean_kernel(
+    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
+    const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
+    __shared__ uint32_t s_keys[kRTile];  // staging
+    // per-wave peer-mask tables, separate from the staging buffer: every
+    // slice clears the words it set, so the tables are zero again after each
+    // tile and are cleared only once, here
+    __shared__ uint32_t s_tbl[kRWaves * 512];
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kRWaves][256];  // 16-B rows for the one-wave phase
+    __shared__ __attribute__((aligned(16))) uint32_t s_gbase[256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_dbase[ONEWAVE ? 256 : 4];
+    __shared__ uint32_t s_wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int i = t; i < kRWaves * 512; i += kRThreads) s_tbl[i] = 0;
+    for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+    const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
+    const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
+    const int t0 = (int)((int64_t)ntiles * xcd / kNumXCDs);
+    int tile = t0 + (int)blockIdx.x / kNumXCDs;
+    if (tile >= t1) return;  // block-uniform
+    const uint32_t n32 = (uint32_t)n;           // n < 2^30
+    const int nbytes = (int)(n32 * 4u);          // the byte bound fits the descriptor's 32 bits
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(in), 0, nbytes,
+                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, nbytes, 0x00020000);
+    const int vlane = (w * kRWaveKeys + lane) * 4;
+    // peer-mask table: slot d = two words (lanes 0-31, 32-63) at tbl + 2d
+    uint32_t *tbl = s_tbl + w * 512;
+    uint32_t *const myword = tbl + (lane >> 5);
+    const uint32_t mybit = 1u << (lane & 31);
+    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);
+    if (ONEWAVE && t < 256) s_dbase[t] = dbase;  // read by wave 0 after the first ranking barrier
+
+    // whole tiles: one offset register (tile base + lane), slices in the
+    // immediate field; the partial last tile (block-uniform) loads and stores
+    // under explicit index checks, so correctness never rests on the
+    // descriptor's range check
+    auto load_tile = [&](uint32_t (&dst)[kRPer], int tl) {
+        const int64_t tile0 = (int64_t)tl * kRTile;
+        if (tile0 + kRTile <= n) {
+            const uint32_t voff = (uint32_t)tile0 * 4u + (uint32_t)vlane;  // < n * 4 < 2^32
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e)
+                dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * 256u), 0, 0);
+        } else {  // 32-bit indices (n < 2^30) keep the partial path's registers small
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e) {
+                const uint32_t i = i0 + e * 64u;
+                dst[e] = i < n32 ? __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(i * 4u), 0, 0) : 0u;
+            }
+        }
+    };
+    auto do_tile = [&](uint32_t (&key)[kRPer], int ptile) {
+        // s_cnt and the tables are zero here: cleared at kernel start and by
+        // the previous tile's write-out phase (behind its closing barrier)
+        uint32_t excl = 0;
+        uint4 excl4 = make_uint4(0, 0, 0, 0);
+        if constexpr (ONEWAVE) {
+            if (w == 0) {
+                const uint32_t *o = offs + (size_t)(4 * lane) * ntiles + ptile;
+                excl4 = make_uint4(o[0], o[ntiles], o[2 * (size_t)ntiles], o[3 * (size_t)ntiles]);
+            }
+        } else {
+            excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
+        }
+        const int64_t tile0 = (int64_t)ptile * kRTile;
+        const bool full = tile0 + kRTile <= n;  // block-uniform
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) key[e] = to_key_t<IN_MODE>(key[e]);
+        if (!full) {  // pads rank last (digit 255 in every pass) and are never stored
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e)
+                if (i0 + e * 64u >= n32) key[e] = 0xffffffffu;
+        }
+        uint32_t rank[kRPer];
+#pragma unroll
+        for (int g = 0; g < kRPer; g += 4) {  // 4 slices in flight: bounds the live LDS results
+            uint32_t lo[4], hi[4], before[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t d = (key[g + e] >> shift) & 255u;
+                atomicOr(myword + 2 * d, mybit);
+                lo[e] = tbl[2 * d];
+                hi[e] = tbl[2 * d + 1];
+                myword[2 * d] = 0;
+                before[e] = s_cnt[w][d];
+                // one add per distinct digit (its lowest lane): 64 lanes adding
+                // to one counter would serialise on skewed digits (the top byte
+                // of normally distributed floats takes a handful of values)
+                const uint64_t m = ((uint64_t)hi[e] << 32) | lo[e];
+                if (lanes_below(m) == 0) atomicAdd(&s_cnt[w][d], (uint32_t)__popcll(m));
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                rank[g + e] = before[e] + __builtin_amdgcn_mbcnt_hi(hi[e], __builtin_amdgcn_mbcnt_lo(lo[e], 0u));
+        }
+        lds_barrier();
+        if constexpr (ONEWAVE) {
+            // wave 0 alone turns the per-wave counts into staging offsets (lane
+            // l: digits 4l..4l+3, 16-byte LDS accesses, a wave-level scan):
+            // no block barrier inside this phase
+            if (w == 0) {
+                uint4 tot4 = make_uint4(0, 0, 0, 0);
+#pragma unroll 1
+                for (int ww = 0; ww < kRWaves; ++ww) {
+                    const uint4 c = reinterpret_cast<const uint4 *>(s_cnt[ww])[lane];
+                    tot4.x += c.x, tot4.y += c.y, tot4.z += c.z, tot4.w += c.w;
+                }
+                const uint32_t ds0 = wave_excl_scan(tot4.x + tot4.y + tot4.z + tot4.w);
+                uint4 run = make_uint4(ds0, ds0 + tot4.x, ds0 + tot4.x + tot4.y, ds0 + tot4.x + tot4.y + tot4.z);
+                const uint4 db = reinterpret_cast<const uint4 *>(s_dbase)[lane];
+                reinterpret_cast<uint4 *>(s_gbase)[lane] =
+                    make_uint4(excl4.x + db.x - run.x, excl4.y + db.y - run.y, excl4.z + db.z - run.z,
+                               excl4.w + db.w - run.w);
+#pragma unroll 1
+                for (int ww = 0; ww < kRWaves; ++ww) {
+                    uint4 *q = reinterpret_cast<uint4 *>(s_cnt[ww]) + lane;
+                    const uint4 c = *q;
+                    *q = run;
+                    run.x += c.x, run.y += c.y, run.z += c.z, run.w += c.w;
+                }
+            }
+        } else {
+            uint32_t cnt = 0, wexcl[kRWaves];
+            if (t < 256) {
+#pragma unroll
+                for (int ww = 0; ww < kRWaves; ++ww) {
+                    wexcl[ww] = cnt;
+                    cnt += s_cnt[ww][t];
+                }
+            }
+            const uint32_t dstart = scan256_excl_lds(cnt, s_wsum);
+            if (t < 256) {
+#pragma unroll
+                for (int ww = 0; ww < kRWaves; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
+                s_gbase[t] = excl + dbase - dstart;
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rank[e]] = key[e];
+        lds_barrier();
+        for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;  // for the next tile
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < kRTile / kRThreads; ++j) {
+                const int i = t + j * kRThreads;
+                const uint32_t k = s_keys[i];
+                __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout,
+                                                      (int)((s_gbase[(k >> shift) & 255u] + (uint32_t)i) * 4u), 0, 0);
+            }
+        } else {
+            for (int j = 0; j < kRTile / kRThreads; ++j) {
+                const int i = t + j * kRThreads;
+                const uint32_t k = s_keys[i];
+                const uint32_t pos = s_gbase[(k >> shift) & 255u] + (uint32_t)i;  // < n + kRTile < 2^31
+                if (pos < n32) __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)(pos * 4u), 0, 0);
+            }
+        }
+        lds_barrier();  // s_keys / s_cnt / s_gbase are rewritten by the next tile
+    };
+
+    uint32_t a[kRPer], b[kRPer];
+    load_tile(a, tile);
+    for (; tile < t1; tile += per) {
+        if (tile + per < t1) load_tile(b, tile + per);  // in flight under this tile's work
+        do_tile(a, tile);
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+    }
+}
+
 // reduce-then-scan, step 1: the tile's digit counts (per-wave LDS atomics,
 // order irrelevant), digit-major
 // (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
@@ -834,16 +1049,38 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // (one tile per block), 3 = reduce-then-scan with the persistent prefetching
 // scatter (ballot peer masks, 1024-thread scan), 4 = variant 3 as in round 2
 // (LDS-table peer masks, 256-thread scan; same-process A/B), 5 = variant 3
-// walking each XCD's tiles from the end (MALL reuse probe).
+// walking each XCD's tiles from the end (MALL reuse probe), 6 = the lean
+// persistent scatter (radix_scatter_lean_kernel), 7 = the same with the
+// one-wave offset phase.
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
 // reduce-then-scan re-reads each tile once more but never waits.
 constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
 
+// pass p of the lean scatter: the first pass reads raw int32 / float32, the
+// last writes them back, the middle passes move keys
+template <int BPC, bool OW>
+void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
+                 const uint32_t *tot, const uint32_t *offs, int ntiles) {
+    const dim3 g((unsigned)blocks), b(kRThreads);
+    const int sh = 8 * p;
+    const bool f = mode == kRawF32;
+    if (p == 0 && f)
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+    else if (p == 0)
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+    else if (p == 3 && f)
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+    else if (p == 3)
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+    else
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+}
+
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 3;
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 6;
     const int ntiles = (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
@@ -875,7 +1112,13 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 hipLaunchKernelGGL(radix_scan1024_kernel, dim3(256), dim3(kScanThreads), 0, s, r.status, ntiles,
                                    r.hist);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            if (variant >= 3) {
+            if (variant >= 6) {
+                const int blocks = std::min(kNumCUs * 2, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
+                if (variant == 6)
+                    launch_lean<2, false>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+                else
+                    launch_lean<2, true>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+            } else if (variant >= 3) {
                 const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
                 if (variant == 3)
                     hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
@@ -1035,10 +1278,10 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 }
 
 // Tuning entry (tools/experiments/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
-// (decoupled look-back), 2 = reduce-then-scan, 3 = reduce-then-scan with the
-// persistent scatter.
+// (decoupled look-back), 2 = reduce-then-scan, 3-7 = reduce-then-scan with a
+// persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 5) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 7) return MPX_ERR_ARG;
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }

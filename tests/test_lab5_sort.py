@@ -250,7 +250,7 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("kind", ["int", "float"])
 @pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
@@ -271,7 +271,7 @@ def test_gpu_radix_variants(gpu, variant, kind, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 3, 6])
 def test_gpu_sort_ws_status_ignores_stale_workspace(gpu, variant):
     """A recycled workspace full of 0xff bytes must not make mpx_sort_ws_status
     report a look-back give-up after a reduce-then-scan sort (which never

@@ -46,8 +46,12 @@ def variant_sort(x, variant):
 
 def main():
     dev = torch.device("cuda:0")
-    for dt in (torch.int32, torch.float32, torch.uint8):
-        for lg in (16, 20, 24, 26):
+    # LAB5_DTYPES=int32,float32 / LAB5_LOGN=26 / LAB5_VARIANTS=3,4 narrow a profiling run
+    dts = [getattr(torch, d) for d in os.environ.get("LAB5_DTYPES", "int32,float32,uint8").split(",")]
+    lgs = [int(v) for v in os.environ.get("LAB5_LOGN", "16,20,24,26").split(",")]
+    only = {int(v) for v in os.environ.get("LAB5_VARIANTS", "1,2,3,4,5,6,7").split(",")}
+    for dt in dts:
+        for lg in lgs:
             n = 1 << lg
             if dt == torch.uint8:
                 src = torch.randint(0, 256, (n,), dtype=dt, device=dev)
@@ -59,7 +63,10 @@ def main():
             variants = {}
             if dt != torch.uint8:
                 for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (3, "reduce_scan_persistent"),
-                              (4, "reduce_scan_persistent_r2"), (5, "reduce_scan_persistent_rev")):
+                              (4, "reduce_scan_persistent_r2"), (5, "reduce_scan_persistent_rev"),
+                              (6, "lean_scatter"), (7, "lean_scatter_onewave")):
+                    if v not in only:
+                        continue
                     try:
                         vms, vout = gpu_ms(lambda x, v=v: variant_sort(x, v), src)
                     except Exception as e:  # noqa: BLE001  (an older libmpx via MPX_LIB_PATH lacks the variant)
