@@ -655,16 +655,29 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     }
 }
 
-// exclusive scan over the 64 lanes of one wave (no LDS barrier)
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    return x - v;
+// Inclusive scan over the 64 lanes of a wave on DPP (row shifts within
+// 16-lane rows, then the row-15 / row-31 broadcasts): six VALU ops, no LDS
+// round trip (the __shfl_up form is six dependent ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// scan256_excl_lds on DPP, without the trailing barrier: the caller orders
+// the next write of s_wsum behind a later block barrier
+__device__ __forceinline__ uint32_t scan256_excl_dpp(uint32_t v, uint32_t *s_wsum) {
+    const int t = threadIdx.x, lane = t & 63;
+    const uint32_t x = wave_incl_scan_dpp(v);
+    if (t < 256 && lane == 63) s_wsum[t >> 6] = x;
+    lds_barrier();
+    uint32_t add = 0;
+    for (int w = 0; w < (t >> 6) && w < 4; ++w) add += s_wsum[w];
+    return x - v + add;
 }
 
 template <int MODE>
@@ -672,7 +685,7 @@ __device__ __forceinline__ uint32_t to_key_t(uint32_t v) { return to_key(v, MODE
 template <int MODE>
 __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, MODE); }
 
-// Lean persistent scatter (production, variants 6 / 7). The same schedule and
+// Lean persistent scatter (variants 6 / 7). The same schedule and
 // ranking as radix_scatter_kernel<false> (LDS peer-mask table), with the
 // per-key VALU cut — the round-3 counters put the scatter on its VALU pipe
 // (51.6M VALU per pass with the LDS table, 85.3M with ballots; 4 cycles each
@@ -691,10 +704,16 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 //     bpermute;
 //   * two register sets ping-pong between the tile being ranked and the tile
 //     being prefetched (no per-tile register copies).
-// BPC blocks per CU (2: 4 waves per SIMD; 3 blocks = 6 waves per SIMD fit the
-// LDS but not the registers: 80 VGPRs spill 280 B per lane).
-template <int IN_MODE, int OUT_MODE, int BPC, bool ONEWAVE>
-__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC * 2))) void radix_scatter_lean_kernel(
+//   * FEWB (variant 7): four block barriers per tile instead of six — each
+//     wave zeroes its own counter row after its own staging reads (no other
+//     wave writes that row before the next tile's first barrier), the 256-digit
+//     scan runs on DPP row shifts / broadcasts with one barrier for the four
+//     wave sums, and nothing needs the closing barrier: the next tile's first
+//     barrier orders its staging / scan writes after this tile's write-out.
+// 2 blocks per CU (4 waves per SIMD; 3 blocks = 6 waves per SIMD fit the LDS
+// but not the registers: 80 VGPRs spill 280 B per lane).
+template <int IN_MODE, int OUT_MODE, bool FEWB>
+__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
     __shared__ uint32_t s_keys[kRTile];  // staging
@@ -702,9 +721,8 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC *
     // slice clears the words it set, so the tables are zero again after each
     // tile and are cleared only once, here
     __shared__ uint32_t s_tbl[kRWaves * 512];
-    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kRWaves][256];  // 16-B rows for the one-wave phase
-    __shared__ __attribute__((aligned(16))) uint32_t s_gbase[256];
-    __shared__ __attribute__((aligned(16))) uint32_t s_dbase[ONEWAVE ? 256 : 4];
+    __shared__ uint32_t s_cnt[kRWaves][256];
+    __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     for (int i = t; i < kRWaves * 512; i += kRThreads) s_tbl[i] = 0;
@@ -720,12 +738,15 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC *
                                                                          0x00020000);
     const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, nbytes, 0x00020000);
     const int vlane = (w * kRWaveKeys + lane) * 4;
-    // peer-mask table: slot d = two words (lanes 0-31, 32-63) at tbl + 2d
+    // peer-mask table: slot d = two words (lanes 0-31, 32-63) at tbl + 2d.
+    // (A split layout — the lanes 0-31 words at tbl[d], the 32-63 words at
+    // tbl[256 + d], so a half-wave's OR / clear spreads over 32 banks instead
+    // of 16 — measured neutral: 37.6M vs 38.4M conflict cycles per pass, the
+    // same time; profiles/lab5_sort.md.)
     uint32_t *tbl = s_tbl + w * 512;
     uint32_t *const myword = tbl + (lane >> 5);
     const uint32_t mybit = 1u << (lane & 31);
-    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);
-    if (ONEWAVE && t < 256) s_dbase[t] = dbase;  // read by wave 0 after the first ranking barrier
+    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);  // + the barrier after the zeroing
 
     // whole tiles: one offset register (tile base + lane), slices in the
     // immediate field; the partial last tile (block-uniform) loads and stores
@@ -748,18 +769,8 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC *
         }
     };
     auto do_tile = [&](uint32_t (&key)[kRPer], int ptile) {
-        // s_cnt and the tables are zero here: cleared at kernel start and by
-        // the previous tile's write-out phase (behind its closing barrier)
-        uint32_t excl = 0;
-        uint4 excl4 = make_uint4(0, 0, 0, 0);
-        if constexpr (ONEWAVE) {
-            if (w == 0) {
-                const uint32_t *o = offs + (size_t)(4 * lane) * ntiles + ptile;
-                excl4 = make_uint4(o[0], o[ntiles], o[2 * (size_t)ntiles], o[3 * (size_t)ntiles]);
-            }
-        } else {
-            excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
-        }
+        // s_cnt and the tables are zero here (kernel start / previous write-out)
+        const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
         const int64_t tile0 = (int64_t)ptile * kRTile;
         const bool full = tile0 + kRTile <= n;  // block-uniform
 #pragma unroll
@@ -793,52 +804,32 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC *
                 rank[g + e] = before[e] + __builtin_amdgcn_mbcnt_hi(hi[e], __builtin_amdgcn_mbcnt_lo(lo[e], 0u));
         }
         lds_barrier();
-        if constexpr (ONEWAVE) {
-            // wave 0 alone turns the per-wave counts into staging offsets (lane
-            // l: digits 4l..4l+3, 16-byte LDS accesses, a wave-level scan):
-            // no block barrier inside this phase
-            if (w == 0) {
-                uint4 tot4 = make_uint4(0, 0, 0, 0);
-#pragma unroll 1
-                for (int ww = 0; ww < kRWaves; ++ww) {
-                    const uint4 c = reinterpret_cast<const uint4 *>(s_cnt[ww])[lane];
-                    tot4.x += c.x, tot4.y += c.y, tot4.z += c.z, tot4.w += c.w;
-                }
-                const uint32_t ds0 = wave_excl_scan(tot4.x + tot4.y + tot4.z + tot4.w);
-                uint4 run = make_uint4(ds0, ds0 + tot4.x, ds0 + tot4.x + tot4.y, ds0 + tot4.x + tot4.y + tot4.z);
-                const uint4 db = reinterpret_cast<const uint4 *>(s_dbase)[lane];
-                reinterpret_cast<uint4 *>(s_gbase)[lane] =
-                    make_uint4(excl4.x + db.x - run.x, excl4.y + db.y - run.y, excl4.z + db.z - run.z,
-                               excl4.w + db.w - run.w);
-#pragma unroll 1
-                for (int ww = 0; ww < kRWaves; ++ww) {
-                    uint4 *q = reinterpret_cast<uint4 *>(s_cnt[ww]) + lane;
-                    const uint4 c = *q;
-                    *q = run;
-                    run.x += c.x, run.y += c.y, run.z += c.z, run.w += c.w;
-                }
-            }
-        } else {
-            uint32_t cnt = 0, wexcl[kRWaves];
-            if (t < 256) {
+        uint32_t cnt = 0, wexcl[kRWaves];
+        if (t < 256) {
 #pragma unroll
-                for (int ww = 0; ww < kRWaves; ++ww) {
-                    wexcl[ww] = cnt;
-                    cnt += s_cnt[ww][t];
-                }
+            for (int ww = 0; ww < kRWaves; ++ww) {
+                wexcl[ww] = cnt;
+                cnt += s_cnt[ww][t];
             }
-            const uint32_t dstart = scan256_excl_lds(cnt, s_wsum);
-            if (t < 256) {
+        }
+        const uint32_t dstart = FEWB ? scan256_excl_dpp(cnt, s_wsum) : scan256_excl_lds(cnt, s_wsum);
+        if (t < 256) {
 #pragma unroll
-                for (int ww = 0; ww < kRWaves; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
-                s_gbase[t] = excl + dbase - dstart;
-            }
+            for (int ww = 0; ww < kRWaves; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
+            s_gbase[t] = excl + dbase - dstart;
         }
         lds_barrier();
 #pragma unroll
         for (int e = 0; e < kRPer; ++e) s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rank[e]] = key[e];
-        lds_barrier();
-        for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;  // for the next tile
+        if constexpr (FEWB) {
+            lds_barrier();
+            // this wave's staging reads of its own row are done (program order)
+#pragma unroll
+            for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
+        } else {
+            lds_barrier();
+            for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;  // for the next tile
+        }
         if (full) {
 #pragma unroll
             for (int j = 0; j < kRTile / kRThreads; ++j) {
@@ -855,7 +846,7 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(BPC *
                 if (pos < n32) __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)(pos * 4u), 0, 0);
             }
         }
-        lds_barrier();  // s_keys / s_cnt / s_gbase are rewritten by the next tile
+        if constexpr (!FEWB) lds_barrier();  // s_keys / s_cnt / s_gbase are rewritten by the next tile
     };
 
     uint32_t a[kRPer], b[kRPer];
@@ -1050,8 +1041,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // scatter (ballot peer masks, 1024-thread scan), 4 = variant 3 as in round 2
 // (LDS-table peer masks, 256-thread scan; same-process A/B), 5 = variant 3
 // walking each XCD's tiles from the end (MALL reuse probe), 6 = the lean
-// persistent scatter (radix_scatter_lean_kernel), 7 = the same with the
-// one-wave offset phase.
+// persistent scatter (radix_scatter_lean_kernel), 7 = the same with four
+// barriers per tile (FEWB; production above kOnesweepMaxN).
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
@@ -1060,27 +1051,27 @@ constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (prof
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
-template <int BPC, bool OW>
+template <bool FEWB>
 void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
                  const uint32_t *tot, const uint32_t *offs, int ntiles) {
     const dim3 g((unsigned)blocks), b(kRThreads);
     const int sh = 8 * p;
     const bool f = mode == kRawF32;
     if (p == 0 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 0)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, BPC, OW>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
 }
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 6;
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 7;
     const int ntiles = (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
@@ -1115,9 +1106,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             if (variant >= 6) {
                 const int blocks = std::min(kNumCUs * 2, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
                 if (variant == 6)
-                    launch_lean<2, false>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+                    launch_lean<false>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
                 else
-                    launch_lean<2, true>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+                    launch_lean<true>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
             } else if (variant >= 3) {
                 const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
                 if (variant == 3)

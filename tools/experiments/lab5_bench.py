@@ -64,7 +64,7 @@ def main():
             if dt != torch.uint8:
                 for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (3, "reduce_scan_persistent"),
                               (4, "reduce_scan_persistent_r2"), (5, "reduce_scan_persistent_rev"),
-                              (6, "lean_scatter"), (7, "lean_scatter_onewave")):
+                              (6, "lean_scatter"), (7, "lean_scatter_fewb")):
                     if v not in only:
                         continue
                     try:
