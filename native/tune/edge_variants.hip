@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void linear_copy_kernel(const u32x4_t *__restr
 // keeps every halo load live. F bit 0: per-row LDS exchange with the
 // neighbouring thread + barrier (the horizontal pass's cost); bit 1: odd
 // bands walk upwards; bit 2: no XCD remap; bit 3: non-temporal stores;
-// bit 4: 512-thread workgroups over 2048 columns.
+// bit 4: 512-thread workgroups over 2048 columns; bit 5: no halo loads.
 template <int F>
 __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
                                                          int w4, int h, int R, int nchunks) {
@@ -96,7 +96,12 @@ __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restri
         const int y = up ? ye + 1 - j : ys - 2 + j;
         return min(max(y, 0), h - 1);
     };
-    auto ld = [&](int j) { return in[(int64_t)row_of(min(j, R + 3)) * w4 + c]; };
+    // bit 5: no halo loads (the walk's 2 + 2 halo rows read as zero): the
+    // traffic of a band whose halo rows come from its neighbours through LDS
+    auto ld = [&](int j) {
+        if ((F & 32) && (j < 2 || j > R + 1)) return u32x4_t{0u, 0u, 0u, 0u};
+        return in[(int64_t)row_of(min(j, R + 3)) * w4 + c];
+    };
     u32x4_t r[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = ld(j);
@@ -138,7 +143,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
     }
     MPX_CHECK_ARG(seg > 0, "seg must be > 0");
     if (v == 8) {  // row bands: seg = rows per band (multiple of 8), d = flag bits
-        MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 32, "band probe: w % 4096 == 0, seg % 4 == 0");
+        MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 64, "band probe: w % 4096 == 0, seg % 4 == 0");
         const int tpb = (d & 16) ? 512 : 1024;
         const int nchunks = w / (4 * tpb), nb = (h + seg - 1) / seg;
         const dim3 g((unsigned)(nb * nchunks)), b(tpb);
@@ -149,7 +154,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
 #define MPX_BAND(F) \
     case F: hipLaunchKernelGGL(band_copy_kernel<F>, g, b, 0, sb, vi, vo, w / 4, h, seg, nchunks); break;
             MPX_BAND(0) MPX_BAND(1) MPX_BAND(2) MPX_BAND(3) MPX_BAND(4) MPX_BAND(10) MPX_BAND(11) MPX_BAND(18)
-            MPX_BAND(19) MPX_BAND(26)
+            MPX_BAND(19) MPX_BAND(26) MPX_BAND(34) MPX_BAND(42)
             default: set_error("unsupported band flags %d", d); return MPX_ERR_ARG;
 #undef MPX_BAND
         }

@@ -141,7 +141,8 @@ def main():
     for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
         variants[f"copy/linear-{nm}"] = (
             (lambda d=d: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
-    for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26)] + [(16, 0), (16, 4)]:
+    for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26)] + [(16, 0), (16, 4), (16, 34),
+                                                                                        (16, 42), (32, 10), (32, 42)]:
         if True:  # row bands, 16-B vector per thread (ref None: XOR of rows, no reference)
             variants[f"copy/band-seg{seg}-f{fl}"] = (
                 (lambda fl=fl, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
