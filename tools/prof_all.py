@@ -35,10 +35,11 @@ def main():
         del a, b, c
     if "lab3" in which:
         img = torch.randint(0, 256, (8192, 8192, 4), dtype=torch.uint8, device=dev)
-        mu, inv = ops.class_stats(img.cpu(), class_points_for(8192, 8192, 16, 64, seed=16))
-        for path in ("direct", "fast", "mfma", "mfma64"):
-            for _ in range(REPS):
-                ops.classify_(img, mu, inv, path=path)
+        for nc, paths in ((16, ("direct", "fast", "mfma8")), (32, ("fast", "mfma8"))):  # AUTO: mfma8 from 24
+            mu, inv = ops.class_stats(img.cpu(), class_points_for(8192, 8192, nc, 64, seed=nc))
+            for path in paths:
+                for _ in range(REPS):
+                    ops.classify_(img, mu, inv, path=path)
         del img
     if "jacobi" in which:
         n = 16384
