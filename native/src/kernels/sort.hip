@@ -702,31 +702,34 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 //     order, so the read returns the count of the slices before it, and
 //     lanes_below(peer mask) the rank among its peers — no find-first-bit or
 //     bpermute;
-//   * two register sets ping-pong between the tile being ranked and the tile
-//     being prefetched (no per-tile register copies).
+//   * the next tile's keys load into a second register set while this tile is
+//     ranked, staged and written.
 //   * FEWB (variant 7): four block barriers per tile instead of six — each
 //     wave zeroes its own counter row after its own staging reads (no other
 //     wave writes that row before the next tile's first barrier), the 256-digit
 //     scan runs on DPP row shifts / broadcasts with one barrier for the four
 //     wave sums, and nothing needs the closing barrier: the next tile's first
 //     barrier orders its staging / scan writes after this tile's write-out.
-// 2 blocks per CU (4 waves per SIMD; 3 blocks = 6 waves per SIMD fit the LDS
-// but not the registers: 80 VGPRs spill 280 B per lane).
-template <int IN_MODE, int OUT_MODE, bool FEWB>
-__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_lean_kernel(
+// TPB = 512: 8192-key tiles, 2 blocks per CU (4 waves per SIMD; 3 blocks = 6
+// waves per SIMD fit the LDS but not the registers: 80 VGPRs spill 280 B per
+// lane). TPB = 256 (variant 8): 4096-key tiles, 4 blocks per CU — twice the
+// independent barrier domains per CU for the same waves.
+template <int IN_MODE, int OUT_MODE, bool FEWB, int TPB = kRThreads>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
-    __shared__ uint32_t s_keys[kRTile];  // staging
+    constexpr int NW = TPB / 64, TILE = TPB * kRPer;  // kRWaveKeys keys per wave either way
+    __shared__ uint32_t s_keys[TILE];  // staging
     // per-wave peer-mask tables, separate from the staging buffer: every
     // slice clears the words it set, so the tables are zero again after each
     // tile and are cleared only once, here
-    __shared__ uint32_t s_tbl[kRWaves * 512];
-    __shared__ uint32_t s_cnt[kRWaves][256];
+    __shared__ uint32_t s_tbl[NW * 512];
+    __shared__ uint32_t s_cnt[NW][256];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    for (int i = t; i < kRWaves * 512; i += kRThreads) s_tbl[i] = 0;
-    for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;
+    for (int i = t; i < NW * 512; i += TPB) s_tbl[i] = 0;
+    for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;
     const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
     const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
     const int t0 = (int)((int64_t)ntiles * xcd / kNumXCDs);
@@ -753,8 +756,8 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // under explicit index checks, so correctness never rests on the
     // descriptor's range check
     auto load_tile = [&](uint32_t (&dst)[kRPer], int tl) {
-        const int64_t tile0 = (int64_t)tl * kRTile;
-        if (tile0 + kRTile <= n) {
+        const int64_t tile0 = (int64_t)tl * TILE;
+        if (tile0 + TILE <= n) {
             const uint32_t voff = (uint32_t)tile0 * 4u + (uint32_t)vlane;  // < n * 4 < 2^32
 #pragma unroll
             for (int e = 0; e < kRPer; ++e)
@@ -771,8 +774,8 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     auto do_tile = [&](uint32_t (&key)[kRPer], int ptile) {
         // s_cnt and the tables are zero here (kernel start / previous write-out)
         const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
-        const int64_t tile0 = (int64_t)ptile * kRTile;
-        const bool full = tile0 + kRTile <= n;  // block-uniform
+        const int64_t tile0 = (int64_t)ptile * TILE;
+        const bool full = tile0 + TILE <= n;  // block-uniform
 #pragma unroll
         for (int e = 0; e < kRPer; ++e) key[e] = to_key_t<IN_MODE>(key[e]);
         if (!full) {  // pads rank last (digit 255 in every pass) and are never stored
@@ -804,10 +807,10 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                 rank[g + e] = before[e] + __builtin_amdgcn_mbcnt_hi(hi[e], __builtin_amdgcn_mbcnt_lo(lo[e], 0u));
         }
         lds_barrier();
-        uint32_t cnt = 0, wexcl[kRWaves];
+        uint32_t cnt = 0, wexcl[NW];
         if (t < 256) {
 #pragma unroll
-            for (int ww = 0; ww < kRWaves; ++ww) {
+            for (int ww = 0; ww < NW; ++ww) {
                 wexcl[ww] = cnt;
                 cnt += s_cnt[ww][t];
             }
@@ -815,7 +818,7 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t dstart = FEWB ? scan256_excl_dpp(cnt, s_wsum) : scan256_excl_lds(cnt, s_wsum);
         if (t < 256) {
 #pragma unroll
-            for (int ww = 0; ww < kRWaves; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
+            for (int ww = 0; ww < NW; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
             s_gbase[t] = excl + dbase - dstart;
         }
         lds_barrier();
@@ -828,21 +831,21 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
         } else {
             lds_barrier();
-            for (int i = t; i < kRWaves * 256; i += kRThreads) (&s_cnt[0][0])[i] = 0;  // for the next tile
+            for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;  // for the next tile
         }
         if (full) {
 #pragma unroll
-            for (int j = 0; j < kRTile / kRThreads; ++j) {
-                const int i = t + j * kRThreads;
+            for (int j = 0; j < TILE / TPB; ++j) {
+                const int i = t + j * TPB;
                 const uint32_t k = s_keys[i];
                 __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout,
                                                       (int)((s_gbase[(k >> shift) & 255u] + (uint32_t)i) * 4u), 0, 0);
             }
         } else {
-            for (int j = 0; j < kRTile / kRThreads; ++j) {
-                const int i = t + j * kRThreads;
+            for (int j = 0; j < TILE / TPB; ++j) {
+                const int i = t + j * TPB;
                 const uint32_t k = s_keys[i];
-                const uint32_t pos = s_gbase[(k >> shift) & 255u] + (uint32_t)i;  // < n + kRTile < 2^31
+                const uint32_t pos = s_gbase[(k >> shift) & 255u] + (uint32_t)i;  // < n + TILE < 2^31
                 if (pos < n32) __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)(pos * 4u), 0, 0);
             }
         }
@@ -864,17 +867,17 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 // (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
 // 4-byte stores into whole lines
 constexpr int kCThreads = 256;
-constexpr int kCPer = kRTile / kCThreads;  // 32 keys per thread
 // VEC (16-B aligned input, whole tile in range): counting ignores order, so
 // each lane reads 16-B pieces (8 loads of 1 KiB per wave instead of 32 of
 // 256 B); the partial last tile keeps the 4-B form.
-template <bool VEC>
+template <bool VEC, int TILE>
 __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in, int64_t n, int shift, int mode,
                                                 int tile, uint32_t *hw) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    constexpr int kWaveKeys = kRTile / (kCThreads / 64);  // 2048 contiguous keys per wave
+    constexpr int kCPer = TILE / kCThreads;              // 32 keys per thread (16 for 4096-key tiles)
+    constexpr int kWaveKeys = TILE / (kCThreads / 64);  // 2048 contiguous keys per wave
     if constexpr (VEC) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(in + (int64_t)tile * kRTile + w * kWaveKeys) + lane;
+        const uint4 *src = reinterpret_cast<const uint4 *>(in + (int64_t)tile * TILE + w * kWaveKeys) + lane;
         uint4 q[kCPer / 4];
 #pragma unroll
         for (int e = 0; e < kCPer / 4; ++e) q[e] = src[e * 64];
@@ -886,7 +889,7 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
             atomicAdd(&hw[(to_key(q[e].w, mode) >> shift) & 255u], 1u);
         }
     } else {
-        const int64_t base = (int64_t)tile * kRTile + w * kWaveKeys + lane;
+        const int64_t base = (int64_t)tile * TILE + w * kWaveKeys + lane;
         uint32_t key[kCPer];
 #pragma unroll
         for (int e = 0; e < kCPer; ++e) {
@@ -899,6 +902,7 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
     }
 }
 
+template <int TILE = kRTile>
 __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *__restrict__ in, int64_t n, int shift,
                                                                 int mode, uint32_t *__restrict__ cnt, int ntiles) {
     __shared__ uint32_t h[kCThreads / 64][256];
@@ -907,10 +911,10 @@ __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *
     __syncthreads();
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     // block-uniform: whole tile in range and the input 16-B aligned
-    if (((int64_t)tile + 1) * kRTile <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0)
-        count_tile_keys<true>(in, n, shift, mode, tile, h[w]);
+    if (((int64_t)tile + 1) * TILE <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0)
+        count_tile_keys<true, TILE>(in, n, shift, mode, tile, h[w]);
     else
-        count_tile_keys<false>(in, n, shift, mode, tile, h[w]);
+        count_tile_keys<false, TILE>(in, n, shift, mode, tile, h[w]);
     __syncthreads();
     uint32_t c = 0;
 #pragma unroll
@@ -1016,10 +1020,11 @@ struct RadixWs {
 };
 
 int64_t radix_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
+constexpr int kRTileSmall = kRTile / 2;  // the 256-thread lean scatter's tile (variant 8)
 
-size_t radix_ws_bytes(int64_t n) {
+size_t radix_ws_bytes(int64_t n) {  // status sized for the smaller tile (twice the tiles)
     const size_t keys = ((size_t)n * 4 + 255) / 256 * 256;
-    return keys + (4 * 256 + 64) * 4 + (size_t)4 * radix_tiles(n) * 256 * 4;
+    return keys + (4 * 256 + 64) * 4 + (size_t)4 * ((n + kRTileSmall - 1) / kRTileSmall) * 256 * 4;
 }
 
 RadixWs radix_layout(void *ws, int64_t n) {
@@ -1042,37 +1047,44 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // (LDS-table peer masks, 256-thread scan; same-process A/B), 5 = variant 3
 // walking each XCD's tiles from the end (MALL reuse probe), 6 = the lean
 // persistent scatter (radix_scatter_lean_kernel), 7 = the same with four
-// barriers per tile (FEWB; production above kOnesweepMaxN).
+// barriers per tile (FEWB; production above kOnesweepMaxN), 8 = 7 on
+// 4096-key tiles (256-thread blocks, 4 per CU).
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
 // reduce-then-scan re-reads each tile once more but never waits.
 constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
+constexpr int64_t kTile4kMaxN = (int64_t)1 << 24;    // variant 8 up to here (measured sizes only)
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
-template <bool FEWB>
+template <bool FEWB, int TPB = kRThreads>
 void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
                  const uint32_t *tot, const uint32_t *offs, int ntiles) {
-    const dim3 g((unsigned)blocks), b(kRThreads);
+    const dim3 g((unsigned)blocks), b(TPB);
     const int sh = 8 * p;
     const bool f = mode == kRawF32;
     if (p == 0 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 0)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, FEWB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
 }
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : 7;
-    const int ntiles = (int)r.tiles;
+    // 4096-key tiles win up to 2^24 keys (2^20: 0.070 vs 0.075 ms, 2^24: 0.221
+    // vs 0.229) and lose at 2^26 (0.987 vs 0.828; not yet explained — a
+    // candidate: with 16 tiles per block the 64-B digit runs of neighbouring
+    // tiles stop meeting in L2; profiles/lab5_sort.md)
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 8 : 7;
+    // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
+    const int ntiles = variant == 8 ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
         hipLaunchKernelGGL(radix_hist_kernel,
@@ -1094,8 +1106,12 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                r.ctr + p, r.err, ntiles);
         } else {
             // offsets in status[0 .. 256 * ntiles), digit totals in hist[0 .. 256)
-            hipLaunchKernelGGL(radix_count_kernel, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src, n, 8 * p,
-                               in_mode, r.status, ntiles);
+            if (variant == 8)
+                hipLaunchKernelGGL(radix_count_kernel<kRTileSmall>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
+                                   n, 8 * p, in_mode, r.status, ntiles);
+            else
+                hipLaunchKernelGGL(radix_count_kernel<kRTile>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src, n,
+                                   8 * p, in_mode, r.status, ntiles);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             if (variant == 4)
                 hipLaunchKernelGGL(radix_scan_kernel, dim3(256), dim3(256), 0, s, r.status, ntiles, r.hist);
@@ -1104,11 +1120,14 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                    r.hist);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             if (variant >= 6) {
-                const int blocks = std::min(kNumCUs * 2, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
+                const int rounded = (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs;
                 if (variant == 6)
-                    launch_lean<false>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+                    launch_lean<false>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
+                else if (variant == 7)
+                    launch_lean<true>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
                 else
-                    launch_lean<true>(p, mode, blocks, s, src, dst, n, r.hist, r.status, ntiles);
+                    launch_lean<true, kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
+                                                      r.status, ntiles);
             } else if (variant >= 3) {
                 const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
                 if (variant == 3)
@@ -1273,6 +1292,6 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 7) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 8) return MPX_ERR_ARG;
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }

@@ -250,7 +250,7 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("kind", ["int", "float"])
 @pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
