@@ -867,13 +867,12 @@ bool build_i8(int nc, const double *mu, const double *inv, I8Params &ip) {
 }
 }  // namespace
 
-// AUTO: MFMA8 from kAutoMfma8MinClasses classes, else FAST32; DIRECT when no
-// decision bound can be proven for these statistics. Measured on MI355X
-// (profiles/lab3_classify.md): the f32 MFMA and
-// the f32 VALU share one datapath on gfx950 — SQ_VALU_MFMA_BUSY_CYCLES and the
-// VALU issue cycles ADD UP to the kernel time — so the distance GEMM cannot hide
-// the ranking work behind the matrix core, and FAST32 is as fast or faster at
-// every class count (nc = 4: 132 vs 546 us, nc = 32: 677 vs 689 us at 8192^2).
+// Paths other than MFMA8 under AUTO: FAST32, or DIRECT when no decision bound
+// can be proven for these statistics. The fp32 MFMA form (MFMA) never wins:
+// the f32 MFMA and the f32 VALU share one datapath on gfx950 —
+// SQ_VALU_MFMA_BUSY_CYCLES and the VALU issue cycles ADD UP to the kernel time
+// (nc = 4: 132 vs 546 us, nc = 32: 677 vs 689 us at 8192^2;
+// profiles/lab3_classify.md).
 int classify_choose(int nc, int path, bool fast_ok) {
     (void)nc;
     if (path == MPX_CLS_DIRECT || !fast_ok) return MPX_CLS_DIRECT;
@@ -881,17 +880,23 @@ int classify_choose(int nc, int path, bool fast_ok) {
     return path;
 }
 
-// AUTO above this class count runs MFMA8 (its statistics permitting): same
-// box, 8192^2, µs (profiles/lab3_classify.md): nc 4 fast 130 / mfma8 256,
-// nc 16 360 / 352 (parity), nc 32 633 / 494.
+// AUTO runs MFMA8 (its statistics permitting) where it measured faster than
+// FAST32: exactly 16 classes (one full 16-class accumulator set) and from 24
+// up. Same box, 8192^2, two runs each, µs (profiles/lab3_classify.md):
+//   nc      8        12       14       16       18       20       24
+//   fast  208-211  279-285  323-330  356-361  394-398  416-418  492-506
+//   mfma8 260-282  330-341  340-344  342-342  461-468  466-480  467-483
+// MFMA8's cost steps with its accumulator sets (classes 1-16 / 17-32), FAST32's
+// grows linearly; nc 32: 634 / 498.
 constexpr int kAutoMfma8MinClasses = 24;
+inline bool auto_mfma8(int nc) { return nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.
 int classify_resolve(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
                      Fast64Params &fp64, I8Params &ip8) {
     if (path == MPX_CLS_DIRECT || !aligned) return MPX_CLS_DIRECT;
-    if (path == MPX_CLS_AUTO && nc >= kAutoMfma8MinClasses && build_i8(nc, mu, inv, ip8)) return MPX_CLS_MFMA8;
+    if (path == MPX_CLS_AUTO && auto_mfma8(nc) && build_i8(nc, mu, inv, ip8)) return MPX_CLS_MFMA8;
     const bool ok = path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
                     : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
                                             : build_fast(nc, mu, inv, fp);

@@ -146,7 +146,12 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
     mu20, inv20 = stats(20)
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
-    # from 24 classes AUTO runs the exact int8-MFMA distance GEMM (margin in key units)
+    mu14, inv14 = stats(14)
+    assert ops.classify_plan(mu14, inv14, "auto")[0] == "fast"
+    # at exactly 16 and from 24 classes AUTO runs the exact int8-MFMA distance
+    # GEMM (measured faster there; margin in key units)
+    mu16, inv16 = stats(16)
+    assert ops.classify_plan(mu16, inv16, "auto")[0] == "mfma8"
     mu28, inv28 = stats(28)
     path28, margin28 = ops.classify_plan(mu28, inv28, "auto")
     assert path28 == "mfma8" and margin28 >= 1

@@ -90,12 +90,15 @@ def bench_lab2(dev, size=4096):
 def bench_lab3(dev, size=8192):
     img = torch.randint(0, 256, (size, size, 4), dtype=torch.uint8, device=dev)
     host = img.cpu()
-    for nc in (4, 16, 32):
+    # LAB3_NCS / LAB3_PATHS narrow a sweep (e.g. the AUTO threshold: LAB3_NCS=8,12,16,20,24 LAB3_PATHS=fast,mfma8)
+    ncs = [int(v) for v in os.environ.get("LAB3_NCS", "4,16,32").split(",")]
+    paths = os.environ.get("LAB3_PATHS", "direct,fast,mfma,mfma64,mfma8,auto").split(",")
+    for nc in ncs:
         pts = class_points_for(size, size, nc, 64, seed=nc)
         mu, inv = ops.class_stats(host, pts)
         ref = host.clone()
         cpu = cpu_time_ms(lambda: ops.classify_(ref, mu, inv))
-        for path in ("direct", "fast", "mfma", "mfma64", "mfma8", "auto"):
+        for path in paths:
             work = img.clone()
             amb = torch.zeros(1, dtype=torch.int32, device=dev)
             ops.classify_(work, mu, inv, path=path, ambiguous=amb)
