@@ -289,8 +289,8 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
 // (both half-waves load the same bytes), and group m = 0..3 uses pixel
 // 4 (l & 31) + m as column l & 31, so every result lands in the lane that
 // owns the pixel's uint4. The two half-waves' top-2 keys are merged with
-// v_permlane32_swap. NREG = accumulator registers with real classes (8 for
-// nc <= 16, 16 for nc <= 32).
+// v_permlane32_swap. NREG = accumulator registers with real classes (4 for
+// nc <= 8, 8 for nc <= 16, 12 for nc <= 24, 16 for nc <= 32).
 // ---------------------------------------------------------------------------
 template <int NREG>
 __global__ __launch_bounds__(256) void classify_mfma32_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
@@ -881,14 +881,15 @@ int classify_choose(int nc, int path, bool fast_ok) {
 }
 
 // AUTO runs MFMA8 (its statistics permitting) where it measured faster than
-// FAST32: exactly 16 classes (one full 16-class accumulator set) and from 24
+// FAST32: exactly 16 classes (accumulator registers 0-7 all real) and from 22
 // up. Same box, 8192^2, two runs each, µs (profiles/lab3_classify.md):
-//   nc      8        12       14       16       18       20       24
-//   fast  208-211  279-285  323-330  356-361  394-398  416-418  492-506
-//   mfma8 260-282  330-341  340-344  342-342  461-468  466-480  467-483
-// MFMA8's cost steps with its accumulator sets (classes 1-16 / 17-32), FAST32's
-// grows linearly; nc 32: 634 / 498.
-constexpr int kAutoMfma8MinClasses = 24;
+//   nc      8        12       14       16       17       18       20       22       24
+//   fast  208-211  279-285  323-330  356-361  384-386  392-395  417-422  454-457  480-490
+//   mfma8 260-282  330-341  340-344  342-342  405-408  394-405  416-418  405-415  415-430
+// MFMA8's ranking cost steps with the accumulator registers it must rank
+// (8 for <= 16 classes, 12 for <= 24, 16 for <= 32), FAST32's grows
+// linearly; nc 32: 634 / 498.
+constexpr int kAutoMfma8MinClasses = 22;
 inline bool auto_mfma8(int nc) { return nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
@@ -930,6 +931,8 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
                 hipLaunchKernelGGL(classify_mfma8_kernel<4>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
             else if (nc <= 16)
                 hipLaunchKernelGGL(classify_mfma8_kernel<8>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+            else if (nc <= 24)  // registers 0-11 hold classes 0-23
+                hipLaunchKernelGGL(classify_mfma8_kernel<12>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
             else
                 hipLaunchKernelGGL(classify_mfma8_kernel<16>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8,
                                    amb);

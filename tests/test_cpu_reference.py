@@ -148,7 +148,7 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
     mu14, inv14 = stats(14)
     assert ops.classify_plan(mu14, inv14, "auto")[0] == "fast"
-    # at exactly 16 and from 24 classes AUTO runs the exact int8-MFMA distance
+    # at exactly 16 and from 22 classes AUTO runs the exact int8-MFMA distance
     # GEMM (measured faster there; margin in key units)
     mu16, inv16 = stats(16)
     assert ops.classify_plan(mu16, inv16, "auto")[0] == "mfma8"
