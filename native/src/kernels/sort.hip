@@ -356,25 +356,9 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// The same peer mask on the VALU: one ballot per digit bit, each lane keeping
-// the lanes whose bit agrees with its own, m &= ~(ballot ^ own) (one
-// v_bitop3_b32 per 32-bit half on gfx950): 8 x (bfe + cmp + 2 bitop3) VALU
-// per 64 keys and no LDS. The LDS table costs 3 random-address LDS ops per 64
-// keys whose bank conflicts (a half-wave's 32 lanes land on 16 even banks)
-// were ~21 of the scatter's ~35 extra LDS cycles per slice
-// (profiles/lab5_sort.md); the VALU had room (51.6M instructions in ~190 us).
-// `key` is the whole key: bit `shift + b` is digit bit b.
-__device__ __forceinline__ uint64_t match_digit_valu(uint32_t key, int shift) {
-    uint32_t lo = ~0u, hi = ~0u;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const uint32_t own = (uint32_t)__builtin_amdgcn_sbfe((int)key, shift + b, 1);  // 0 or ~0
-        const uint64_t B = __ballot(own != 0u);
-        lo &= ~((uint32_t)B ^ own);
-        hi &= ~((uint32_t)(B >> 32) ^ own);
-    }
-    return ((uint64_t)hi << 32) | lo;
-}
+// (A ballot form of the peer mask — 8 x (bfe + cmp + 2 bitop3) VALU per 64
+// keys, no LDS — ran the round-3 scatter at 85.3M VALU instructions and 214 us
+// per pass against 190 us with the LDS table; retired, profiles/lab5_sort.md.)
 
 // Digit pass. LOOKBACK (onesweep): the tile id comes from an atomic counter
 // and the global digit offsets from decoupled look-back over `status`.
@@ -547,12 +531,9 @@ __device__ __forceinline__ uint32_t scan256_excl_lds(uint32_t v, uint32_t *s_wsu
 // are LDS-only so the prefetch stays in flight across them.
 constexpr int kPersistBlocksPerCU = 2;
 
-// VALU_MATCH: peer masks from ballots (match_digit_valu, production) or from
-// the LDS table (match_digit_lds, the round-2 form: tuning variant 4).
-// REV: walk each XCD's tile range from its end (tuning variant 5): the count
-// kernel that just read this pass's input finished with the range ends, so
-// those tiles are the likeliest to still sit in the 256 MB MALL.
-template <bool VALU_MATCH, bool REV = false>
+// The round-2 production scatter (LDS peer-mask table, leader ds_add_rtn +
+// bpermute ranking), kept as tuning variant 4 for same-process A/B against
+// the lean kernel below.
 __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift, int in_mode, int out_mode,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
@@ -567,7 +548,6 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const int t0 = (int)((int64_t)ntiles * xcd / kNumXCDs);
     int tile = t0 + (int)blockIdx.x / kNumXCDs;
     if (tile >= t1) return;  // block-uniform
-    auto phys = [&](int tl) { return REV ? t0 + t1 - 1 - tl : tl; };  // walk position -> tile
     // digit bases of the whole array (the same for every tile of the pass)
     const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);
 
@@ -580,15 +560,15 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             dst[e] = i < n ? in[i] : 0u;
         }
     };
-    load_tile(raw, phys(tile));
+    load_tile(raw, tile);
     for (; tile < t1; tile += per) {
-        const int ptile = phys(tile);
+        const int ptile = tile;
         const int64_t tile0 = (int64_t)ptile * kRTile;
-        if (tile + per < t1) load_tile(nxt, phys(tile + per));  // in flight under this tile's work
+        if (tile + per < t1) load_tile(nxt, tile + per);  // in flight under this tile's work
         const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
         for (int i = t; i < kRWaves * 256; i += kRThreads) {
             (&s_cnt[0][0])[i] = 0;
-            if (!VALU_MATCH) reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
+            reinterpret_cast<uint64_t *>(s_keys)[i] = 0;
         }
         lds_barrier();
         uint32_t key[kRPer], rank[kRPer];
@@ -604,8 +584,7 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             uint64_t m[kRG];
 #pragma unroll
             for (int e = 0; e < kRG; ++e)
-                m[e] = VALU_MATCH ? match_digit_valu(key[g + e], shift)
-                                  : match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
+                m[e] = match_digit_lds((key[g + e] >> shift) & 255u, lane, tbl);
             uint32_t old[kRG], pre[kRG];
 #pragma unroll
             for (int e = 0; e < kRG; ++e) {
@@ -685,8 +664,8 @@ __device__ __forceinline__ uint32_t to_key_t(uint32_t v) { return to_key(v, MODE
 template <int MODE>
 __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, MODE); }
 
-// Lean persistent scatter (variants 6 / 7). The same schedule and
-// ranking as radix_scatter_kernel<false> (LDS peer-mask table), with the
+// Lean persistent scatter (variants 7 / 8, production). The same schedule and
+// ranking as radix_scatter_kernel (LDS peer-mask table), with the
 // per-key VALU cut — the round-3 counters put the scatter on its VALU pipe
 // (51.6M VALU per pass with the LDS table, 85.3M with ballots; 4 cycles each
 // per SIMD ~ 88 / 145 us of a 190 / 214 us pass):
@@ -704,7 +683,7 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 //     bpermute;
 //   * the next tile's keys load into a second register set while this tile is
 //     ranked, staged and written.
-//   * FEWB (variant 7): four block barriers per tile instead of six — each
+//   * four block barriers per tile instead of six (the retired variant 6) — each
 //     wave zeroes its own counter row after its own staging reads (no other
 //     wave writes that row before the next tile's first barrier), the 256-digit
 //     scan runs on DPP row shifts / broadcasts with one barrier for the four
@@ -714,7 +693,7 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 // waves per SIMD fit the LDS but not the registers: 80 VGPRs spill 280 B per
 // lane). TPB = 256 (variant 8): 4096-key tiles, 4 blocks per CU — twice the
 // independent barrier domains per CU for the same waves.
-template <int IN_MODE, int OUT_MODE, bool FEWB, int TPB = kRThreads>
+template <int IN_MODE, int OUT_MODE, int TPB = kRThreads>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
@@ -815,7 +794,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
                 cnt += s_cnt[ww][t];
             }
         }
-        const uint32_t dstart = FEWB ? scan256_excl_dpp(cnt, s_wsum) : scan256_excl_lds(cnt, s_wsum);
+        const uint32_t dstart = scan256_excl_dpp(cnt, s_wsum);
         if (t < 256) {
 #pragma unroll
             for (int ww = 0; ww < NW; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
@@ -824,15 +803,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
         lds_barrier();
 #pragma unroll
         for (int e = 0; e < kRPer; ++e) s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rank[e]] = key[e];
-        if constexpr (FEWB) {
-            lds_barrier();
-            // this wave's staging reads of its own row are done (program order)
+        lds_barrier();
+        // this wave's staging reads of its own row are done (program order)
 #pragma unroll
-            for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
-        } else {
-            lds_barrier();
-            for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;  // for the next tile
-        }
+        for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
         if (full) {
 #pragma unroll
             for (int j = 0; j < TILE / TPB; ++j) {
@@ -849,7 +823,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
                 if (pos < n32) __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)(pos * 4u), 0, 0);
             }
         }
-        if constexpr (!FEWB) lds_barrier();  // s_keys / s_cnt / s_gbase are rewritten by the next tile
     };
 
     uint32_t a[kRPer], b[kRPer];
@@ -1042,13 +1015,12 @@ RadixWs radix_layout(void *ws, int64_t n) {
 }
 
 // Radix variants: 1 = onesweep (decoupled look-back), 2 = reduce-then-scan
-// (one tile per block), 3 = reduce-then-scan with the persistent prefetching
-// scatter (ballot peer masks, 1024-thread scan), 4 = variant 3 as in round 2
-// (LDS-table peer masks, 256-thread scan; same-process A/B), 5 = variant 3
-// walking each XCD's tiles from the end (MALL reuse probe), 6 = the lean
-// persistent scatter (radix_scatter_lean_kernel), 7 = the same with four
-// barriers per tile (FEWB; production above kOnesweepMaxN), 8 = 7 on
-// 4096-key tiles (256-thread blocks, 4 per CU).
+// (one tile per block), 4 = reduce-then-scan with the round-2 persistent
+// scatter (radix_scatter_kernel, 256-thread scan; same-process A/B), 7 = the
+// lean persistent scatter (radix_scatter_lean_kernel, 8192-key tiles), 8 = 7
+// on 4096-key tiles (256-thread blocks, 4 per CU). Retired after round-3
+// measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
+// tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
@@ -1058,22 +1030,22 @@ constexpr int64_t kTile4kMaxN = (int64_t)1 << 24;    // variant 8 up to here (me
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
-template <bool FEWB, int TPB = kRThreads>
+template <int TPB = kRThreads>
 void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
                  const uint32_t *tot, const uint32_t *offs, int ntiles) {
     const dim3 g((unsigned)blocks), b(TPB);
     const int sh = 8 * p;
     const bool f = mode == kRawF32;
     if (p == 0 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 0)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else if (p == 3)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
     else
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, FEWB, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
 }
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
@@ -1119,26 +1091,17 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 hipLaunchKernelGGL(radix_scan1024_kernel, dim3(256), dim3(kScanThreads), 0, s, r.status, ntiles,
                                    r.hist);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            if (variant >= 6) {
+            if (variant >= 7) {
                 const int rounded = (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs;
-                if (variant == 6)
-                    launch_lean<false>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
-                else if (variant == 7)
-                    launch_lean<true>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
+                if (variant == 7)
+                    launch_lean(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
                 else
-                    launch_lean<true, kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
-                                                      r.status, ntiles);
-            } else if (variant >= 3) {
+                    launch_lean<kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
+                                               r.status, ntiles);
+            } else if (variant == 4) {
                 const int blocks = std::min(kNumCUs * kPersistBlocksPerCU, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
-                if (variant == 3)
-                    hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
-                                       dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
-                else if (variant == 5)
-                    hipLaunchKernelGGL((radix_scatter_kernel<true, true>), dim3((unsigned)blocks), dim3(kRThreads), 0,
-                                       s, src, dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
-                else
-                    hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src,
-                                       dst, n, 8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
+                hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)blocks), dim3(kRThreads), 0, s, src, dst, n,
+                                   8 * p, in_mode, out_mode, r.hist, r.status, ntiles);
             } else {
                 hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst,
                                    n, 8 * p, in_mode, out_mode, r.hist, r.status, r.ctr, r.err, ntiles);
@@ -1288,10 +1251,13 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 }
 
 // Tuning entry (tools/experiments/lab5_bench.py): radix variant 0 = auto, 1 = onesweep
-// (decoupled look-back), 2 = reduce-then-scan, 3-7 = reduce-then-scan with a
-// persistent scatter (see radix_sort32).
+// (decoupled look-back), 2 = reduce-then-scan, 4 / 7 / 8 = reduce-then-scan
+// with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 8) return MPX_ERR_ARG;
+    if (variant < 0 || variant > 8 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 or 8", variant);
+        return MPX_ERR_ARG;
+    }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
 }

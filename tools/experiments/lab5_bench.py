@@ -49,7 +49,7 @@ def main():
     # LAB5_DTYPES=int32,float32 / LAB5_LOGN=26 / LAB5_VARIANTS=3,4 narrow a profiling run
     dts = [getattr(torch, d) for d in os.environ.get("LAB5_DTYPES", "int32,float32,uint8").split(",")]
     lgs = [int(v) for v in os.environ.get("LAB5_LOGN", "16,20,24,26").split(",")]
-    only = {int(v) for v in os.environ.get("LAB5_VARIANTS", "1,2,3,4,5,6,7,8").split(",")}
+    only = {int(v) for v in os.environ.get("LAB5_VARIANTS", "1,2,4,7,8").split(",")}
     for dt in dts:
         for lg in lgs:
             n = 1 << lg
@@ -62,9 +62,8 @@ def main():
             ms, out = gpu_ms(ops.sort_, src)
             variants = {}
             if dt != torch.uint8:
-                for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (3, "reduce_scan_persistent"),
-                              (4, "reduce_scan_persistent_r2"), (5, "reduce_scan_persistent_rev"),
-                              (6, "lean_scatter"), (7, "lean_scatter_fewb"), (8, "lean_scatter_tile4096")):
+                for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (4, "reduce_scan_persistent_r2"),
+                              (7, "lean_scatter"), (8, "lean_scatter_tile4096")):
                     if v not in only:
                         continue
                     try:
