@@ -812,15 +812,20 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
     const int lane = threadIdx.x & 63;
     constexpr bool up = UP;
-    const int cin = x0 + 4 * lane;
-    const bool st = cin < w;
-    const int cc = min(cin, w - 4);
+    // OPT bit 9 (HL, 248-column strips): lane l loads the quad at x0 - 4 + 4l;
+    // lanes 0 and 63 only feed their neighbours through the DPP shifts (no
+    // apron loads) and store nothing
+    constexpr bool HL = (OPT & 512) != 0;
+    const int cin = HL ? x0 - 4 + 4 * lane : x0 + 4 * lane;
+    const bool st = HL ? (lane >= 1 && lane <= 62 && cin < w) : cin < w;
+    const int cc = HL ? min(max(cin, 0), w - 4) : min(cin, w - 4);
     const bool q_right = cin >= w;
+    const bool q_left = HL && cin < 0;  // strip 0, lane 0: clamp-to-edge replicates pixel 0
     // apron: lane 0 reads the two columns left of the strip, lane 63 the two
     // right of it; at the image edges the lane's own edge pixel stands in
     const bool ap_left = lane == 0, ap_right = lane == 63;
     // OPT bit 4 (cost probe only, wrong at strip edges): no apron loads
-    const bool ap_have = !(OPT & 16) && ((ap_left && x0 > 0) || (ap_right && x0 + 256 < w));
+    const bool ap_have = !HL && !(OPT & 16) && ((ap_left && x0 > 0) || (ap_right && x0 + 256 < w));
     constexpr int kDrop = 0x7ffffff0;
     const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : kDrop;
     const int iy0 = ys - A;
@@ -843,7 +848,10 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
         // non-temporal; bit 6: every row does (probes)
-        if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
+        if constexpr (HL) {  // no aprons
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 0);
+            ap = u32x2_t{0u, 0u};
+        } else if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, (OPT & 64) ? 2 : 0);
         } else if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 2);
@@ -856,6 +864,9 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         return q;
     };
     auto fix_quad = [&](u32x4_t q) -> u32x4_t {
+        if constexpr (HL) {
+            if (q_left) return u32x4_t{q.x, q.x, q.x, q.x};
+        }
         return q_right ? u32x4_t{q.w, q.w, q.w, q.w} : q;
     };
     // OPT bit 3 (walks of at most 32 rows): every apron of the walk in ONE
@@ -1023,7 +1034,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // results at the strip edges), bit 5 non-temporal loads of rows no neighbouring
 // segment reads, bit 6 non-temporal loads of every row, bit 7 keeps the apron
 // loads plain under bit 5 / 6, bit 3 one batched apron load per walk (walks of
-// at most 32 rows: segment + K - 1 <= 32).
+// at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
+// lanes instead of aprons.
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
@@ -1042,10 +1054,11 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
     const int sg = (!(alt & 2) || segs < 3 || sg0 == 0) ? sg0 : (sg0 == 1 ? segs - 1 : sg0 - 1);
     const int ys = oy0 + sg * seg;
     const int ye = min(ys + seg, oy1);
+    constexpr int SW = (OPT & 512) ? 248 : 256;  // output columns per strip
     if ((alt & 1) && (sg & 1))  // wave-uniform: odd segments walk up
-        band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+        band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
     else
-        band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+        band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
 }
 
 // Gray value packing helper for the non-stream kernels.

@@ -127,7 +127,7 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     if (!rs.up) rs.up = in;
     if (!rs.dn) rs.dn = in;
     if (rs.up != in || rs.dn != in) alt |= 2;  // remote halo rows: boundary segments first
-    const int strips = (w + 255) / 256;
+    const int strips = (OPT & 512) ? (w + 247) / 248 : (w + 255) / 256;
     if (seg <= 0) {
         const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
         const int64_t work = (int64_t)(oy1 - oy0) * strips;
@@ -149,15 +149,19 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // rows) are 16-B aligned, with non-temporal output stores. MI355X 4096^2, 6
 // rotated pairs (tools/kbench.py, µs): sobel5 separable 28.9 (30.3 with the
 // 8-B-lane wave kernel; 29.4 with plain stores), sobel5_dense 32.7 (41.4),
-// Roberts 27.8 (30.4). Default (2): NT stores, plain loads. MPX_CONV_BAND=0:
-// wave kernel, 1: band kernel with plain stores, 3: NT stores + non-temporal
-// loads of the rows no neighbouring segment re-reads (three same-box runs:
-// -2.8% / +2% / -1% on sobel5, sobel5_dense +6%: no stable gain, not the
-// default); read once per process.
+// Roberts 27.8 (30.4). Default (-1, MPX_CONV_BAND unset): separable windows
+// also load the rows no neighbouring segment re-reads non-temporally (OPT 34),
+// dense windows keep plain loads (OPT 2) — round 3, bench.py alternated on two
+// boxes: 583 / 584 / 583 and 574 / 582 Gpixel/s plain vs 614 / 603 / 605 and
+// 604 / 588 non-temporal; kbench: gauss5 -1.3 us, sobel5 -0.3 to -0.8,
+// sobel5_dense +0.4 to +2.9 (profiles/lab2_conv.md). MPX_CONV_BAND=0: wave
+// kernel, 1: band kernel with plain stores, 2: NT stores and plain loads
+// everywhere, 3: NT stores + NT interior loads everywhere; read once per
+// process.
 inline int band_mode() {
     static const int v = [] {
         const char *e = std::getenv("MPX_CONV_BAND");
-        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 2;
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
     }();
     return v;
 }
@@ -181,9 +185,10 @@ inline constexpr bool kBandFits = A <= 2 && K - 1 - A <= 2;
 template <int K, int A, int MODE, class F>
 int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                 const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
-    if (band_mode() == 1)
+    const int m = band_mode();
+    if (m == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-    if (band_mode() == 2)
+    if (m == 2 || (m < 0 && !F::kSep))
         return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
     return launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
 }

@@ -237,7 +237,7 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         // band kernel (conv_band4_kernel): p1 = segment rows (0 = auto), p2 % 100 =
         // waves per SIMD the auto segments target (0 = default), p2 / 100 % 10 == 1: no
         // alternation; p2 / 1000 = OPT (1: 5 waves per SIMD, 2: NT stores, 3: both, 6: NT + 16-wave groups,
-        // 34 / 66: NT stores + NT interior / all row loads)
+        // 34 / 66: NT stores + NT interior / all row loads, 514: NT stores + 248-column strips with halo lanes)
         MPX_CHECK_ARG(k == 5 && p1 >= 0 && w % 4 == 0 && aligned16(in) && aligned16(out), "band variant: k = 5, w % 4 == 0");
         const Taps st = make_taps(k, wx, wy, true, true);
         const int per = p2 % 100 > 0 ? p2 % 100 : edgel::kBand4PerSimd, alt = (p2 / 100) % 10 == 1 ? 0 : 1;
@@ -246,7 +246,7 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
     case O:                                                                                                   \
         return edgel::launch_band4<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps, O>(in, out, w, w, 0, h, 0, h - 1, st, s, \
                                                                                       p1, edge::RowSrc{}, per, alt);
-            MPX_BAND4(0) MPX_BAND4(1) MPX_BAND4(2) MPX_BAND4(3) MPX_BAND4(6) MPX_BAND4(18) MPX_BAND4(34) MPX_BAND4(66) MPX_BAND4(162) MPX_BAND4(10) MPX_BAND4(11)
+            MPX_BAND4(0) MPX_BAND4(1) MPX_BAND4(2) MPX_BAND4(3) MPX_BAND4(6) MPX_BAND4(18) MPX_BAND4(34) MPX_BAND4(66) MPX_BAND4(162) MPX_BAND4(10) MPX_BAND4(11) MPX_BAND4(514)
 #undef MPX_BAND4
         }
         set_error("unsupported band OPT %d", p2 / 1000);

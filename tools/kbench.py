@@ -102,7 +102,7 @@ def main():
                                                               swx, swy, 0))), sref)
     for seg, per in ((0, 0), (0, 2000), (24, 2000), (0, 18000), (0, 34000), (0, 66000), (0, 162000),
                      (20, 34000), (24, 34000), (12, 34000),
-                     (0, 10000), (0, 10005), (0, 11005), (24, 10000)):
+                     (0, 10000), (0, 10005), (0, 11005), (24, 10000), (0, 514000), (0, 514005)):
         # 18000: no apron loads — a cost probe whose strip edges are wrong (no reference check)
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
