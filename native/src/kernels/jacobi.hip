@@ -230,7 +230,10 @@ __device__ __forceinline__ T wave_max_dpp(T v) {
     }
 }
 
-template <typename T, int AUX = 0, bool LNT = false, bool TAIL_EXIT = true, bool PEER = false, bool ALT = false,
+// LNT: 0 plain loads, 1 every row non-temporal (tuning), 2 only the rows no
+// neighbouring row block reads (i0 + 1 .. i1 - 2), the conv band kernel's
+// round-3 default for separable windows
+template <typename T, int AUX = 0, int LNT = 0, bool TAIL_EXIT = true, bool PEER = false, bool ALT = false,
           int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restrict__ u, T *__restrict__ un, int cols,
                                                           int pitch, int r0, int r1, int strips, int rows_per_wave,
@@ -282,8 +285,11 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
                     return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, kCpolSystem));
                 }
             }
-            if constexpr (LNT) return __builtin_nontemporal_load(p);  // tuning variant
-            else return *p;
+            if constexpr (LNT == 1) return __builtin_nontemporal_load(p);  // tuning variant
+            if constexpr (LNT == 2) {
+                if (i > i0 && i < i1 - 1) return __builtin_nontemporal_load(p);  // wave-uniform
+            }
+            return *p;
         };
         const uint32_t soff = out_lane ? (uint32_t)(cv * NV * sizeof(T)) : kDrop;
         const int j0 = cv * NV;
@@ -437,7 +443,7 @@ int launch_jacobi(const T *u, T *un, int cols, int pitch, int r0, int r1, T *res
         int R = kJacobiRows;
         while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
         const int nwaves = strips * ((rows + R - 1) / R);
-        hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
+        hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 0, true, false, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
                            as_stream(stream), u, un, cols, pitch, r0, r1, strips, R, nwaves, resid, mpx_jacobi_peer{});
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
         return MPX_OK;
@@ -471,7 +477,7 @@ int launch_jacobi_peer(const T *u, T *un, int cols, int pitch, int rows, T *resi
     int R = kJacobiRows;
     while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;
     const int nwaves = strips * ((rows + R - 1) / R);
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, true, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 0, true, true, true>), dim3((nwaves + 3) / 4), dim3(256), 0,
                        as_stream(stream), u, un, cols, pitch, 1, rows + 1, strips, R, nwaves, resid, pr);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
@@ -510,9 +516,10 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
                                   int R, int aux, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(u && un && cols >= 1 && pitch >= cols && r0 >= 1 && r1 >= r0 && R >= 1, "bad arguments");
-    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6 || aux == 10 || aux == 18 || aux == 50,
+    MPX_CHECK_ARG(aux == 0 || aux == 2 || aux == 6 || aux == 10 || aux == 18 || aux == 22 || aux == 50,
                   "aux must be 0, 2, 6 (2 + non-temporal loads), 10 (2 without the tail exit) or 18 (2 + "
-                  "alternating walk directions), 50 (18 with 16-wave workgroups)");
+                  "alternating walk directions), 22 (18 + non-temporal interior row loads), 50 (18 with 16-wave "
+                  "workgroups)");
     const int NV = fp64 ? 2 : 4;
     MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un), "needs the vector layout");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
@@ -523,25 +530,29 @@ extern "C" int mpx_jacobi_variant(void *u, void *un, int cols, int pitch, int r0
     hipLaunchKernelGGL((jacobi_wave_kernel<T, A>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, \
                        R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVN(T)                                                                                             \
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, true>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 1>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, r1,    \
                        strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVA(T)                                                                                             \
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true>), g, b, 0, s, (const T *)u, (T *)un, cols,  \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 0, true, false, true>), g, b, 0, s, (const T *)u, (T *)un, cols,  \
                        pitch, r0, r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVW(T)                                                                                             \
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, true, false, true, 16>), dim3((nwaves + 15) / 16), dim3(1024),  \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 0, true, false, true, 16>), dim3((nwaves + 15) / 16), dim3(1024),  \
                        0, s, (const T *)u, (T *)un, cols, pitch, r0, r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
+#define MPX_JVI(T)                                                                                             \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 2, true, false, true>), g, b, 0, s, (const T *)u, (T *)un, cols,  \
+                       pitch, r0, r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
 #define MPX_JVX(T)                                                                                             \
-    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, false, false>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, \
+    hipLaunchKernelGGL((jacobi_wave_kernel<T, 2, 0, false>), g, b, 0, s, (const T *)u, (T *)un, cols, pitch, r0, \
                        r1, strips, R, nwaves, (T *)resid, mpx_jacobi_peer{})
     if (fp64) {
-        if (aux == 50) MPX_JVW(double); else if (aux == 18) MPX_JVA(double); else if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
+        if (aux == 22) MPX_JVI(double); else if (aux == 50) MPX_JVW(double); else if (aux == 18) MPX_JVA(double); else if (aux == 10) MPX_JVX(double); else if (aux == 6) MPX_JVN(double); else if (aux) MPX_JV(double, 2); else MPX_JV(double, 0);
     } else {
-        if (aux == 50) MPX_JVW(float); else if (aux == 18) MPX_JVA(float); else if (aux == 10) MPX_JVX(float); else if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
+        if (aux == 22) MPX_JVI(float); else if (aux == 50) MPX_JVW(float); else if (aux == 18) MPX_JVA(float); else if (aux == 10) MPX_JVX(float); else if (aux == 6) MPX_JVN(float); else if (aux) MPX_JV(float, 2); else MPX_JV(float, 0);
     }
 #undef MPX_JV
 #undef MPX_JVN
 #undef MPX_JVX
+#undef MPX_JVI
 #undef MPX_JVA
 #undef MPX_JVW
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
