@@ -740,7 +740,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
             const uint32_t voff = (uint32_t)tile0 * 4u + (uint32_t)vlane;  // < n * 4 < 2^32
 #pragma unroll
             for (int e = 0; e < kRPer; ++e)
-                dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * 256u), 0, 0);
+                // non-temporal: the keys are read once, and L2 stays free to merge
+                // the partial-line digit runs this tile and its XCD neighbours
+                // write (2^26 int32 0.828 -> 0.769 ms; NT output stores instead
+                // lose those merges: 1.28 ms; profiles/lab5_sort.md)
+                dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * 256u), 0, 2);
         } else {  // 32-bit indices (n < 2^30) keep the partial path's registers small
             const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
 #pragma unroll
