@@ -224,6 +224,9 @@ def run(args) -> int:
 
     seen = {"torch_distributed": dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1,
             "rccl_native": ctx.native.size() if ctx.native is not None else None}
+    # which physical GPU each rank ran on (PCI domain:bus:device), so an N-GPU
+    # record shows N distinct devices
+    rank_devices = parallel.all_gather_object(device_id(ctx.device), ctx)
     if ctx.rank == 0:
         rec = {
             "metric": BASELINE_METRIC,
@@ -258,6 +261,8 @@ def run(args) -> int:
                 "working_set_MiB_per_gpu": round(len(dets) * 2 * args.size * args.size * 4 / 2**20, 1),
             },
             "world_size_seen": seen,
+            "rank_devices": rank_devices,
+            "distinct_devices": len(set(rank_devices)),
             "per_rank_ms_per_step": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
             "verified_bit_exact": ok and (args.no_verify or checked == n * len(dets) * args.size * args.size),
             "verified_pixels": checked,
@@ -338,6 +343,19 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     if rec.get("verified_bit_exact") is None:
         rec.pop("verified_bit_exact", None)
     return rec
+
+
+def device_id(dev) -> str:
+    """PCI location of a GPU ("dddd:bb:dd"), or "cpu"."""
+    import torch
+
+    if dev.type != "cuda":
+        return "cpu"
+    p = torch.cuda.get_device_properties(dev)
+    bus = getattr(p, "pci_bus_id", None)
+    if bus is None:
+        return f"cuda:{dev.index}"
+    return f"{getattr(p, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(p, 'pci_device_id', 0):02x}"
 
 
 def regen_slab(seed: int, rows: int, size: int, device):

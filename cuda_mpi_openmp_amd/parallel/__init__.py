@@ -1,6 +1,6 @@
 """Multi-GPU tier: one process per MI355X, torch.distributed over RCCL/xGMI."""
 
-from .collectives import (all_gather_floats, all_reduce_max, all_reduce_sum, all_reduce_sum_host,
+from .collectives import (all_gather_floats, all_gather_object, all_reduce_max, all_reduce_sum, all_reduce_sum_host,
                           broadcast_object, gather_slabs, max_over_ranks, scatter_rows)
 from .dist import DistContext, context, init, shutdown
 from .fault import EXIT_HUNG, FaultInjected, Watchdog, fault_hook
@@ -10,6 +10,7 @@ from .slab import Slab, max_rows_per_gpu, min_ranks_for
 
 __all__ = [
     "all_gather_floats",
+    "all_gather_object",
     "all_reduce_max",
     "all_reduce_sum_host",
     "all_reduce_sum",

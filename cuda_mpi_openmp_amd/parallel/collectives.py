@@ -79,6 +79,15 @@ def all_reduce_sum_host(value: float, ctx: DistContext) -> float:
     return float(t.item())
 
 
+def all_gather_object(obj: Any, ctx: DistContext) -> List[Any]:
+    """Every rank's picklable host object, in rank order."""
+    if not ctx.is_distributed:
+        return [obj]
+    every: List[Any] = [None] * ctx.world
+    dist.all_gather_object(every, obj)
+    return every
+
+
 def broadcast_object(obj: Any, ctx: DistContext, src: int = 0) -> Any:
     if not ctx.is_distributed:
         return obj

@@ -96,6 +96,8 @@ def test_bench_self_launches_ranks_cpu():
     """--gpus N without a torchrun environment launches N ranks itself."""
     rec = _run(["--gpus", "3", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2"])
     assert rec["n_gpus"] == 3 and rec["world_size_seen"]["torch_distributed"] == 3
+    # one entry per rank naming the device it ran on (PCI location on GPUs)
+    assert rec["rank_devices"] == ["cpu"] * 3 and rec["distinct_devices"] == 1
     assert len(rec["per_rank_ms_per_step"]) == 3 and rec["verified_bit_exact"] is True
     # every pixel of every rotated slab on every rank was compared
     assert rec["verified_pixels"] == 3 * 2 * 64 * 64
