@@ -149,19 +149,19 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // rows) are 16-B aligned, with non-temporal output stores. MI355X 4096^2, 6
 // rotated pairs (tools/kbench.py, µs): sobel5 separable 28.9 (30.3 with the
 // 8-B-lane wave kernel; 29.4 with plain stores), sobel5_dense 32.7 (41.4),
-// Roberts 27.8 (30.4). Default (-1, MPX_CONV_BAND unset): separable windows
-// also load the rows no neighbouring segment re-reads non-temporally (OPT 34),
-// dense windows keep plain loads (OPT 2) — round 3, bench.py alternated on two
-// boxes: 583 / 584 / 583 and 574 / 582 Gpixel/s plain vs 614 / 603 / 605 and
-// 604 / 588 non-temporal; kbench: gauss5 -1.3 us, sobel5 -0.3 to -0.8,
-// sobel5_dense +0.4 to +2.9 (profiles/lab2_conv.md). MPX_CONV_BAND=0: wave
-// kernel, 1: band kernel with plain stores, 2: NT stores and plain loads
-// everywhere, 3: NT stores + NT interior loads everywhere; read once per
-// process.
+// Roberts 27.8 (30.4). Default (MPX_CONV_BAND unset or 3): NT stores and
+// non-temporal loads of the rows no neighbouring segment re-reads (OPT 34) —
+// round 3, bench.py alternated on two boxes: 583 / 584 / 583 and 574 / 582
+// Gpixel/s with plain loads vs 614 / 603 / 605 and 604 / 588; every named
+// filter through ops.conv, two alternations (µs, plain -> NT): sobel5 28.4 ->
+// 27.0, gauss5 28.0 -> 27.1, gauss5_dense 30.7 -> 27.1, sobel5_dense 32.9 ->
+// 32.3, 3x3 filters -0.6 to -0.8, Roberts / sharpen3 / box3 within 0.15
+// (profiles/lab2_conv.md). MPX_CONV_BAND=0: wave kernel, 1: band kernel with
+// plain stores, 2: NT stores and plain loads; read once per process.
 inline int band_mode() {
     static const int v = [] {
         const char *e = std::getenv("MPX_CONV_BAND");
-        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
+        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
     }();
     return v;
 }
@@ -188,7 +188,7 @@ int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     const int m = band_mode();
     if (m == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-    if (m == 2 || (m < 0 && !F::kSep))
+    if (m == 2)
         return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
     return launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
 }
