@@ -45,11 +45,18 @@ __device__ __forceinline__ uint32_t mag_to_gray(float s) {
     }
 }
 
-// Fast path for two magnitudes at once: r = v_sqrt(min(s, 255^2)) decides
+// Fast path for two magnitudes at once: r = v_sqrt(med3(s, 0.5^2, 255.5^2)) decides
 // trunc(sqrt_rn(s)) unless fract(r) is within kSqrtMargin of an integer; one
 // wave-level branch then recomputes both lanes' pair exactly (rare).
 __device__ __forceinline__ void mag2_to_gray(float s0, float s1, uint32_t &g0, uint32_t &g1) {
-    const float c0 = fminf(s0, 65025.0f), c1 = fminf(s1, 65025.0f);
+    // clamp into [0.5^2, 255.5^2] with one v_med3_f32: a zero gradient then
+    // gives r = 0.5 and a saturated one r = 255.5, both half-way between
+    // integers, so the margin test decides them on the fast path (trunc = 0 /
+    // 255, the exact answers) instead of sending them to the fallback — a
+    // plain min(s, 255^2) put both exactly on an integer. Iterated (streaming)
+    // frames are full of them, random frames almost never.
+    const float c0 = __builtin_amdgcn_fmed3f(s0, 0.25f, 65280.25f);
+    const float c1 = __builtin_amdgcn_fmed3f(s1, 0.25f, 65280.25f);
     const float r0 = __builtin_amdgcn_sqrtf(c0), r1 = __builtin_amdgcn_sqrtf(c1);
     const float f0 = __builtin_amdgcn_fractf(r0), f1 = __builtin_amdgcn_fractf(r1);
     constexpr float kHalfOpen = 0.5f - kSqrtMargin;
