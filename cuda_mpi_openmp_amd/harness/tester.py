@@ -122,17 +122,36 @@ class Tester:
         print(f"[Experiments] FINISH time exe: {time.time() - t0}")
         return df
 
-    def report_speedup(self, df: pd.DataFrame) -> None:
+    def report_speedup(self, df: pd.DataFrame) -> Optional[pd.DataFrame]:
+        """CPU median / GPU median per GPU group (kernel_size, n_gpus): printed
+        and persisted as ``speedup_<gpu bin>.csv`` next to the stats CSVs (SURVEY
+        §5 ``speedup_vs_cpu``; the reference keeps every run attribute in CSV,
+        reference tester.py:254-285)."""
         if "CPU" not in set(df["device"]) or self.gpu_label not in set(df["device"]):
-            return
-        cpu = df[df["device"] == "CPU"]["time_kernel_exe_ms"].median()
+            return None
+        cpu_t = df[df["device"] == "CPU"]["time_kernel_exe_ms"]
+        cpu = cpu_t.median()
         g = df[df["device"] == self.gpu_label].copy()
         g["ks"] = g["kernel_size"].apply(_kernel_key)
-        for ks, grp in g.groupby("ks"):
+        if "n_gpus" not in g:
+            g["n_gpus"] = 1
+        rows = []
+        for (ks, ng), grp in g.groupby(["ks", "n_gpus"]):
             med = grp["time_kernel_exe_ms"].median()
-            if med:
-                print(f"[Speedup] CPU median {cpu:.5f} ms / {self.gpu_label}_{ks} median {med:.5f} ms = "
-                      f"{cpu / med:.1f}x")
+            if not med:
+                continue
+            print(f"[Speedup] CPU median {cpu:.5f} ms / {self.gpu_label}_{ks} median {med:.5f} ms = "
+                  f"{cpu / med:.1f}x")
+            rows.append({"device": self.gpu_label, "kernel_size": ks, "n_gpus": int(ng),
+                         "gpu_runs": int(len(grp)), "gpu_median_ms": float(med),
+                         "cpu_runs": int(len(cpu_t)), "cpu_median_ms": float(cpu),
+                         "speedup_vs_cpu": float(cpu / med)})
+        if not rows:
+            return None
+        out = pd.DataFrame(rows)
+        bin_name = os.path.splitext(os.path.basename(self.binary_path_gpu))[0]
+        out.to_csv(os.path.join(self.dir2save, f"speedup_{bin_name}.csv"), index=False)
+        return out
 
     def plot(self, df: pd.DataFrame) -> Optional[str]:
         """``median_execution_time.png`` next to the GPU binary (utils/plots.py)."""

@@ -126,6 +126,38 @@ __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restri
     }
 }
 
+// Burst-tile probe (v = 16): a workgroup of T threads owns
+// a tile of 4T columns x R output rows, every lane ONE aligned 16-B quad per
+// row; it issues all R + 4 row loads of its column at once (no walking ring),
+// then stores R rows (out[y] = in[y-2] ^ in[y] ^ in[y+2] keeps every halo load
+// live) and exits. Tiles are many rounds deep, so the dispatcher sweeps the
+// in-flight window down the image the way the linear copy does. F bit 0:
+// xcd_remap (each XCD sweeps a contiguous eighth of the tiles, vertical
+// neighbours share its L2), else blockIdx order (one window over all XCDs);
+// bit 1: non-temporal loads; bit 2: non-temporal stores.
+template <int R, int F>
+__global__ __launch_bounds__(1024) void burst_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
+                                                          int w4, int h, int tpr) {
+    const int b = (F & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int band = b / tpr, chunk = b - band * tpr;
+    const int c = chunk * (int)blockDim.x + (int)threadIdx.x;
+    const int ys = band * R;
+    u32x4_t r[R + 4];
+#pragma unroll
+    for (int j = 0; j < R + 4; ++j) {
+        const int y = min(max(ys - 2 + j, 0), h - 1);
+        if constexpr ((F & 2) != 0) r[j] = __builtin_nontemporal_load(in + (int64_t)y * w4 + c);
+        else r[j] = in[(int64_t)y * w4 + c];
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if (ys + j >= h) break;
+        const u32x4_t o = r[j] ^ r[j + 2] ^ r[j + 4];
+        if constexpr ((F & 4) != 0) __builtin_nontemporal_store(o, out + (int64_t)(ys + j) * w4 + c);
+        else out[(int64_t)(ys + j) * w4 + c] = o;
+    }
+}
+
 }  // namespace
 
 extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, int h, int v, int d, int seg,
@@ -142,6 +174,33 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
         return MPX_OK;
     }
     MPX_CHECK_ARG(seg > 0, "seg must be > 0");
+    if (v == 16) {  // burst tiles: seg = R output rows per tile, d = F | (threads code << 4)
+        const int tcode = (d >> 4) & 3, F = d & 7;
+        MPX_CHECK_ARG(tcode <= 2, "burst probe: threads code 0 / 1 / 2 = 256 / 512 / 1024");
+        const int tpb = 256 << tcode;
+        MPX_CHECK_ARG(w % (4 * tpb) == 0, "burst probe: w %% (4 * threads) == 0");
+        const int tpr = w / (4 * tpb), nb = (h + seg - 1) / seg;
+        const dim3 g((unsigned)(nb * tpr)), b(tpb);
+        const u32x4_t *vi = (const u32x4_t *)in;
+        u32x4_t *vo = (u32x4_t *)out;
+#define MPX_BURST_F(RR, FF) \
+    case FF: hipLaunchKernelGGL((burst_copy_kernel<RR, FF>), g, b, 0, s0, vi, vo, w / 4, h, tpr); break;
+#define MPX_BURST(RR)                                                                                            \
+    case RR:                                                                                                     \
+        switch (F) {                                                                                             \
+            MPX_BURST_F(RR, 0) MPX_BURST_F(RR, 1) MPX_BURST_F(RR, 2) MPX_BURST_F(RR, 3) MPX_BURST_F(RR, 4)       \
+            MPX_BURST_F(RR, 5) MPX_BURST_F(RR, 6) MPX_BURST_F(RR, 7)                                             \
+        }                                                                                                        \
+        break;
+        switch (seg) {
+            MPX_BURST(2) MPX_BURST(4) MPX_BURST(8) MPX_BURST(12) MPX_BURST(16) MPX_BURST(24)
+            default: set_error("unsupported burst rows %d", seg); return MPX_ERR_ARG;
+        }
+#undef MPX_BURST
+#undef MPX_BURST_F
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+        return MPX_OK;
+    }
     if (v == 8) {  // row bands: seg = rows per band (multiple of 8), d = flag bits
         MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 64, "band probe: w % 4096 == 0, seg % 4 == 0");
         const int tpb = (d & 16) ? 512 : 1024;

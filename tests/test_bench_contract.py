@@ -63,6 +63,25 @@ def test_bench_json_carries_no_hard_coded_ratio():
     assert abs(rec["vs_baseline"] - rec["value"] / 4.4) < 0.01 + 1e-3 * rec["vs_baseline"]
 
 
+def test_bench_measurement_hygiene_fields_cpu():
+    """the CPU baseline is a median of >= 5 runs (min too), the
+    published-methodology serial -O0 time rides along, and the time-based
+    warm-up reports what it ran (the driver's "warmup" field stays W)."""
+    rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2", "--no-stream",
+                "--warmup-ms", "5"])
+    assert rec["warmup"] == 1 and rec["warmup_ms"] >= 5.0 and rec["warmup_steps_run"] >= 2
+    assert rec["cpu_runs"] >= 5 and 0 < rec["cpu_ms_per_image_min"] <= rec["cpu_ms_per_image"]
+    assert abs(rec["speedup_vs_cpu"] - rec["cpu_ms_per_image"] / rec["gpu_ms_per_image"]) \
+        < 0.051 + 1e-3 * rec["speedup_vs_cpu"]
+    if os.path.exists(os.path.join(ROOT, "labs", "lab2", "src", "cpu_exe")):
+        assert rec["cpu_serial_o0_ms_per_image"] > 0
+        assert abs(rec["speedup_vs_cpu_serial_o0"] - rec["cpu_serial_o0_ms_per_image"] / rec["gpu_ms_per_image"]) \
+            < 0.051 + 1e-3 * rec["speedup_vs_cpu_serial_o0"]
+    rec0 = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2", "--no-stream",
+                 "--warmup-ms", "0", "--no-warm"])
+    assert rec0["warmup_ms"] == 0 and rec0["warmup_steps_run"] == 0
+
+
 def test_bench_contract_single_process_cpu():
     rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--overlap", "pipeline"])
     assert REQUIRED <= set(rec) and rec["n_gpus"] == 1

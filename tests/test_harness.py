@@ -96,6 +96,12 @@ def test_harness_lab2_cpu_binaries(tmp_path):
         assert col in df.columns
     assert len(df) == 3 and df["test_verification_result"].all()
     assert os.path.exists(lab / "src" / "median_execution_time.png")
+    # the CPU/GPU speedup of every GPU group is persisted, not only printed
+    sp = pd.read_csv(lab / "src" / "speedup_cpu_omp_exe.csv")
+    for col in ("device", "kernel_size", "n_gpus", "gpu_median_ms", "cpu_median_ms", "speedup_vs_cpu"):
+        assert col in sp.columns
+    assert len(sp) == 1 and sp["gpu_runs"][0] == 3 and sp["cpu_runs"][0] == 3
+    assert abs(sp["speedup_vs_cpu"][0] - sp["cpu_median_ms"][0] / sp["gpu_median_ms"][0]) < 1e-9
     # outputs land under data_out/<bin>_<k1>_<k2>/, inputs untouched
     assert os.path.isdir(lab / "data_out" / "cpu_omp_exe_None_None")
     assert sorted(os.listdir(lab / "data")) == sorted(os.listdir(os.path.join(ROOT, "labs", "lab2", "data")))

@@ -147,6 +147,18 @@ def main():
             variants[f"copy/band-seg{seg}-f{fl}"] = (
                 (lambda fl=fl, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
                                                                               fl, seg, 0))), None)
+    # burst tiles: R output rows per tile, all R + 4 row
+    # loads of a lane issued at once, many rounds of tiles; f = flag bits
+    # (1 xcd_remap, 2 NT loads, 4 NT stores), t = threads per workgroup
+    for R in (2, 4, 8, 12, 16, 24):
+        for tcode in (0, 1, 2):
+            for fl in (0, 1, 4, 5, 6, 7):
+                if tcode == 1 and fl not in (5, 7):
+                    continue
+                d = fl | (tcode << 4)
+                variants[f"copy/burst-r{R}-t{256 << tcode}-f{fl}"] = (
+                    (lambda d=d, R=R: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 16,
+                                                                            d, R, 0))), None)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
