@@ -233,6 +233,15 @@ def run(args) -> int:
     # which physical GPU each rank ran on (PCI domain:bus:device), so an N-GPU
     # record shows N distinct devices
     rank_devices = parallel.all_gather_object(device_id(ctx.device), ctx)
+    # an N-GPU record must come from N distinct GPUs unless ranks share devices
+    # on purpose (one-GPU rehearsals, CPU dry runs): ADVICE r3
+    rehearsal = (ctx.device.type != "cuda" or os.environ.get("MPX_DIST_BACKEND") == "gloo"
+                 or os.environ.get("MPX_DIST_CONTRACT") == "nccl")
+    shared_devices = n > 1 and len(set(rank_devices)) < n and not rehearsal
+    if shared_devices and ctx.rank == 0:
+        print(f"[bench] {n} ranks ran on {len(set(rank_devices))} distinct device(s) {rank_devices}; an {n}-GPU "
+              f"record needs {n} GPUs", file=sys.stderr)
+    ok &= not shared_devices
     if ctx.rank == 0:
         rec = {
             "metric": BASELINE_METRIC,
@@ -271,6 +280,7 @@ def run(args) -> int:
             "world_size_seen": seen,
             "rank_devices": rank_devices,
             "distinct_devices": len(set(rank_devices)),
+            "rehearsal": rehearsal,
             "per_rank_ms_per_step": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
             "verified_bit_exact": ok and (args.no_verify or checked == n * len(dets) * args.size * args.size),
             "verified_pixels": checked,

@@ -8,6 +8,7 @@ lab3 class parameters computed on one rank.
 
 from __future__ import annotations
 
+import os
 from typing import Any, List, Optional
 
 import torch
@@ -20,6 +21,16 @@ from .slab import Slab
 def _native_ok(x: torch.Tensor, ctx: DistContext) -> bool:
     return ctx.native is not None and x.is_cuda and x.is_contiguous() and x.dtype in (
         torch.float64, torch.float32, torch.int32)
+
+
+def _scalar_device(ctx: DistContext, site: str):
+    """Where a host scalar's tensor goes for a collective: the rank's GPU under
+    RCCL (it takes device tensors only), the host under gloo.
+    ``MPX_CONTRACT_INJECT=<site>`` puts it on the host anyway — a test hook
+    that the nccl contract (parallel/contract.py) must catch at ``site``."""
+    if ctx.backend != "nccl" or os.environ.get("MPX_CONTRACT_INJECT") == site:
+        return "cpu"
+    return ctx.device
 
 
 def _host_staged(x: torch.Tensor, ctx: DistContext) -> bool:
@@ -54,7 +65,7 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
     """Max of a host scalar over ranks (e.g. each rank's step time)."""
     if not ctx.is_distributed:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_scalar_device(ctx, "max_over_ranks"))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -63,7 +74,7 @@ def all_gather_floats(value: float, ctx: DistContext) -> List[float]:
     """Every rank's host scalar, in rank order (e.g. per-rank step times)."""
     if not ctx.is_distributed:
         return [float(value)]
-    dev = ctx.device if ctx.backend == "nccl" else "cpu"
+    dev = _scalar_device(ctx, "all_gather_floats")
     mine = torch.tensor([float(value)], dtype=torch.float64, device=dev)
     every = [torch.empty_like(mine) for _ in range(ctx.world)]
     dist.all_gather(every, mine)
@@ -74,7 +85,7 @@ def all_reduce_sum_host(value: float, ctx: DistContext) -> float:
     """Sum of a host scalar over ranks."""
     if not ctx.is_distributed:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_scalar_device(ctx, "all_reduce_sum_host"))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 

@@ -18,6 +18,8 @@ from typing import Any, Optional
 import torch
 import torch.distributed as dist
 
+from . import contract as _contract
+
 
 @dataclass
 class DistContext:
@@ -67,26 +69,44 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    contract = _contract.active()
+    rehearsal = contract or os.environ.get("MPX_DIST_BACKEND") == "gloo"
     if use_cuda:
         ndev = torch.cuda.device_count()
         if ndev == 0:
             raise RuntimeError("device='cuda' requested but no GPU is visible")
+        if world > ndev and not rehearsal:
+            # ranks would silently share devices (local_rank % ndev): refuse, as
+            # the launcher does before spawning (sysfs may list GPUs
+            # this container cannot open)
+            import sys
+
+            print(f"[dist] WORLD_SIZE={world} but only {ndev} GPU(s) are usable in this process; refusing to put "
+                  f"several ranks on one device (MPX_DIST_CONTRACT=nccl or MPX_DIST_BACKEND=gloo rehearse that)",
+                  file=sys.stderr)
+            raise SystemExit(2)
         torch.cuda.set_device(local_rank % ndev)
         dev = torch.device("cuda", local_rank % ndev)
     else:
         dev = torch.device("cpu")
     if backend is None:
         # MPX_DIST_BACKEND=gloo: control plane over gloo, e.g. to rehearse several
-        # ranks on one GPU (RCCL refuses two ranks per device)
-        backend = os.environ.get("MPX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+        # ranks on one GPU (RCCL refuses two ranks per device);
+        # MPX_DIST_CONTRACT=nccl: the same rehearsal through the nccl code paths
+        # (parallel/contract.py)
+        backend = "nccl" if contract else (os.environ.get("MPX_DIST_BACKEND") or ("nccl" if use_cuda else "gloo"))
     ctx = DistContext(rank=rank, world=world, local_rank=local_rank, device=dev, backend=backend)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda and backend == "nccl":
+        kw = dict(backend="gloo" if contract else backend, rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if use_cuda and backend == "nccl" and not contract:
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    if world > 1 and use_cuda and backend == "nccl":
+    if world > 1 and contract:
+        _contract.install(dev)
+        ctx.native = _contract.ContractNativeComm.create(ctx) if use_cuda else None
+    elif world > 1 and use_cuda and backend == "nccl":
         from .native_comm import NativeComm  # collective: every rank runs init()
 
         ctx.native = NativeComm.create(ctx)
@@ -103,6 +123,7 @@ def shutdown() -> None:
         _CTX.native = None
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+    _contract.uninstall()
     _CTX = None
 
 

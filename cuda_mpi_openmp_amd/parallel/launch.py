@@ -9,8 +9,11 @@ image). Inside a rank, :func:`check_world` refuses a WORLD_SIZE that differs
 from the requested N.
 
 One-GPU rehearsal: with ``MPX_DIST_BACKEND=gloo`` several ranks may share a
-device (control plane over gloo, halos over IPC-mapped peer memory); every
-other GPU run needs N visible devices or fails with exit code 2.
+device (control plane over gloo, halos over IPC-mapped peer memory); with
+``MPX_DIST_CONTRACT=nccl`` they share it through the framework's RCCL code
+paths (``parallel/contract.py``); every other GPU run needs N usable devices
+or fails with exit code 2 — here, and again inside each rank
+(``parallel/dist.py``).
 
 The reference has no multi-process code at all; this is the
 north-star "1/2/4/8 MI355X" launch path.
@@ -41,25 +44,39 @@ def free_port() -> int:
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
 
-def _kfd_gpu_count(root: str = KFD_NODES) -> Optional[int]:
+DRI = "/dev/dri"
+
+
+def _kfd_gpu_count(root: str = KFD_NODES, dri: str = DRI) -> Optional[int]:
     """GPU agents in the KFD topology (nodes whose gfx_target_version is set;
-    CPU nodes report 0) — read from sysfs, no HIP runtime involved. None when
-    the topology is unreadable."""
+    CPU nodes report 0) that this process can actually open — read from sysfs,
+    no HIP runtime involved. Containers do not namespace sysfs, so a lease of
+    one render node still lists every GPU of the host: a node counts only when
+    its ``/dev/dri/renderD<drm_render_minor>`` is readable and writable here
+    (ADVICE r3). None when the topology is unreadable."""
     try:
         names = os.listdir(root)
     except OSError:
         return None
     n = 0
     for d in names:
+        props = {}
         try:
             with open(os.path.join(root, d, "properties")) as f:
                 for line in f:
                     k, _, v = line.partition(" ")
-                    if k == "gfx_target_version":
-                        n += int(v.strip() or 0) != 0
-                        break
-        except (OSError, ValueError):
+                    props[k] = v.strip()
+        except OSError:
             continue
+        try:
+            if int(props.get("gfx_target_version") or 0) == 0:
+                continue
+            minor = int(props.get("drm_render_minor", "-1"))
+        except ValueError:
+            continue
+        if minor >= 0 and not os.access(os.path.join(dri, f"renderD{minor}"), os.R_OK | os.W_OK):
+            continue
+        n += 1
     return n
 
 
@@ -98,7 +115,7 @@ def relaunch_if_needed(script: str, argv: Sequence[str], gpus: int, device: str)
     code (non-zero when N devices are not available)."""
     if in_rank_env() or gpus <= 1:
         return None
-    rehearsal = os.environ.get("MPX_DIST_BACKEND") == "gloo"
+    rehearsal = os.environ.get("MPX_DIST_BACKEND") == "gloo" or os.environ.get("MPX_DIST_CONTRACT") == "nccl"
     if device != "cpu" and not rehearsal:
         ndev = visible_devices()
         if device == "cuda" and ndev == 0:

@@ -221,6 +221,18 @@ def test_visible_devices_from_sysfs(tmp_path, monkeypatch):
         (d / "properties").write_text(f"cpu_cores_count 4\ngfx_target_version {ver}\nsimd_count 8\n")
     assert launch._kfd_gpu_count(str(tmp_path)) == 3
     assert launch._kfd_gpu_count(str(tmp_path / "missing")) is None
+    # sysfs lists every GPU of the host; only render nodes this
+    # process can open count (nodes 1 and 4 -> renderD128 / renderD131)
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for i, minor in ((1, 128), (2, 129), (4, 131)):
+        (tmp_path / str(i) / "properties").write_text(f"gfx_target_version 90500\ndrm_render_minor {minor}\n")
+    (dri / "renderD128").write_text("")
+    (dri / "renderD131").write_text("")
+    assert launch._kfd_gpu_count(str(tmp_path), str(dri)) == 2
+    (dri / "renderD131").chmod(0o000)
+    if not os.access(dri / "renderD131", os.R_OK):  # (root ignores the mode bits)
+        assert launch._kfd_gpu_count(str(tmp_path), str(dri)) == 1
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
     assert launch._visible_filter(3) == 2
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")

@@ -92,11 +92,11 @@ def plan(n: int, a, ndev: int) -> List[dict]:
     lacks = None if shared or n <= ndev else f"needs {n} GPUs, {ndev} visible"
     for halo in ("peer", "rccl"):
         skip = lacks
-        if n > 1 and halo == "rccl" and a.rehearse and not cpu:
+        if n > 1 and halo == "rccl" and a.rehearse and not cpu and not a.contract:
             skip = "RCCL refuses several ranks on one GPU (rehearsal uses peer halos)"
         if n == 1 and halo == "rccl":
             skip = "single rank: no halo transport"
-        if cpu and halo == "peer" and n > 1:
+        if cpu and halo == "peer" and n > 1:  # (also under --contract)
             skip = "peer halos need GPUs (IPC); the CPU run uses gloo send/recv"
         jobs.append({"name": f"conv/{halo}", "kind": "weak", "skip": skip,
                      "cmd": [py, "bench.py", "--gpus", str(n), "--halo", halo, "--no-cpu-baseline", *dev, *conv_sz]})
@@ -188,6 +188,9 @@ def main(argv=None) -> int:
     p.add_argument("--out", default="scaling")
     p.add_argument("--device", choices=["auto", "cpu"], default="auto")
     p.add_argument("--rehearse", action="store_true", help="ranks share the visible GPUs (gloo control plane)")
+    p.add_argument("--contract", action="store_true",
+                   help="with --rehearse: run the ranks through the framework's RCCL code paths under the nccl "
+                        "device contract (MPX_DIST_CONTRACT=nccl, parallel/contract.py) instead of plain gloo")
     p.add_argument("--quick", action="store_true", help="fewer steps per run")
     p.add_argument("--only", default="", help="run only jobs whose name contains this string")
     p.add_argument("--timeout", type=float, default=600.0, help="seconds per job")
@@ -198,7 +201,10 @@ def main(argv=None) -> int:
     ndev = 0 if a.device == "cpu" else visible_gpus()
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if a.device == "cpu" or a.rehearse:
+    if a.contract:
+        env["MPX_DIST_CONTRACT"] = "nccl"
+        env.pop("MPX_DIST_BACKEND", None)
+    elif a.device == "cpu" or a.rehearse:
         env["MPX_DIST_BACKEND"] = "gloo"
     rows: List[dict] = []
     with open(os.path.join(out, "scaling.log"), "w") as log:
