@@ -401,22 +401,26 @@ def settle(step_fn, chunk: int, warmup_ms: float, ctx, sync, watchdog, parallel,
     if warmup_ms <= 0:
         return {"steps": 0, "ms": 0.0}
     t0 = time.perf_counter()
-    for _ in range(chunk):
-        step_fn()
-    finish()
-    sync()
-    probe = (time.perf_counter() - t0) * 1e3 / chunk
-    rest = max(0, int(warmup_ms / max(probe, 1e-3)) + 1 - chunk)
-    rest = int(parallel.max_over_ranks(float(min(rest, 200000)), ctx))
-    for i in range(rest):
-        step_fn()
-        if i % 256 == 255:
-            watchdog.beat()
-    finish()
-    sync()
+    steps = 0
+    rest = chunk
+    for _ in range(16):  # rounds: each agrees across ranks on how many more steps to run
+        for i in range(rest):
+            step_fn()
+            if i % 256 == 255:
+                watchdog.beat()
+        steps += rest
+        finish()
+        sync()
+        elapsed = (time.perf_counter() - t0) * 1e3
+        need = parallel.max_over_ranks(warmup_ms - elapsed, ctx)
+        watchdog.beat()
+        if need <= 0:
+            break
+        per_step = elapsed / steps
+        # every rank must run the same count (halo sends / recvs stay matched)
+        rest = int(parallel.max_over_ranks(float(max(1, min(200000, int(need / max(per_step, 1e-3)) + 1))), ctx))
     ctx.barrier()
-    watchdog.beat()
-    return {"steps": chunk + rest, "ms": round((time.perf_counter() - t0) * 1e3, 2)}
+    return {"steps": steps, "ms": round((time.perf_counter() - t0) * 1e3, 2)}
 
 
 def cpu_baseline_ms(det, size: int, ops, runs: int = 5) -> dict:

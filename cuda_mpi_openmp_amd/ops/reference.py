@@ -73,14 +73,27 @@ def vsub(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return a.cpu() - b.cpu()
 
 
-def classify(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray) -> torch.Tensor:
+def classify_dist(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, device=None,
+                  chunk: int = 1 << 21) -> torch.Tensor:
+    """fp64 quadratic forms (p - mu_c)^T A_c (p - mu_c) of every pixel and class,
+    (N, C), computed in pixel chunks (an 8192^2 image x 32 classes would need
+    51 GB at once) on ``device`` (default: the CPU) with plain torch ops."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    p_all = img.reshape(-1, 4)[:, :3]
+    m = torch.as_tensor(mu, dtype=torch.float64, device=dev)
+    A = torch.as_tensor(inv, dtype=torch.float64, device=dev)
+    out = torch.empty((p_all.shape[0], m.shape[0]), dtype=torch.float64)
+    for s0 in range(0, p_all.shape[0], chunk):
+        p = p_all[s0:s0 + chunk].to(dev).to(torch.float64)
+        d = p[:, None, :] - m[None, :, :]  # (n, C, 3)
+        t = torch.einsum("ncj,cji->nci", d, A)
+        out[s0:s0 + chunk] = (t * d).sum(-1).cpu()
+    return out
+
+
+def classify(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, device=None) -> torch.Tensor:
     """fp64 direct quadratic forms, strict-< argmin (lowest class on ties), NaN -> 255."""
-    p = img.cpu()[..., :3].to(torch.float64).reshape(-1, 3)
-    m = torch.as_tensor(mu, dtype=torch.float64)
-    A = torch.as_tensor(inv, dtype=torch.float64)
-    d = p[:, None, :] - m[None, :, :]  # (N, C, 3)
-    t = torch.einsum("ncj,cji->nci", d, A)
-    dist = (t * d).sum(-1)
+    dist = classify_dist(img, mu, inv, device)
     # a class is a candidate only if dist < DBL_MAX (NaN and +inf never win)
     cand = dist < torch.finfo(torch.float64).max
     d2 = torch.where(cand, dist, torch.full_like(dist, float("inf")))

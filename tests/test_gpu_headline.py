@@ -86,3 +86,92 @@ def test_jacobi_sweep_2048x16384_fp64(gpu):
     ops.jacobi_sweep(ud, un, 1, rows + 1, res)
     assert torch.equal(un.cpu(), un_c)
     assert res.item() == r_cpu
+
+
+# ---------------------------------------------------------------------------
+# Independent oracles at the headline shapes: plain torch
+# fp32 (ops/reference.py: F.conv2d over the dense K x K window, one summation
+# order of its own) for every named filter, and torch fp64 quadratic forms for
+# lab3 — not the framework's own C reference.
+# ---------------------------------------------------------------------------
+from cuda_mpi_openmp_amd.ops import filters as _filters  # noqa: E402
+from cuda_mpi_openmp_amd.ops import reference as _ref  # noqa: E402
+
+# measured on these exact images (CPU native == GPU bit for bit): at most 154
+# +-1 pixels of 16.8 M for any filter / image (gauss5 separable vs its dense
+# oracle); the bound leaves 5x margin
+_MAX_OFF_BY_ONE = 800
+
+
+def _oracle_check(got: torch.Tensor, img: torch.Tensor, f) -> None:
+    exp = _ref.conv(img, f)
+    assert torch.equal(got[..., 3], exp[..., 3]), "alpha must pass through"
+    assert torch.equal(got[..., 0], got[..., 1]) and torch.equal(got[..., 0], got[..., 2])
+    d = (got[..., 0].to(torch.int16) - exp[..., 0].to(torch.int16)).abs()
+    assert int(d.max()) <= 1, f"{f.name}: gray level off by {int(d.max())}"
+    assert int((d == 1).sum()) <= _MAX_OFF_BY_ONE, f"{f.name}: {int((d == 1).sum())} pixels off by one"
+    if f.base_mode == _filters.MODE_MAG2:
+        # saturated (oracle magnitude >= 256) and zero gradients: exact
+        y = _ref.luma(img)
+        import torch.nn.functional as F
+
+        up, dn = f.anchor, f.k - 1 - f.anchor
+        yp = F.pad(y[None, None], (up, dn, up, dn), mode="replicate")
+        wx, wy = f.dense()
+        gx = F.conv2d(yp, torch.tensor(wx, dtype=torch.float32).reshape(1, 1, f.k, f.k))[0, 0]
+        gy = F.conv2d(yp, torch.tensor(wy, dtype=torch.float32).reshape(1, 1, f.k, f.k))[0, 0]
+        s = gx * gx + gy * gy
+        sure = (s >= 256.0 ** 2) | (s == 0)
+        assert torch.equal(got[..., 0][sure], exp[..., 0][sure]), f"{f.name}: saturated / zero gradient differs"
+
+
+@pytest.fixture(scope="module")
+def oracle_imgs(img4096):
+    sat = rand_img(4096, 4096, seed=23)
+    sat[..., :3] = (sat[..., :3] > 127).to(torch.uint8) * 255  # every channel 0 or 255: the v_med3 clamp ends
+    return {"random": img4096["random"], "smooth": img4096["smooth"], "saturated": sat}
+
+
+@pytest.mark.parametrize("kind", ["random", "smooth", "saturated"])
+@pytest.mark.parametrize("name", _filters.list_filters())
+def test_conv_4096_vs_torch_oracle(gpu, oracle_imgs, kind, name):
+    img = oracle_imgs[kind]
+    f = ops.get_filter(name)
+    _oracle_check(ops.conv(img.to(gpu), f).cpu(), img, f)
+
+
+def test_conv_4096_iterated_sobel5_vs_torch_oracle(gpu, img4096):
+    """A 20-step iterated sobel5 frame (mostly 0 / 255: the streaming bench's
+    frames) convolved once more, against the torch oracle."""
+    f = ops.get_filter("sobel5")
+    x = img4096["random"].to(gpu)
+    for _ in range(20):
+        x = ops.conv(x, f)
+    frame = x.cpu()
+    ext = ((frame[..., 0] == 0) | (frame[..., 0] == 255)).float().mean().item()
+    assert ext > 0.5, f"iterated frame not saturation-heavy ({ext:.2f})"
+    _oracle_check(ops.conv(x, f).cpu(), frame, f)
+
+
+def test_classify_8192_nc32_vs_torch_fp64_oracle(gpu, lab3_8192):
+    """8192^2, 32 classes, every GPU path against torch fp64 quadratic forms:
+    disagreements only where the two classes' distances are a near-tie."""
+    img, ref = lab3_8192
+    mu, inv, _ = ref[32]
+    px = img.reshape(-1, 4)
+    n, chunk = px.shape[0], 1 << 22
+    best = torch.empty(n, dtype=torch.uint8)
+    for s0 in range(0, n, chunk):  # torch ops on the GPU, no framework kernel
+        best[s0:s0 + chunk] = torch.argmin(_ref.classify_dist(px[s0:s0 + chunk], mu, inv, device=gpu), dim=1)
+    for path in ("fast", "mfma", "mfma64", "mfma8", "auto"):
+        d = img.to(gpu)
+        ops.classify_(d, mu, inv, path=path)
+        got = d.cpu()[..., 3].reshape(-1)
+        bad = (got != best).nonzero().flatten()
+        assert bad.numel() < 1e-4 * n, f"{path}: {bad.numel()} disagreements"
+        if bad.numel():
+            dist = _ref.classify_dist(px[bad], mu, inv, device=gpu)
+            dg = dist.gather(1, got[bad].long()[:, None])[:, 0]
+            db = dist.gather(1, best[bad].long()[:, None])[:, 0]
+            rel = ((dg - db).abs() / db.abs().clamp_min(1e-300)).max().item()
+            assert rel < 1e-9, f"{path}: a disagreement is not a near-tie (relative gap {rel:.3g})"
