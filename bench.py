@@ -341,8 +341,13 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     watchdog.beat()
     per_rank = parallel.all_gather_floats(mine, ctx)
     elapsed = max(per_rank)
-    for d in sdets:
-        d.check_stream()
+    # a device-side halo wait that gave up on ANY rank fails every rank here,
+    # before the gathers below (a rank raising alone would leave the others
+    # blocked in them until the watchdog fires: ADVICE r3)
+    bad = [d.stream_timed_out() for d in sdets]
+    if parallel.max_over_ranks(1.0 if any(bad) else 0.0, ctx) > 0:
+        raise RuntimeError(f"rank {ctx.rank}: streaming halo wait timed out during the timed steps "
+                           f"({'this rank' if any(bad) else 'on another rank'}; slabs {[i for i, b in enumerate(bad) if b]})")
     rec = {"value_streaming": _sig(n * args.size * args.size * args.steps / elapsed / 1e9),
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
            "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],

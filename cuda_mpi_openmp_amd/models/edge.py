@@ -278,9 +278,13 @@ class SlabEdgeDetector:
         self._sk = k
         return self.stream_out
 
+    def stream_timed_out(self) -> bool:
+        """True when a device-side halo wait of the streaming fetch gave up."""
+        return self.slink is not None and self.slink.timed_out()
+
     def check_stream(self) -> None:
         """Raise when a device-side halo wait of the streaming fetch gave up."""
-        if self.slink is not None and self.slink.timed_out():
+        if self.stream_timed_out():
             raise RuntimeError(f"rank {self.ctx.rank}: streaming halo wait timed out near step {self._sk}")
 
     def _step_pipelined(self) -> torch.Tensor:

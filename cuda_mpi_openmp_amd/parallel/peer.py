@@ -38,6 +38,17 @@ Fault injection (tests): ``MPX_PEER_INJECT=open_stall@R`` (rank R's IPC open
 never returns), ``verify_corrupt@R`` (R reports a wrong checksum),
 ``probe_corrupt@R`` (R writes a wrong probe pattern).
 
+Limitation of the open deadline: ``open_stall`` sleeps on the
+helper thread BEFORE it calls into HIP, so the tests show the vote and the
+RCCL fallback are time-bounded when an open is late, not when an open hangs
+INSIDE the runtime (as hipIpcOpenMemHandle did for one allocation above 2 GiB,
+``profiles/peer_setup.md``). A thread abandoned inside the runtime may hold
+HIP or driver locks, and the in-process fallback (closing the other mappings,
+RCCL initialisation) is then not shown to be bounded; the job watchdog
+(``parallel/fault.py``) still ends such a job. Every allocation these
+transports export stays below ``IPC_MAX_BYTES``, the size class that never
+hung; a job that does hit an open timeout can be re-run with ``--halo rccl``.
+
 Reference: no multi-GPU code exists there; the decomposition is
 the BASELINE north star.
 """

@@ -28,7 +28,8 @@ struct RowSrc {
 //   FAST: hardware v_sqrt_f32 (not correctly rounded) decides the integer part
 //   whenever its result is further than kSqrtMargin from an integer; otherwise
 //   (and only then) the correctly rounded sqrtf runs. tests/test_gpu_kernels.py
-//   checks the equivalence exhaustively for every float s in [0, 65025].
+//   checks the equivalence exhaustively for every float s in [0, 65025], and
+//   the paired production form below (mag2_to_gray) for every float in [0, +inf].
 constexpr float kSqrtMargin = 1.0f / 16384.0f;  // 2^-14 = 4 ulp at 255
 
 template <bool FAST>

@@ -27,10 +27,16 @@ constexpr int kCpolSystem = 1 | 16;              // gfx950 cache policy SC0 | SC
 constexpr uint32_t kSpinDefault = 1u << 22;     // polls (s_sleep 4 each): seconds, not minutes
 
 // Wait until *flag >= target; false (and *err = 1) when the wait gave up.
+// Once any wait of this rank has given up (*err set), later waits return
+// false at once (checked on entry and every 1024 polls) instead of spinning
+// their full limit each — a stalled neighbour costs one timeout, not one per
+// remaining step.
 __device__ __forceinline__ bool wait_at_least(const uint32_t *flag, uint32_t target, uint32_t *err, uint32_t limit) {
     uint32_t spins = 0;
     const uint32_t lim = limit ? limit : kSpinDefault;
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+        if ((spins & 1023u) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+            return false;
         if (++spins > lim) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return false;

@@ -14,14 +14,25 @@ namespace {
 // Exhaustive self-test of the fast magnitude path: every float s in
 // [0, 65025] (bit patterns 0 .. 0x477E0100) must map to the same gray level as
 // the correctly rounded sqrtf. Counts mismatches into *bad.
-// raw = 0: the production fast path (v_sqrt + fract margin + exact fallback);
-// raw = 1: bare truncation of v_sqrt_f32 with no margin test at all.
+// raw = 0: the single-pixel fast path (v_sqrt + fract margin + exact fallback);
+// raw = 1: bare truncation of v_sqrt_f32 with no margin test at all;
+// raw = 2: the paired production path of the band / wave kernels
+// (mag2_to_gray: v_med3 clamp into [0.5^2, 255.5^2], margin test on both
+// lanes, one exact fallback for the pair) — lane pairs (s, s') with s' walking
+// the range backwards, so every value meets fast and fallback partners.
 __global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigned long long *bad, int raw) {
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long nbad = 0;
     for (uint32_t u = first + blockIdx.x * blockDim.x + threadIdx.x; u <= last && u >= first; u += stride) {
         const float s = __builtin_bit_cast(float, u);
         const uint32_t exact = edge::mag_to_gray<false>(s);
+        if (raw == 2) {
+            const float s1 = __builtin_bit_cast(float, last - (u - first));
+            uint32_t g0, g1;
+            edge::mag2_to_gray(s, s1, g0, g1);
+            nbad += (g0 != exact) + (g1 != edge::mag_to_gray<false>(s1));
+            continue;
+        }
         const uint32_t fast = raw ? (uint32_t)__builtin_amdgcn_sqrtf(fminf(s, 65025.0f)) : edge::mag_to_gray<true>(s);
         nbad += fast != exact;
     }
@@ -360,8 +371,10 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
 extern "C" int mpx_selftest_fast_sqrt(unsigned long long *bad_device, int raw, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(bad_device, "null counter");
+    // raw 0 / 1: every float in [0, 65025] (255^2); raw 2: every float in
+    // [0, +inf] (a squared magnitude is never NaN)
     hipLaunchKernelGGL(fast_sqrt_selftest_kernel, dim3(kNumCUs * 16), dim3(256), 0, as_stream(stream), 0u,
-                       0x477E0100u, bad_device, raw);
+                       raw == 2 ? 0x7F800000u : 0x477E0100u, bad_device, raw);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }
