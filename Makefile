@@ -56,7 +56,7 @@ $(B)/k_%.o: native/src/kernels/%.hip $(HDRS) | $(B)
 
 # the lab2 kernels keep scalar v_fmac chains: SLP packing into v_pk_fma_f32 costs
 # hazard NOPs and ~40 VGPRs (8 -> 4 waves per SIMD) for no extra FLOP rate
-$(B)/k_edge.o $(B)/k_edge_roberts.o $(B)/t_edge_variants.o: HIPFLAGS += -fno-slp-vectorize
+$(B)/k_edge.o $(B)/k_edge_roberts.o $(B)/k_edge_stream.o $(B)/t_edge_variants.o: HIPFLAGS += -fno-slp-vectorize
 # MFMA accumulators straight into VGPRs (unified file on gfx950): no v_accvgpr_read per result
 $(B)/k_classify.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 

@@ -107,6 +107,9 @@ _SIGNATURES = {
     "mpx_rows_checksum": (c_int, [c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp]),
     "mpx_peer_probe_run": (c_int, [c_vp, c_vp]),
     "mpx_halo_fetch_run": (c_int, [c_vp, c_vp]),
+    "mpx_conv_stream_peer_ok": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "mpx_conv_stream_peer_run": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp,
+                                         _fp, c_vp, c_vp]),
     "mpx_sync_alloc": (c_int, [c_i64, ctypes.POINTER(c_vp), _ip]),
     "mpx_sync_free": (c_int, [c_vp]),
     "mpx_sync_write": (c_int, [c_vp, c_int, ctypes.c_uint]),

@@ -73,9 +73,10 @@ class SlabEdgeDetector:
 
     ``halo`` selects the transport of the halo rows:
 
-    * ``"peer"``: one-sided — the neighbours' slabs are IPC-mapped once and the
-      convolution kernel reads their boundary rows over xGMI on every step
-      (``parallel.peer``); no exchange kernel, one launch per step;
+    * ``"peer"``: one-sided — the neighbours' mailboxes (their boundary rows,
+      copied there when the slab is loaded) are IPC-mapped once and the
+      convolution kernel reads them over xGMI on every step (``parallel.peer``);
+      no exchange kernel, one launch per step;
     * ``"rccl"``: two-sided send/recv (native RCCL tier, else torch.distributed),
       arranged by ``overlap``;
     * ``"auto"``: ``"peer"`` when every rank can map and verify its neighbours,
@@ -85,11 +86,12 @@ class SlabEdgeDetector:
     reads are new each step (a real inter-rank dependency): the
     filter is iterated — step k convolves step k-1's output — over two
     ping-pong input buffers. Step k's halo rows come from the neighbours'
-    step k-1 output, via a device-signalled fetch kernel (``peer``: publish the
-    step, wait for the neighbours to reach it, copy their boundary rows over
-    xGMI; ``parallel.peer.StreamHaloLink``) or an in-order RCCL send/recv
-    (``rccl``). Results equal a one-device run of the same frame sequence
-    on the whole image.
+    step k-1 output, via the mailboxes (``peer``, ``parallel.peer.
+    StreamHaloLink``: fused into the band kernel — one launch per step, only
+    the slab-edge waves wait on the neighbours and publish the step — or, for
+    shapes the band kernel does not take, a device-signalled fetch kernel
+    before the conv) or an in-order RCCL send/recv (``rccl``). Results equal a
+    one-device run of the same frame sequence on the whole image.
     """
 
     def __init__(self, ctx: DistContext, global_h: int, w: int, filt: str | Filter = "sobel5",
@@ -136,7 +138,7 @@ class SlabEdgeDetector:
             if halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
                 from ..parallel.peer import try_stream_halo
 
-                self.slink = try_stream_halo(ctx, s, self.bufs)
+                self.slink = try_stream_halo(ctx, s, self.bufs, self.filter)
                 if self.slink is None and halo == "peer":
                     raise RuntimeError("streaming peer halo transport unavailable (IPC mapping or probe failed)")
         elif halo != "rccl" and ctx.world > 1 and dev.type == "cuda":
@@ -184,16 +186,21 @@ class SlabEdgeDetector:
         if not self.ctx.is_distributed:
             return "none"
         if self.slink is not None:
-            return "xgmi-peer-signalled-fetch"
+            return "xgmi-peer-fused" if self.slink.fused else "xgmi-peer-signalled-fetch"
         if self.peer is not None:
             return "xgmi-peer"
         return "native-rccl" if self.ctx.native is not None else "torch.distributed"
 
     def halo_filled(self) -> torch.Tensor:
         """The input buffer with its halo rows as the last step read them
-        (peer mode copies them in from the neighbours' slabs first)."""
+        (peer modes copy them in from the neighbours' mailboxes first; the
+        fused streaming form after every rank finished its steps)."""
         if self.peer is not None:
             self.peer.pull(self.bufs[0])
+        if self.slink is not None and self.slink.fused and self._sk:
+            torch.cuda.synchronize(self.bufs[0].device)
+            self.ctx.barrier()
+            self.slink.pull(self._sk - 1)
         return self.buf
 
     def _publish(self) -> None:
@@ -270,6 +277,10 @@ class SlabEdgeDetector:
         a = (k - 1) % 2
         st = torch.cuda.current_stream(self.bufs[0].device).cuda_stream if self.bufs[0].is_cuda else None
         if self.ctx.is_distributed:
+            if self.slink is not None and self.slink.fused:
+                self.slink.conv(k, st)            # ONE launch: the edge waves carry the halo protocol
+                self._sk = k
+                return self.stream_out
             if self.slink is not None:
                 self.slink.fetch(k, st)           # device-ordered: no host round trip
             else:
@@ -320,8 +331,7 @@ class SlabEdgeDetector:
             self.slink.close()
             self.slink = None
         if self.peer is not None:
-            torch.cuda.synchronize(self.out.device)
-            self.peer.close()
+            self.peer.close(collective=True)
             self.peer = None
 
     def finish(self) -> None:

@@ -7,10 +7,12 @@ form.
 Halo transports (``halo=``):
 
 * ``"peer"`` (GPU, default when available): one-sided and device-signalled.
-  Each rank IPC-maps its neighbours' u/u_new buffers and completed-iteration
-  words once; every iteration is ONE sweep kernel whose slab-edge waves wait
-  on the neighbours' counters, read their boundary rows over xGMI and publish
-  this rank's counter (native/src/kernels/jacobi.hip, ``parallel.peer.
+  Each rank IPC-maps its neighbours' mailboxes (completed-iteration word and
+  two parity slots of their edge rows; the slabs are never shared, so they
+  may be any size) once; every iteration is ONE sweep kernel whose slab-edge
+  waves wait on the neighbours' counters, read their edge rows over xGMI,
+  write this rank's new edge rows write-through into its mailbox and publish
+  its counter (native/src/kernels/jacobi.hip, ``parallel.peer.
   JacobiPeerLink``). No exchange kernel, no host round trip per iteration.
 * ``"rccl"``: two-sided send/recv of the edge rows (below).
 
@@ -72,18 +74,17 @@ class SlabJacobi:
             self.overlap = False
         self.peer = None
         if halo not in ("rccl", "none") and ctx.is_distributed and dev.type == "cuda":
-            # two allocations (buffer 0, buffer 1), each shared by IPC; the
-            # iteration words live in a separate sync block (parallel.peer.SyncBlock)
+            # only a small mailbox per rank is IPC-shared (its iteration word and
+            # two parity slots of its edge rows: parallel.peer.Mailbox), so the
+            # u / u_new slabs may be any size
             from ..parallel.peer import try_jacobi_peer
 
-            nel = shape[0] * shape[1]
-            self._storages = [torch.zeros(nel, dtype=dtype, device=dev), torch.zeros(nel, dtype=dtype, device=dev)]
-            self.u = self._storages[0].view(shape)
-            self.un = self._storages[1].view(shape)
+            self.u = torch.zeros(shape, dtype=dtype, device=dev)
+            self.un = torch.zeros(shape, dtype=dtype, device=dev)
             es = self.u.element_size()
             nv = 16 // es
             layout_ok = cols % nv == 0 and self.u.data_ptr() % 16 == 0 and self.un.data_ptr() % 16 == 0
-            self.peer = try_jacobi_peer(ctx, self.slab, self._storages, [self.u, self.un], layout_ok)
+            self.peer = try_jacobi_peer(ctx, self.slab, [self.u, self.un], layout_ok)
             if self.peer is None and halo == "peer":
                 raise RuntimeError("peer halo transport unavailable (IPC mapping failed or cols not a multiple of "
                                    f"{nv})")
@@ -184,8 +185,8 @@ class SlabJacobi:
         corrupt = _fault_hook(self.ctx.rank, self.iteration)
         if not self._halos_valid:
             self.sync_halos()
-        if corrupt:  # injected silent error: one halo value off by one (peer mode: the
-            # edge row the neighbour reads, since the kernel reads its halo in place)
+        if corrupt:  # injected silent error: one value off by one (peer mode: this
+            # rank's first owned row, the one its upper neighbour's halo comes from)
             row = 1 if self.peer is not None else 0 if self.slab.has_up else self.slab.rows + 1
             self.u[row, self.cols // 2] += 1.0
         track = (self.iteration + 1) % self.check_every == 0
@@ -306,10 +307,10 @@ class SlabJacobi:
         return path
 
     def close(self) -> None:
-        """Unmap the neighbours' buffers (peer mode)."""
+        """Collective in peer mode: unmap the neighbours' mailboxes and free this
+        rank's once no rank can still be reading it."""
         if self.peer is not None:
-            torch.cuda.synchronize(self.u.device)
-            self.peer.close()
+            self.peer.close(collective=True)
             self.peer = None
 
     def load_checkpoint(self, prefix: str) -> None:

@@ -116,8 +116,8 @@ class ConvLauncher:
     def __init__(self, src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
                  oy0: int, oy1: int, y_lo: int, y_hi: int, peer=None):
         """``peer``: a ``parallel.PeerHalo`` — rows outside [0, own rows) are then
-        read from the neighbours' IPC-mapped slabs (``mpx_conv_peer``) instead
-        of ``src``'s resident halo rows."""
+        read from the neighbours' IPC-mapped mailboxes (``mpx_conv_peer``)
+        instead of ``src``'s resident halo rows."""
         self.args = _conv_args(src, out, filt, src_row0, out_row0, oy0, oy1, y_lo, y_hi)
         self.empty = oy1 <= oy0
         self.cuda = src.is_cuda

@@ -196,11 +196,15 @@ typedef struct mpx_peer_probe {
     unsigned int spin_limit;
 } mpx_peer_probe;
 int mpx_peer_probe_run(const mpx_peer_probe *p, void *stream);
-/* Streaming halo fetch: publish sync[0] = step (release), then per side s with a
- * neighbour (flag[s] != NULL): wait flag[s] >= step (bounded), and when src[s]
- * is set copy bytes[s] from it (its boundary rows, system-scope loads) to dst[s]
- * (this rank's halo rows). A side without rows to copy still waits: the
- * neighbour reads this rank's rows (write-after-read order). */
+/* Streaming halo fetch (filters the fused band kernel does not cover): block s
+ * first copies this rank's own boundary rows own_src[s] into its mailbox rows
+ * mb_dst[s] (mb_bytes[s], system-scope write-through stores); once BOTH blocks'
+ * copies are acknowledged the later one publishes sync[0] = step (release).
+ * Then per side s with a neighbour (flag[s] != NULL): wait flag[s] >= step
+ * (bounded), and when src[s] is set copy bytes[s] from it (the neighbour's
+ * mailbox rows, system-scope loads) to dst[s] (this rank's halo rows). A side
+ * without rows to copy still waits: the neighbour reads this rank's mailbox
+ * (write-after-read order). */
 typedef struct mpx_halo_fetch {
     const void *src[2];
     void *dst[2];
@@ -209,8 +213,43 @@ typedef struct mpx_halo_fetch {
     unsigned int *sync;
     unsigned int step;
     unsigned int spin_limit;
+    const void *own_src[2];
+    void *mb_dst[2];
+    int64_t mb_bytes[2];
 } mpx_halo_fetch;
 int mpx_halo_fetch_run(const mpx_halo_fetch *f, void *stream);
+/* Streaming convolution with the halo exchange fused into the band kernel (one
+ * launch per step, no fetch kernel): the waves whose rows touch the slab edges
+ * read their halo rows straight from the neighbours' mailboxes (system-scope
+ * loads) after a bounded wait on the neighbour's step word, write their first
+ * n_first / last n_last output rows into this rank's mailbox as well
+ * (write-through), and the last of the n_edge edge waves publishes the step;
+ * interior waves never wait. The step index c = this rank's sync[0] (completed
+ * steps, read on the device): the halo rows come from slot c & 1 of the
+ * neighbours' mailboxes, the output rows go to slot (c + 1) & 1 of this one.
+ * up_src[p] / dn_src[p]: biased row-source pointers (logical row g < 0 at
+ * up_src[p] + g * w, g >= own_rows at dn_src[p] + g * w); NULL flag = global
+ * edge (the clamp rows then come from `in` itself). Requires the band kernel:
+ * k <= 5 with at most two columns of reach per side, w % 4 == 0, pitch == w,
+ * 16-byte aligned rows. */
+typedef struct mpx_conv_stream_peer {
+    const uint32_t *up_src[2];
+    const uint32_t *dn_src[2];
+    const unsigned int *up_flag;
+    const unsigned int *dn_flag;
+    uint32_t *mb_first[2];
+    uint32_t *mb_last[2];
+    unsigned int *sync;
+    int n_first;
+    int n_last;
+    int n_edge; /* filled in by the launcher */
+    unsigned int spin_limit;
+} mpx_conv_stream_peer;
+int mpx_conv_stream_peer_run(const uint32_t *in, uint32_t *out, int w, int pitch, int own_rows, int y_lo, int y_hi,
+                         int k, int anchor, int mode, const float *wx, const float *wy,
+                         const mpx_conv_stream_peer *sp, void *stream);
+/* 1 when mpx_conv_stream_peer can run this launch shape, else 0 */
+int mpx_conv_stream_peer_ok(int w, int pitch, int own_rows, int k, int anchor, int mode);
 /* IPC-exportable sync block: uncached (kind 2), fine-grained (1) or coarse (0) memory, zeroed */
 int mpx_sync_alloc(int64_t bytes, void **ptr, int *kind);
 int mpx_sync_free(void *ptr);
@@ -232,9 +271,11 @@ int mpx_sync_clear(unsigned int *sync, int64_t bytes);
 /* One-sided, device-signalled halo sweep of a whole slab (rows 1..rows of a
  * (rows + 2) x pitch buffer): the halo rows are read from the neighbours'
  * IPC-mapped buffers, ordered by completed-iteration counters (see jacobi.hip).
- * up_row[k] / dn_row[k]: the neighbour's last / first owned row in the buffer
- * that is its u at even (k = 0) / odd (k = 1) iterations; NULL (with a NULL
- * flag) at the global boundary, where the local halo row is the boundary row.
+ * up_row[k] / dn_row[k]: the neighbour's last / first owned row of u at even
+ * (k = 0) / odd (k = 1) iterations — rows of its MAILBOX (a small exported
+ * allocation, so slabs of any size keep the one-sided transport), or of its
+ * slab buffers when mb_first / mb_last are NULL; NULL (with a NULL flag) at
+ * the global boundary, where the local halo row is the boundary row.
  * sync: this rank's mpx_jacobi_sync_bytes() block; word 0 = completed
  * iterations (the neighbours' *_flag points at theirs), word 64 != 0 after a
  * bounded wait gave up. */
@@ -245,6 +286,12 @@ typedef struct mpx_jacobi_peer {
     const unsigned int *dn_flag;
     unsigned int *sync;
     unsigned int spin_limit; /* polls before a wait gives up (0 = default, ~seconds) */
+    /* this rank's mailbox rows (one row each; slot p receives the edge row of
+     * u^(t) for t % 2 == p, written during sweep t - 1 with write-through
+     * stores): mb_first = its first owned row (read by the upper neighbour),
+     * mb_last = its last (read by the lower one); NULL at a global edge */
+    void *mb_first[2];
+    void *mb_last[2];
 } mpx_jacobi_peer;
 int mpx_jacobi_sync_bytes(void);
 int mpx_jacobi_peer_sweep(int fp64, void *u, void *un, int cols, int pitch, int rows, void *resid,

@@ -33,12 +33,14 @@ const void *module_anchor_classify();
 const void *module_anchor_edge();
 const void *module_anchor_edge_roberts();
 const void *module_anchor_sort();
+const void *module_anchor_edge_stream();
 }  // namespace mpx
 
 extern "C" int mpx_preload_modules(void) {
     const void *anchors[] = {mpx::module_anchor_vsub(),         mpx::module_anchor_jacobi(),
                              mpx::module_anchor_classify(),     mpx::module_anchor_edge(),
-                             mpx::module_anchor_edge_roberts(), mpx::module_anchor_sort()};
+                             mpx::module_anchor_edge_roberts(), mpx::module_anchor_sort(),
+                             mpx::module_anchor_edge_stream()};
     for (const void *k : anchors) {
         hipFuncAttributes attr;
         MPX_RETURN_IF_HIP_ERROR(hipFuncGetAttributes(&attr, k));

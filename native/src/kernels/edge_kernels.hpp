@@ -5,6 +5,7 @@
 #include <type_traits>
 
 #include "internal.hpp"
+#include "peer_sync.hpp"
 
 namespace mpx {
 namespace edge {
@@ -808,10 +809,16 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
 // ---------------------------------------------------------------------------
 // One wave's segment walk in one direction (UP: bottom row first), prologue
 // included, so nothing but scalars is live across the direction branch.
-template <int K, int A, int MODE, bool FAST, class F, bool UP, int OPT>
+// SPW (fused streaming halo, mpx_conv_stream_peer): an edge wave's walk — every
+// row loads at system scope (the neighbours' mailbox rows change every step),
+// and output rows 0 .. nf-1 / own_rows-nl .. own_rows-1 are also stored
+// write-through into this rank's mailbox rows mbf / mbl (one extra store per
+// row, dropped by the buffer bounds check on the other rows: no branch).
+template <int K, int A, int MODE, bool FAST, class F, bool UP, int OPT, bool SPW = false>
 __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                      int w, int pitch, int ys, int ye, int y_lo, int y_hi, int x0,
-                                                     const Taps &taps, RowSrc rs) {
+                                                     const Taps &taps, RowSrc rs, uint32_t *mbf = nullptr,
+                                                     uint32_t *mbl = nullptr, int nf = 0, int nl = 0) {
     constexpr int R = K - 1 - A;
     constexpr int NV = 4 + A + R;
     constexpr bool TWO = (MODE == MPX_CONV_MAG2);
@@ -856,7 +863,10 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
         // non-temporal; bit 6: every row does (probes)
-        if constexpr (HL) {  // no aprons
+        if constexpr (SPW) {  // fused streaming edge walk: mailbox rows change every step
+            q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, peer::kCpolSystem);
+            ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ao, 0, peer::kCpolSystem);
+        } else if constexpr (HL) {  // no aprons
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 0);
             ap = u32x2_t{0u, 0u};
         } else if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
@@ -1019,6 +1029,14 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const __amdgpu_buffer_rsrc_t orow =
             __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(o, orow, st ? cin * 4 : kDrop, 0, (OPT & 2) ? 2 : 0);
+        if constexpr (SPW) {
+            const int own = rs.own_rows;
+            const bool mf = mbf != nullptr && y < nf, ml = mbl != nullptr && y >= own - nl;  // wave-uniform
+            uint32_t *mrow = mf ? mbf + (int64_t)y * w : (ml ? mbl + (int64_t)(y - (own - nl)) * w : out);
+            const __amdgpu_buffer_rsrc_t mr =
+                __builtin_amdgcn_make_buffer_rsrc(mrow, 0, (row_ok && (mf || ml)) ? w * 4 : 0, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(o, mr, st ? cin * 4 : kDrop, 0, peer::kCpolSystem);
+        }
     };
     const int nrows = ye - ys;
     const int nfull = nrows / D;
@@ -1044,11 +1062,11 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // loads plain under bit 5 / 6, bit 3 one batched apron load per walk (walks of
 // at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
 // lanes instead of aprons.
-template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
+template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                                                          int seg, int nwaves, int strips, int alt, Taps taps,
-                                                         RowSrc rs) {
+                                                         RowSrc rs, mpx_conv_stream_peer sp) {
     static_assert(A <= 2 && K - 1 - A <= 2, "apron covers two columns on each side");
     constexpr int WPB = (OPT & 4) ? 16 : 4;
     const int gw = xcd_remap(blockIdx.x, gridDim.x) * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1063,6 +1081,44 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
     const int ys = oy0 + sg * seg;
     const int ye = min(ys + seg, oy1);
     constexpr int SW = (OPT & 512) ? 248 : 256;  // output columns per strip
+    if constexpr (SP) {
+        // fused streaming halo: a wave whose rows touch a slab edge that has a
+        // neighbour (reads its rows, or writes rows it reads) is an edge wave
+        constexpr int R = K - 1 - A;
+        const bool top = sp.up_flag != nullptr && (ys - A < 0 || ys < sp.n_first);
+        const bool bot = sp.dn_flag != nullptr && (ye - 1 + R >= rs.own_rows || ye > rs.own_rows - sp.n_last);
+        if (top || bot) {  // wave-uniform
+            // completed steps of this rank = the index of this step (bumped only after
+            // every edge wave of the step has finished: no edge wave reads it bumped)
+            const uint32_t c = __hip_atomic_load(sp.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a neighbour at >= c finished its step c - 1: its output frame c is in its
+            // mailbox slot c & 1 (read-after-write), and it no longer reads this
+            // rank's slot (c + 1) & 1, which this step overwrites (write-after-read)
+            if (top) peer::wait_at_least(sp.up_flag, c, sp.sync + 64, sp.spin_limit);
+            if (bot) peer::wait_at_least(sp.dn_flag, c, sp.sync + 64, sp.spin_limit);
+            if (sp.up_flag) rs.up = sp.up_src[c & 1u];
+            if (sp.dn_flag) rs.dn = sp.dn_src[c & 1u];
+            uint32_t *mbf = top ? sp.mb_first[(c + 1) & 1u] : nullptr;
+            uint32_t *mbl = bot ? sp.mb_last[(c + 1) & 1u] : nullptr;
+            if ((alt & 1) && (sg & 1))
+                band4_walk<K, A, MODE, FAST, F, true, OPT, true>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW,
+                                                                 taps, rs, mbf, mbl, sp.n_first, sp.n_last);
+            else
+                band4_walk<K, A, MODE, FAST, F, false, OPT, true>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW,
+                                                                  taps, rs, mbf, mbl, sp.n_first, sp.n_last);
+            // every write-through store of this wave acknowledged, then count the
+            // wave; the last edge wave of the step publishes c + 1 (release)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((threadIdx.x & 63) == 0) {
+                const uint32_t n = __hip_atomic_fetch_add(sp.sync + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n + 1 == (uint32_t)sp.n_edge) {
+                    __hip_atomic_store(sp.sync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    peer::publish(sp.sync, c + 1);
+                }
+            }
+            return;
+        }
+    }
     if ((alt & 1) && (sg & 1))  // wave-uniform: odd segments walk up
         band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
     else

@@ -119,14 +119,16 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
 // (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
 // 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
 inline constexpr int kBand4PerSimd = 4;
-template <int K, int A, int MODE, bool FAST, class F, int OPT = 0>
+// SP: the fused streaming-halo form (mpx_conv_stream_peer_run; *sp required, its
+// n_edge filled in here).
+template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                  const Taps &taps, hipStream_t s, int seg, edge::RowSrc rs, int per_simd = kBand4PerSimd,
-                 int alt = 1) {
+                 int alt = 1, mpx_conv_stream_peer *sp = nullptr) {
     MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
     if (!rs.up) rs.up = in;
     if (!rs.dn) rs.dn = in;
-    if (rs.up != in || rs.dn != in) alt |= 2;  // remote halo rows: boundary segments first
+    if (rs.up != in || rs.dn != in || SP) alt |= 2;  // remote halo rows: boundary segments first
     const int strips = (OPT & 512) ? (w + 247) / 248 : (w + 255) / 256;
     if (seg <= 0) {
         const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
@@ -138,9 +140,23 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
     constexpr int wpb = (OPT & 4) ? 16 : 4;
-    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT>), dim3((unsigned)((nwaves + wpb - 1) / wpb)),
+    mpx_conv_stream_peer desc{};
+    if constexpr (SP) {
+        MPX_CHECK_ARG(sp && sp->sync && oy0 == 0 && oy1 == rs.own_rows, "fused streaming halo: whole slab, sync block");
+        // edge waves (conv_band4_kernel<SP>): segments touching an edge that has a neighbour
+        constexpr int R = K - 1 - A;
+        int nseg = 0;
+        for (int g = 0; g < segs; ++g) {
+            const int ys = oy0 + g * seg, ye = std::min(ys + seg, oy1);
+            nseg += (sp->up_flag && (ys - A < 0 || ys < sp->n_first)) ||
+                    (sp->dn_flag && (ye - 1 + R >= rs.own_rows || ye > rs.own_rows - sp->n_last));
+        }
+        sp->n_edge = nseg * strips;
+        desc = *sp;
+    }
+    hipLaunchKernelGGL((edge::conv_band4_kernel<K, A, MODE, FAST, F, OPT, SP>), dim3((unsigned)((nwaves + wpb - 1) / wpb)),
                        dim3(64 * wpb), 0,
-                       s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs);
+                       s, in, out, w, pitch, oy0, oy1, y_lo, y_hi, seg, (int)nwaves, strips, alt, taps, rs, desc);
     return MPX_OK;
 }
 

@@ -257,6 +257,8 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
         const T *base = u + (int64_t)cvc * NV;
         const bool edge = PEER && (rb == 0 || i1 == r1);
         const T *up_row = nullptr, *dn_row = nullptr;
+        T *mbf = nullptr, *mbl = nullptr;  // this sweep's mailbox rows (slot of u^(it+1))
+        const bool mbx = PEER && (pr.mb_first[0] != nullptr || pr.mb_last[0] != nullptr);
         uint32_t it = 0;
         if constexpr (PEER) {
             if (edge) {
@@ -271,6 +273,10 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
                     peer::wait_at_least(pr.dn_flag, it, pr.sync + kSyncErr, pr.spin_limit);
                     dn_row = static_cast<const T *>(pr.dn_row[it & 1u]) + (int64_t)cvc * NV;
                 }
+                // the waits above also order the mailbox writes: a neighbour at >= it
+                // has finished sweep it - 1, the last reader of slot (it + 1) & 1
+                if (rb == 0) mbf = static_cast<T *>(pr.mb_first[(it + 1) & 1u]);
+                if (i1 == r1) mbl = static_cast<T *>(pr.mb_last[(it + 1) & 1u]);
             }
         }
         auto ld = [&](int i) {
@@ -342,11 +348,28 @@ __global__ __launch_bounds__(64 * WPB) void jacobi_wave_kernel(const T *__restri
                 const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
                     un + (int64_t)(UPW ? max(r, i0) : min(r, i1 - 1)) * pitch, 0, cols * (int)sizeof(T), 0x00020000);
                 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                if (PEER && edge && (r == r0 || r == r1 - 1))  // a row the neighbours read: write through
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0,
-                                                           kCpolSystem);
-                else
+                if constexpr (PEER) {
+                    // mailbox mode: every row stores to un with the sweep's policy, and
+                    // a second, write-through store copies the two edge rows into this
+                    // rank's mailbox slot for u^(it+1) (dropped — out-of-range offset —
+                    // everywhere else: two stores per row on every path, so the wait
+                    // counts stay exact without a branch); slab mode (no mailbox): the
+                    // edge rows themselves are stored write-through
+                    const bool first = edge && r == r0 && mbf != nullptr;
+                    const bool last = edge && r == r1 - 1 && mbl != nullptr;
+                    if (!mbx && edge && (r == r0 || r == r1 - 1))
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0,
+                                                               kCpolSystem);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0,
+                                                               AUX);
+                    const __amdgpu_buffer_rsrc_t mrow = __builtin_amdgcn_make_buffer_rsrc(
+                        first ? mbf : (last ? mbl : un), 0, (first || last) ? cols * (int)sizeof(T) : 0, 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), mrow,
+                                                           (rok && (first || last)) ? soff : kDrop, 0, kCpolSystem);
+                } else {
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, res), orow, rok ? soff : kDrop, 0, AUX);
+                }
                 // keep each step's prefetch at its start: the scheduler otherwise sinks
                 // loads past the next step's use and the wait counts collapse to 0
                 __builtin_amdgcn_sched_barrier(0);
@@ -471,8 +494,13 @@ int launch_jacobi_peer(const T *u, T *un, int cols, int pitch, int rows, T *resi
     constexpr int NV = JVec<T>::n;
     MPX_CHECK_ARG(pitch % NV == 0 && cols % NV == 0 && aligned16(u) && aligned16(un),
                   "peer halos need the 16-byte vector layout (cols and pitch multiples of the vector width)");
-    for (const void *q : {pr.up_row[0], pr.up_row[1], pr.dn_row[0], pr.dn_row[1]})
-        MPX_CHECK_ARG(!q || aligned16(q), "neighbour rows must be 16-byte aligned");
+    for (const void *q : {pr.up_row[0], pr.up_row[1], pr.dn_row[0], pr.dn_row[1], (const void *)pr.mb_first[0],
+                          (const void *)pr.mb_first[1], (const void *)pr.mb_last[0], (const void *)pr.mb_last[1]})
+        MPX_CHECK_ARG(!q || aligned16(q), "neighbour and mailbox rows must be 16-byte aligned");
+    MPX_CHECK_ARG(!pr.mb_first[0] == !pr.mb_first[1] && !pr.mb_last[0] == !pr.mb_last[1],
+                  "mailbox rows come in slot pairs");
+    MPX_CHECK_ARG((!pr.mb_first[0] || pr.up_flag) && (!pr.mb_last[0] || pr.dn_flag),
+                  "a mailbox side needs the neighbour that reads it");
     const int strips = (cols / NV + kStripVec - 1) / kStripVec;
     int R = kJacobiRows;
     while (R > 1 && (int64_t)strips * ((rows + R - 1) / R) < 16384) R >>= 1;

@@ -11,12 +11,19 @@
 //    path, publishes a counter with the production release, and reads its
 //    neighbours' rows after the production wait — on real xGMI links before
 //    any timed or verified work trusts them (mismatch or timeout -> RCCL);
-//  * mpx_halo_fetch — the streaming convolution's halo exchange: publish this
-//    rank's step, wait (bounded) for each neighbour to reach it (read-after-
-//    write on the rows this rank copies, write-after-read on the rows the
-//    neighbour copies from this rank), copy their boundary rows into the local
-//    halo rows with system-scope loads. One tiny launch per step, no RCCL
-//    kernel, no host round trip.
+//  * mpx_halo_fetch — the streaming convolution's halo exchange for filters the
+//    fused band kernel (edge_stream.hip) does not cover: copy this rank's
+//    boundary rows into its mailbox (write-through), publish its step, wait
+//    (bounded) for each neighbour to reach it (read-after-write on the rows
+//    this rank copies, write-after-read on the mailbox the neighbour reads),
+//    copy their mailbox rows into the local halo rows with system-scope loads.
+//    One tiny launch per step, no RCCL kernel, no host round trip.
+//
+// Mailboxes: every rank exports ONE small allocation — the 512-B sync block
+// followed by two parity slots of its first and last boundary rows — and the
+// neighbours map only that, never the slab (so slabs of any size, sized for
+// 288 GB, keep the one-sided transport; round 2's hipIpcOpenMemHandle hang
+// concerned a single allocation above 2 GiB).
 //
 // Reference: no multi-GPU code exists (/root/reference/
 // CMakeLists.txt:2 name only); this is the north-star halo tier.
@@ -118,14 +125,38 @@ __global__ __launch_bounds__(256) void peer_probe_kernel(mpx_peer_probe p) {
 // ---------------------------------------------------------------------------
 // streaming halo fetch: block b serves side b (0 = rows above, 1 = rows below)
 // ---------------------------------------------------------------------------
+constexpr int kSyncCtr = 32;  // arrivals of the two blocks' mailbox copies
+
 __global__ __launch_bounds__(256) void halo_fetch_kernel(mpx_halo_fetch f) {
     const int side = blockIdx.x;
-    if (threadIdx.x == 0) peer::publish(f.sync + kSyncStep, f.step);  // idempotent per block
+    // (1) this rank's boundary rows of the frame being read -> its mailbox slot
+    // (system-scope write-through stores). The slot was last read by the side's
+    // neighbour two steps ago; this rank's previous fetch waited for that
+    // neighbour to start its next step, so the read is over (write-after-read).
+    if (f.own_src[side]) {
+        const uint32_t words = (uint32_t)(f.mb_bytes[side] / 4);
+        const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(f.own_src[side]), 0,
+                                                                             (int)f.mb_bytes[side], 0x00020000);
+        const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(f.mb_dst[side], 0, (int)f.mb_bytes[side],
+                                                                             0x00020000);
+        for (uint32_t w = threadIdx.x; w < words; w += 256)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_raw_buffer_load_b32(src, w * 4, 0, 0), dst, w * 4, 0,
+                                                  peer::kCpolSystem);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores acknowledged
+    __syncthreads();
+    // (2) the later of the two blocks publishes the step (release)
+    if (threadIdx.x == 0) {
+        const uint32_t c = __hip_atomic_fetch_add(f.sync + kSyncCtr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 1u) {
+            __hip_atomic_store(f.sync + kSyncCtr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            peer::publish(f.sync + kSyncStep, f.step);
+        }
+    }
     if (!f.flag[side]) return;  // block-uniform: global edge
-    // wait even when no rows are copied from this side (one-sided windows such
-    // as Roberts): the neighbour READS this rank's rows, and its reaching
-    // `step` means it finished the fetch of step - 1, so the buffer this
-    // step's convolution overwrites is no longer being read (write-after-read)
+    // (3) wait even when no rows are copied from this side (one-sided windows such
+    // as Roberts): the neighbour READS this rank's mailbox, and its reaching
+    // `step` means it started step `step`, so its fetch of step - 1 is over
     __shared__ int s_ok;
     if (threadIdx.x < 64) {  // one wave polls
         const bool ok = peer::wait_at_least(f.flag[side], f.step, f.sync + kSyncErr, f.spin_limit);
@@ -197,6 +228,10 @@ extern "C" int mpx_halo_fetch_run(const mpx_halo_fetch *f, void *stream) {
         MPX_CHECK_ARG((!f->src[s] || (f->flag[s] && f->dst[s])), "copied rows need the neighbour's flag and a dst");
         MPX_CHECK_ARG(!f->src[s] || (f->bytes[s] > 0 && f->bytes[s] % 4 == 0 && f->bytes[s] < (int64_t)1 << 31),
                       "halo bytes must be a positive multiple of 4");
+        MPX_CHECK_ARG(!f->own_src[s] == !f->mb_dst[s], "mailbox rows need a source and a destination");
+        MPX_CHECK_ARG(!f->own_src[s] || (f->mb_bytes[s] > 0 && f->mb_bytes[s] % 4 == 0 &&
+                                         f->mb_bytes[s] < (int64_t)1 << 31),
+                      "mailbox bytes must be a positive multiple of 4");
     }
     hipLaunchKernelGGL(halo_fetch_kernel, dim3(2), dim3(256), 0, as_stream(stream), *f);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());

@@ -156,18 +156,23 @@ def _jacobi_peer_ckpt_worker(rank, world, port, rows, cols, ckdir, errq):
         errq.put(f"rank {rank}: {traceback.format_exc()}")
 
 
-def _stream_peer_worker(rank, world, port, h, w, filt, steps, errq):
-    """Streaming conv on GPU ranks sharing one device: the device-signalled
-    halo fetch (publish step, bounded wait, xGMI copy) each step; N ranks ==
-    one device running the same frame sequence on the whole image."""
+def _stream_peer_worker(rank, world, port, h, w, filt, steps, errq, fused=True):
+    """Streaming conv on GPU ranks sharing one device: the halo exchange fused
+    into the band kernel (edge waves wait, read the neighbours' mailboxes,
+    publish; one launch per step) for aligned widths, else the device-signalled
+    fetch kernel; N ranks == one device running the same frame sequence on the
+    whole image."""
     try:
         from cuda_mpi_openmp_amd.models.edge import stream_reference
 
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank))
+        if not fused:
+            os.environ["MPX_STREAM_FUSED"] = "0"
         ctx = parallel.init(device="cuda", backend="gloo")
         det = SlabEdgeDetector(ctx, h, w, filt, halo="peer", stream=True)
-        assert det.transport == "xgmi-peer-signalled-fetch", det.transport
+        want = "xgmi-peer-fused" if (fused and w % 4 == 0) else "xgmi-peer-signalled-fetch"
+        assert det.transport == want, (det.transport, want)
         s = det.slab
         for seed, k in ((21, steps), (22, steps + 3)):
             full = _img(h, w, seed)
@@ -180,6 +185,13 @@ def _stream_peer_worker(rank, world, port, h, w, filt, steps, errq):
             if ctx.rank == 0:
                 ref = stream_reference(full.to(ctx.device), filt, k).cpu()
                 assert torch.equal(got.cpu(), ref), f"streaming peer conv differs ({filt}, {k} steps)"
+            # this rank's last step against the CPU reference on the halo rows it read
+            buf = det.halo_filled().cpu()
+            exp = torch.empty((s.rows, w, 4), dtype=torch.uint8)
+            ops.conv_rows(buf, exp, det.filter, src_row0=s.own_offset, out_row0=0, oy0=0, oy1=s.rows,
+                          y_lo=s.y_lo, y_hi=s.y_hi)
+            assert torch.equal(exp, det.stream_out.cpu()), "last step differs from the CPU on its halo rows"
+            ctx.barrier()
         det.close()
         parallel.shutdown()
     except Exception:  # noqa: BLE001
@@ -313,13 +325,33 @@ def test_jacobi_peer_graph_after_parity_flipping_reload(gpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (4, "sobel5_dense"), (8, "sobel5")])
+@pytest.mark.parametrize("world,filt", [(2, "sobel5"), (3, "roberts"), (4, "sobel5_dense"), (8, "sobel5"),
+                                        (4, "roberts"), (3, "gauss5")])
 def test_stream_peer_equals_one_device(gpu, world, filt):
-    """each step's input is the previous step's output, so the
-    halo rows change every step; the signalled fetch orders them on the
-    device. Aligned (64) and unaligned (62) widths."""
-    w = 64 if world != 3 else 62
-    _run_ranks(_stream_peer_worker, world, 8 * 6 + 5, w, filt, 5)
+    """each step's input is the previous step's output,
+    so the halo rows change every step; the fused band kernel (aligned widths:
+    64, 260) or the signalled fetch kernel (unaligned: 62) orders them on the
+    device. Slabs of a few rows up to a few segments."""
+    w = {3: 62}.get(world, 64) if filt != "gauss5" else 260
+    h = 8 * 6 + 5 if filt != "gauss5" else 8 * 37 + 5
+    _run_ranks(_stream_peer_worker, world, h, w, filt, 5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_stream_peer_fetch_kernel_aligned(gpu, world):
+    """The fetch-kernel form (MPX_STREAM_FUSED=0) on an aligned width: the A/B
+    partner of the fused form, over the same mailboxes."""
+    _run_ranks(_stream_peer_worker, world, 8 * 6 + 5, 64, "sobel5", 5, fused=False)
+
+
+@pytest.mark.gpu
+def test_jacobi_peer_slabs_beyond_2gib(gpu):
+    """per-rank u / u_new slabs of 20,000 x 16,384 fp64 (2.6 GB
+    each, past the 2 GiB size whose IPC open hung in round 2) keep the
+    one-sided transport — only the mailboxes are exported — and stay
+    bit-identical to one device."""
+    _run_ranks(_jacobi_peer_worker, 2, 40000, 16384, 20, True, timeout=400)
 
 
 @pytest.mark.gpu
