@@ -70,7 +70,7 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_cuda = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     contract = _contract.active()
-    rehearsal = contract or os.environ.get("MPX_DIST_BACKEND") == "gloo"
+    rehearsal = contract or (backend or os.environ.get("MPX_DIST_BACKEND")) == "gloo"
     if use_cuda:
         ndev = torch.cuda.device_count()
         if ndev == 0:

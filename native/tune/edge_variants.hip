@@ -92,7 +92,8 @@ __global__ __launch_bounds__(256) void linear_copy_kernel(const u32x4_t *__restr
 // keeps every halo load live. F bit 0: per-row LDS exchange with the
 // neighbouring thread + barrier (the horizontal pass's cost); bit 1: odd
 // bands walk upwards; bit 2: no XCD remap; bit 3: non-temporal stores;
-// bit 4: 512-thread workgroups over 2048 columns; bit 5: no halo loads.
+// bit 4: 512-thread workgroups over 2048 columns; bit 5: no halo loads;
+// bit 6: non-temporal loads (the linear NT copy's load policy).
 template <int F>
 __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
                                                          int w4, int h, int R, int nchunks) {
@@ -111,6 +112,7 @@ __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restri
     // traffic of a band whose halo rows come from its neighbours through LDS
     auto ld = [&](int j) {
         if ((F & 32) && (j < 2 || j > R + 1)) return u32x4_t{0u, 0u, 0u, 0u};
+        if constexpr ((F & 64) != 0) return __builtin_nontemporal_load(in + (int64_t)row_of(min(j, R + 3)) * w4 + c);
         return in[(int64_t)row_of(min(j, R + 3)) * w4 + c];
     };
     u32x4_t r[8];
@@ -145,10 +147,18 @@ __global__ __launch_bounds__(1024) void band_copy_kernel(const u32x4_t *__restri
 // in-flight window down the image the way the linear copy does. F bit 0:
 // xcd_remap (each XCD sweeps a contiguous eighth of the tiles, vertical
 // neighbours share its L2), else blockIdx order (one window over all XCDs);
-// bit 1: non-temporal loads; bit 2: non-temporal stores.
+// bit 1: non-temporal loads; bit 2: non-temporal stores; bit 3: 96 KiB of
+// (idle) LDS per workgroup, so one workgroup per CU is resident and the tiles
+// run in several rounds (a compact in-flight window even at large R).
 template <int R, int F>
 __global__ __launch_bounds__(1024) void burst_copy_kernel(const u32x4_t *__restrict__ in, u32x4_t *__restrict__ out,
                                                           int w4, int h, int tpr) {
+    if constexpr ((F & 8) != 0) {
+        __shared__ uint32_t cap[96 * 256];  // residency cap only
+        if (threadIdx.x == 0) cap[h & 1023] = (uint32_t)h;
+        __syncthreads();
+        if (cap[h & 1023] == 0xdeadbeefu) out[0] = u32x4_t{0u, 0u, 0u, 0u};  // never (h < 2^31): keeps the array
+    }
     const int b = (F & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int band = b / tpr, chunk = b - band * tpr;
     const int c = chunk * (int)blockDim.x + (int)threadIdx.x;
@@ -186,7 +196,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
     }
     MPX_CHECK_ARG(seg > 0, "seg must be > 0");
     if (v == 16) {  // burst tiles: seg = R output rows per tile, d = F | (threads code << 4)
-        const int tcode = (d >> 4) & 3, F = d & 7;
+        const int tcode = (d >> 4) & 3, F = d & 15;
         MPX_CHECK_ARG(tcode <= 2, "burst probe: threads code 0 / 1 / 2 = 256 / 512 / 1024");
         const int tpb = 256 << tcode;
         MPX_CHECK_ARG(w % (4 * tpb) == 0, "burst probe: w %% (4 * threads) == 0");
@@ -200,7 +210,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
     case RR:                                                                                                     \
         switch (F) {                                                                                             \
             MPX_BURST_F(RR, 0) MPX_BURST_F(RR, 1) MPX_BURST_F(RR, 2) MPX_BURST_F(RR, 3) MPX_BURST_F(RR, 4)       \
-            MPX_BURST_F(RR, 5) MPX_BURST_F(RR, 6) MPX_BURST_F(RR, 7)                                             \
+            MPX_BURST_F(RR, 5) MPX_BURST_F(RR, 6) MPX_BURST_F(RR, 7) MPX_BURST_F(RR, 13) MPX_BURST_F(RR, 15)     \
         }                                                                                                        \
         break;
         switch (seg) {
@@ -213,7 +223,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
         return MPX_OK;
     }
     if (v == 8) {  // row bands: seg = rows per band (multiple of 8), d = flag bits
-        MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 64, "band probe: w % 4096 == 0, seg % 4 == 0");
+        MPX_CHECK_ARG(w % 4096 == 0 && seg % 4 == 0 && d >= 0 && d < 128, "band probe: w % 4096 == 0, seg % 4 == 0");
         const int tpb = (d & 16) ? 512 : 1024;
         const int nchunks = w / (4 * tpb), nb = (h + seg - 1) / seg;
         const dim3 g((unsigned)(nb * nchunks)), b(tpb);
@@ -224,7 +234,7 @@ extern "C" int mpx_strip_copy_probe(const uint32_t *in, uint32_t *out, int w, in
 #define MPX_BAND(F) \
     case F: hipLaunchKernelGGL(band_copy_kernel<F>, g, b, 0, sb, vi, vo, w / 4, h, seg, nchunks); break;
             MPX_BAND(0) MPX_BAND(1) MPX_BAND(2) MPX_BAND(3) MPX_BAND(4) MPX_BAND(10) MPX_BAND(11) MPX_BAND(18)
-            MPX_BAND(19) MPX_BAND(26) MPX_BAND(34) MPX_BAND(42)
+            MPX_BAND(19) MPX_BAND(26) MPX_BAND(34) MPX_BAND(42) MPX_BAND(72) MPX_BAND(74) MPX_BAND(106)
             default: set_error("unsupported band flags %d", d); return MPX_ERR_ARG;
 #undef MPX_BAND
         }

@@ -141,8 +141,8 @@ def main():
     for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
         variants[f"copy/linear-{nm}"] = (
             (lambda d=d: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
-    for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26)] + [(16, 0), (16, 4), (16, 34),
-                                                                                        (16, 42), (32, 10), (32, 42)]:
+    for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26, 74)] + [
+            (16, 0), (16, 4), (16, 34), (16, 42), (32, 10), (32, 42), (16, 72), (16, 106), (32, 74)]:
         if True:  # row bands, 16-B vector per thread (ref None: XOR of rows, no reference)
             variants[f"copy/band-seg{seg}-f{fl}"] = (
                 (lambda fl=fl, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
@@ -152,8 +152,10 @@ def main():
     # (1 xcd_remap, 2 NT loads, 4 NT stores), t = threads per workgroup
     for R in (2, 4, 8, 12, 16, 24):
         for tcode in (0, 1, 2):
-            for fl in (0, 1, 4, 5, 6, 7):
+            for fl in (0, 1, 4, 5, 6, 7, 13, 15):
                 if tcode == 1 and fl not in (5, 7):
+                    continue
+                if fl >= 8 and (tcode != 2 or R < 8):  # residency cap: 1024-thread tiles, R >= 8
                     continue
                 d = fl | (tcode << 4)
                 variants[f"copy/burst-r{R}-t{256 << tcode}-f{fl}"] = (
