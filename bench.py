@@ -89,6 +89,10 @@ def parse_args(argv=None):
     p.add_argument("--halo", choices=["auto", "peer", "rccl"], default="auto",
                    help="halo transport for N > 1: one-sided xGMI loads from IPC-mapped neighbour slabs (peer), "
                         "RCCL send/recv (rccl), or peer when available (auto)")
+    p.add_argument("--streams", type=int, default=2,
+                   help="HIP streams the rotated static steps alternate over (pair i always on stream i %% S): "
+                        "independent frames overlap one kernel's tail with the next one's start; 1 = one stream. "
+                        "Only where steps are independent (one rank or static peer halos)")
     p.add_argument("--graph", type=int, default=0,
                    help="capture this many steps into one HIP graph and replay it (0 = eager launches; "
                         "in-order and peer halo modes)")
@@ -140,9 +144,23 @@ def run(args) -> int:
     ctx.barrier()
 
     cyc = [0]
+    nstreams = 1
+    if args.streams > 1 and ctx.device.type == "cuda" and all(d.independent_steps for d in dets) and args.graph == 0:
+        if len(dets) % args.streams:
+            raise SystemExit(f"--streams {args.streams} must divide --rotate {len(dets)}")
+        nstreams = args.streams
+    streams = [torch.cuda.Stream(ctx.device) for _ in range(nstreams)] if nstreams > 1 else []
+    handles = [s.cuda_stream for s in streams]
+    if streams:  # every stream starts after the set-up work of the current one
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream(ctx.device))
 
     def rot_step():
-        dets[cyc[0] % len(dets)].step()
+        i = cyc[0] % len(dets)
+        if handles:
+            dets[i].step(handles[i % nstreams])  # pair i always on the same stream: no cross-stream reuse
+        else:
+            dets[i].step()
         cyc[0] += 1
 
     wd_s = args.watchdog if args.watchdog is not None else (300.0 if n > 1 else 0.0)
@@ -274,6 +292,7 @@ def run(args) -> int:
                 "image_hw": [args.size * n, args.size],
                 "halo_rows": [d0.filter.halo_up, d0.filter.halo_down],
                 "graph_steps": args.graph if graph is not None else 0,
+                "streams": nstreams,
                 "rotate": len(dets),
                 "working_set_MiB_per_gpu": round(len(dets) * 2 * args.size * args.size * 4 / 2**20, 1),
             },

@@ -245,18 +245,30 @@ class SlabEdgeDetector:
         ops.conv_rows(self.buf, self.out, self.filter, src_row0=s.own_offset, out_row0=0, oy0=a, oy1=b,
                       y_lo=s.y_lo, y_hi=s.y_hi)
 
-    def step(self) -> torch.Tensor:
-        """Exchange halos and convolve every owned row; returns the output slab."""
+    @property
+    def independent_steps(self) -> bool:
+        """True when a step neither exchanges nor depends on the previous step
+        (one rank, or static peer halos): steps of DIFFERENT detectors may then
+        run on different streams (``step(stream=...)``)."""
+        return not self.stream and not self.pipeline and (not self.ctx.is_distributed or self.peer is not None)
+
+    def step(self, stream: Optional[int] = None) -> torch.Tensor:
+        """Exchange halos and convolve every owned row; returns the output slab.
+        ``stream``: a raw HIP stream handle for the launch (independent steps
+        only); default the current torch stream."""
         if self._traced:
             with trace.range("edge.step"):
-                return self._step()
-        return self._step()
+                return self._step(stream)
+        return self._step(stream)
 
-    def _step(self) -> torch.Tensor:
+    def _step(self, stream: Optional[int] = None) -> torch.Tensor:
         if self.stream:
             return self._step_stream()
         if self.pipeline:
             return self._step_pipelined()
+        if stream is not None and self.independent_steps:
+            self._all(stream)
+            return self.out
         st = torch.cuda.current_stream(self.buf.device).cuda_stream if self.buf.is_cuda else None
         if not self.ctx.is_distributed or self.peer is not None:
             self._all(st)  # peer mode: the kernel reads the neighbours' rows itself
