@@ -51,6 +51,7 @@ _SIGNATURES = {
         [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],
     ),
     "mpx_conv_set_band_min": (ctypes.c_longlong, [ctypes.c_longlong]),
+    "mpx_conv_set_band_mode": (c_int, [c_int]),
     "mpx_conv_peer": (
         c_int,
         [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp],

@@ -90,6 +90,10 @@ int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0
 /* Minimum image size in pixels for the band kernel (smaller aligned images take
  * the wave kernel); returns the previous value, n < 0 only queries. */
 long long mpx_conv_set_band_min(long long n);
+/* band kernel mode (as MPX_CONV_BAND: 0 wave kernel, 1 plain stores, 2 NT stores,
+ * 3 NT stores + NT interior loads (default), 4 vertical halo sharing through LDS
+ * for 5-row windows); returns the previous mode, m < 0 queries */
+int mpx_conv_set_band_mode(int m);
 
 /* Tuning-harness entry (tools/kbench.py): kernel variants for k in {2, 5}, MAG2,
  * whole image. kind 0 = LDS streaming kernel (p1 = rows per wave 4/8/16,

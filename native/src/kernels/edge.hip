@@ -185,6 +185,13 @@ extern "C" int mpx_conv_direct(const uint32_t *in, uint32_t *out, int w, int pit
 
 // Minimum image size (pixels) for the band kernel; returns the previous value.
 // n < 0 only queries. Tests set 0 to run the band kernel on small images.
+// Band kernel mode (MPX_CONV_BAND semantics, 0..4); returns the previous mode.
+// m < 0 only queries.
+extern "C" int mpx_conv_set_band_mode(int m) {
+    if (m < 0 || m > 4) return mpx::edgel::g_band_mode.load();
+    return mpx::edgel::g_band_mode.exchange(m);
+}
+
 extern "C" long long mpx_conv_set_band_min(long long n) {
     if (n < 0) return mpx::edgel::g_band_min_pixels.load();
     return mpx::edgel::g_band_min_pixels.exchange(n);

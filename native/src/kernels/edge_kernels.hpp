@@ -807,6 +807,18 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
 // apron falls back to the lane's own edge pixel at x = 0 and x = w.
 // Requires w % 4 == 0, pitch % 4 == 0 and 16-B aligned rows.
 // ---------------------------------------------------------------------------
+// Vertical halo sharing (conv_band16v_kernel): the LDS slots a wave exchanges
+// its boundary rows through with the vertically adjacent waves of its
+// workgroup (u32 offsets into the kernel's exchange array; < 0 = that side
+// loads its halo rows from memory). A slot holds two raw rows (64 lanes x 16 B)
+// plus the rows' 8-B aprons of lanes 0 and 63; a flag word per slot.
+constexpr int kVsRowWords = 64 * 4 + 4;
+constexpr int kVsSlotWords = 2 * kVsRowWords;
+struct VsX {
+    int take_start = -1, give_start = -1, take_end = -1, give_end = -1;  // slot offsets
+    int ftake_start = 0, fgive_start = 0, ftake_end = 0, fgive_end = 0;  // flag offsets
+};
+
 // One wave's segment walk in one direction (UP: bottom row first), prologue
 // included, so nothing but scalars is live across the direction branch.
 // SPW (fused streaming halo, mpx_conv_stream_peer): an edge wave's walk — every
@@ -814,11 +826,17 @@ __global__ __launch_bounds__(256) void conv_wave_kernel(const uint32_t *__restri
 // and output rows 0 .. nf-1 / own_rows-nl .. own_rows-1 are also stored
 // write-through into this rank's mailbox rows mbf / mbl (one extra store per
 // row, dropped by the buffer bounds check on the other rows: no branch).
-template <int K, int A, int MODE, bool FAST, class F, bool UP, int OPT, bool SPW = false>
+// VSEG > 0 (vertical halo sharing, conv_band16v_kernel): a full segment of
+// exactly VSEG rows whose 2 + 2 halo rows come from the LDS slots in `vx`
+// where a neighbouring wave of the workgroup owns them (those rows issue no
+// memory load), and whose own first / last two rows go into the neighbours'
+// slots; the walk is then fully unrolled. lds: the kernel's exchange array.
+template <int K, int A, int MODE, bool FAST, class F, bool UP, int OPT, bool SPW = false, int VSEG = 0>
 __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                      int w, int pitch, int ys, int ye, int y_lo, int y_hi, int x0,
                                                      const Taps &taps, RowSrc rs, uint32_t *mbf = nullptr,
-                                                     uint32_t *mbl = nullptr, int nf = 0, int nl = 0) {
+                                                     uint32_t *mbl = nullptr, int nf = 0, int nl = 0,
+                                                     uint32_t *lds = nullptr, VsX vx = VsX{}) {
     constexpr int R = K - 1 - A;
     constexpr int NV = 4 + A + R;
     constexpr bool TWO = (MODE == MPX_CONV_MAG2);
@@ -854,11 +872,14 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // those loads are never consumed: their offsets go out of range, so the
     // hardware drops them instead of fetching a neighbour segment's rows
     const int i_last = ye - ys + K - 2;
+    static_assert(VSEG == 0 || (A == 2 && K == 5 && VSEG >= 8), "vertical sharing: 5-row windows, 2 + 2 halo rows");
     auto load_row = [&](int i, u32x2_t &ap) -> u32x4_t {
         const uint32_t *row = row_ptr(min(i, i_last));
         const __amdgpu_buffer_rsrc_t rr =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, w * 4, 0x00020000);
-        const bool live = i <= i_last;  // wave-uniform
+        // wave-uniform; VSEG: rows an LDS slot delivers issue no memory access
+        const bool live = i <= i_last && !(VSEG > 0 && ((i < 2 && vx.take_start >= 0) ||
+                                                        (i >= VSEG + 2 && vx.take_end >= 0)));
         const int qo = live ? cc * 4 : kDrop, ao = live ? ap_off : kDrop;
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
@@ -959,8 +980,42 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         }
     };
 
+    // VSEG exchange: raw rows (fix_quad is applied by the reader, whose lanes
+    // sit at the same columns) and lanes 0 / 63's aprons; a slot row r of a
+    // walk row i: down walks keep the rows' image order, up walks reverse it
+    auto vs_put = [&](int slot, int r, u32x4_t q, u32x2_t ap) {
+        *reinterpret_cast<u32x4_t *>(lds + slot + r * kVsRowWords + 4 * lane) = q;
+        if (ap_left || ap_right)
+            *reinterpret_cast<u32x2_t *>(lds + slot + r * kVsRowWords + 256 + (ap_right ? 2 : 0)) = ap;
+    };
+    auto vs_get = [&](int slot, int r, u32x2_t &ap) -> u32x4_t {
+        if (ap_left || ap_right)
+            ap = *reinterpret_cast<const u32x2_t *>(lds + slot + r * kVsRowWords + 256 + (ap_right ? 2 : 0));
+        return *reinterpret_cast<const u32x4_t *>(lds + slot + r * kVsRowWords + 4 * lane);
+    };
+    auto vs_flag = [&](int f) { __hip_atomic_store(lds + f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto vs_wait = [&](int f) {
+        while (__hip_atomic_load(lds + f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+            __builtin_amdgcn_s_sleep(1);
+    };
+
 #pragma unroll
     for (int q = 0; q < D; ++q) pre[q] = load_row(q, apr[q]);
+    if constexpr (VSEG > 0) {
+        // start of the walk: give this wave's first two rows (walk rows 2, 3) as
+        // soon as they arrive, then take the neighbour's two (walk rows 0, 1) —
+        // the neighbour does the same, so neither waits on the other's walk
+        if (vx.give_start >= 0) {
+            vs_put(vx.give_start, UP ? 1 : 0, pre[2], apr[2]);
+            vs_put(vx.give_start, UP ? 0 : 1, pre[3], apr[3]);
+            vs_flag(vx.fgive_start);
+        }
+        if (vx.take_start >= 0) {
+            vs_wait(vx.ftake_start);
+            pre[0] = vs_get(vx.take_start, UP ? 1 : 0, apr[0]);
+            pre[1] = vs_get(vx.take_start, UP ? 0 : 1, apr[1]);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < K - 1; ++u) {
         const u32x4_t px = fix_quad(pre[u]);
@@ -972,6 +1027,18 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const int u = (K - 1 + v) % K;
         const int q = (K - 1 + v) % D;
         const int i = K - 1 + g * D + v;
+        if constexpr (VSEG > 0) {
+            // end of the walk: give the last two own rows (walk rows VSEG, VSEG+1)
+            // as they are consumed, take the neighbour's two (VSEG+2, VSEG+3)
+            if (vx.give_end >= 0 && (i == VSEG || i == VSEG + 1)) {
+                vs_put(vx.give_end, UP ? (i == VSEG ? 1 : 0) : (i == VSEG ? 0 : 1), pre[q], apr[q]);
+                if (i == VSEG + 1) vs_flag(vx.fgive_end);
+            }
+            if (vx.take_end >= 0 && (i == VSEG + 2 || i == VSEG + 3)) {
+                if (i == VSEG + 2) vs_wait(vx.ftake_end);
+                pre[q] = vs_get(vx.take_end, UP ? (i == VSEG + 2 ? 1 : 0) : (i == VSEG + 2 ? 0 : 1), apr[q]);
+            }
+        }
         const u32x4_t px = fix_quad(pre[q]);
         const u32x2_t ap = apr[q];
         pre[q] = load_row(i + D, apr[q]);
@@ -1038,6 +1105,11 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             __builtin_amdgcn_raw_buffer_store_b128(o, mr, st ? cin * 4 : kDrop, 0, peer::kCpolSystem);
         }
     };
+    if constexpr (VSEG > 0) {  // ye - ys == VSEG: every row index compile-time
+#pragma unroll
+        for (int j = 0; j < VSEG; ++j) row_step(j / D, j % D);
+        return;
+    }
     const int nrows = ye - ys;
     const int nfull = nrows / D;
     const int rem = nrows - nfull * D;
@@ -1123,6 +1195,83 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
         band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
     else
         band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+}
+
+// ---------------------------------------------------------------------------
+// Band kernel with VERTICAL halo sharing (LDS): a 16-wave
+// workgroup owns 16 vertically consecutive VSEG-row segments of one 256-column
+// strip (one resident workgroup per CU at the band kernel's 4 waves per SIMD).
+// The 2 + 2 halo rows a segment shares with the segment above / below are
+// loaded ONCE, by the wave that owns them, and handed to the neighbour through
+// LDS (~62 KiB of row slots; the alternating walk directions make each pair
+// of neighbours reach their shared rows at the same moment: at the start of
+// both walks or at the end of both). Only the workgroup's outer boundaries
+// read halo rows from memory — 4 per 16 x VSEG rows instead of 4 per VSEG —
+// so every row load can be non-temporal. Copy probe of this traffic
+// (tools/kbench.py copy/band-seg16-f106 vs f74, NT loads): 25.25 vs 26.47 us.
+// Segments that are not full (the image's last) and their neighbours fall back
+// to the memory halo walk. Results are bit-identical to conv_band4_kernel (the
+// same consume / tap order; only where a row's bytes come from changes).
+// ---------------------------------------------------------------------------
+template <int K, int A, int MODE, bool FAST, class F, int VSEG>
+__global__ __launch_bounds__(1024) void conv_band16v_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                            int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                                                            int segs, int strips, Taps taps) {
+    constexpr int NB = 15;  // boundaries between the 16 waves
+    __shared__ __attribute__((aligned(16))) uint32_t xlds[2 * NB * kVsSlotWords + 2 * NB];
+    constexpr int kFlag0 = 2 * NB * kVsSlotWords;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 2 * NB) xlds[kFlag0 + threadIdx.x] = 0u;
+    __syncthreads();  // before any wave can exit or exchange
+    const int strip = blockIdx.x % strips;
+    const int sg = (blockIdx.x / strips) * 16 + wv;
+    if (sg >= segs) return;  // wave-uniform; nobody exchanges with it (not full)
+    const int ys = oy0 + sg * VSEG;
+    const int ye = min(ys + VSEG, oy1);
+    auto full = [&](int g) { return g >= 0 && g < segs && oy0 + (g + 1) * VSEG <= oy1; };
+    const bool me = full(sg);
+    const bool top = me && wv > 0 && full(sg - 1);    // exchange with the wave above (boundary wv - 1)
+    const bool bot = me && wv < 15 && full(sg + 1);   // with the wave below (boundary wv)
+    // slot (boundary b, side s): s = 0 holds the upper wave's last two rows, s = 1
+    // the lower wave's first two rows; flags in the same (b, s) order
+    auto slot = [](int b, int s) { return (2 * b + s) * kVsSlotWords; };
+    auto flag = [](int b, int s) { return kFlag0 + 2 * b + s; };
+    const bool upw = sg & 1;  // odd segments walk up (as conv_band4_kernel with alt = 1)
+    VsX vx;
+    // a down walk starts at its top and ends at its bottom, an up walk the reverse
+    const bool st_nb = upw ? bot : top, en_nb = upw ? top : bot;
+    const int bs = upw ? wv : wv - 1, be = upw ? wv - 1 : wv;  // boundaries at the start / end side
+    if (st_nb) {
+        // start side: down walk = the boundary above (take s = 0, give s = 1), up walk = below (take 1, give 0)
+        vx.take_start = slot(bs, upw ? 1 : 0);
+        vx.give_start = slot(bs, upw ? 0 : 1);
+        vx.ftake_start = flag(bs, upw ? 1 : 0);
+        vx.fgive_start = flag(bs, upw ? 0 : 1);
+    }
+    if (en_nb) {
+        vx.take_end = slot(be, upw ? 0 : 1);
+        vx.give_end = slot(be, upw ? 1 : 0);
+        vx.ftake_end = flag(be, upw ? 0 : 1);
+        vx.fgive_end = flag(be, upw ? 1 : 0);
+    }
+    constexpr int OPT = 2 | 64;  // NT stores, every row load non-temporal
+    RowSrc rs;
+    rs.up = in;  // whole-image or resident-halo launches: every row is `in`'s
+    rs.dn = in;
+    if (me) {
+        if (upw)
+            band4_walk<K, A, MODE, FAST, F, true, OPT, false, VSEG>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256,
+                                                                    taps, rs, nullptr, nullptr, 0, 0, xlds, vx);
+        else
+            band4_walk<K, A, MODE, FAST, F, false, OPT, false, VSEG>(in, out, w, pitch, ys, ye, y_lo, y_hi,
+                                                                     strip * 256, taps, rs, nullptr, nullptr, 0, 0,
+                                                                     xlds, vx);
+    } else {  // a partial segment: the memory halo walk
+        if (upw)
+            band4_walk<K, A, MODE, FAST, F, true, 34>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+        else
+            band4_walk<K, A, MODE, FAST, F, false, 34>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * 256, taps, rs);
+    }
 }
 
 // Gray value packing helper for the non-stream kernels.

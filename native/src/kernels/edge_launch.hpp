@@ -160,6 +160,27 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     return MPX_OK;
 }
 
+inline constexpr int kBandModeDefault = 3;
+
+// Vertical halo sharing (conv_band16v_kernel): 16-wave workgroups of 16
+// consecutive 16-row segments of one strip; the shared halo rows travel
+// through LDS instead of being loaded twice. 5-row windows (A = 2) only,
+// rows resident in `in` (no neighbour-slab row sources).
+inline constexpr int kVSeg = 16;
+template <int K, int A, int MODE, bool FAST, class F>
+int launch_band16v(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
+                   const Taps &taps, hipStream_t s) {
+    static_assert(K == 5 && A == 2, "vertical sharing covers 5-row windows");
+    MPX_CHECK_ARG(w % 4 == 0 && pitch % 4 == 0 && aligned16(in) && aligned16(out), "band kernel: 16-B aligned rows");
+    const int strips = (w + 255) / 256;
+    const int segs = (oy1 - oy0 + kVSeg - 1) / kVSeg;
+    const int64_t nblk = (int64_t)strips * ((segs + 15) / 16);
+    MPX_CHECK_ARG(nblk < ((int64_t)1 << 31), "image too large for one launch");
+    hipLaunchKernelGGL((edge::conv_band16v_kernel<K, A, MODE, FAST, F, kVSeg>), dim3((unsigned)nblk), dim3(1024), 0, s,
+                       in, out, w, pitch, oy0, oy1, y_lo, y_hi, segs, strips, taps);
+    return MPX_OK;
+}
+
 // The band kernel serves every launch whose window reaches at most two columns
 // on each side (K <= 5 except 4x4-style anchors) and whose rows (and neighbour
 // rows) are 16-B aligned, with non-temporal output stores. MI355X 4096^2, 6
@@ -174,13 +195,15 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
 // 32.3, 3x3 filters -0.6 to -0.8, Roberts / sharpen3 / box3 within 0.15
 // (profiles/lab2_conv.md). MPX_CONV_BAND=0: wave kernel, 1: band kernel with
 // plain stores, 2: NT stores and plain loads; read once per process.
-inline int band_mode() {
-    static const int v = [] {
-        const char *e = std::getenv("MPX_CONV_BAND");
-        return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
-    }();
-    return v;
+// MPX_CONV_BAND=4: the vertical-halo-sharing kernel (conv_band16v_kernel) for
+// 5-row windows with resident rows, mode 3 otherwise. mpx_conv_set_band_mode()
+// switches the mode at run time (tests, A/B in one process).
+inline int band_mode_env() {
+    const char *e = std::getenv("MPX_CONV_BAND");
+    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : kBandModeDefault;
 }
+inline std::atomic<int> g_band_mode{band_mode_env()};
+inline int band_mode() { return g_band_mode.load(std::memory_order_relaxed); }
 // Small images (below kBandMinPixels) keep the wave kernel: with one resident
 // round of 16-row segments a 1-Mpx image is only a few hundred waves, and the
 // reference harness's cold single launches on its 0.5-2 Mpx images measured
@@ -202,6 +225,10 @@ template <int K, int A, int MODE, class F>
 int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
                 const Taps &taps, hipStream_t s, const edge::RowSrc &rs) {
     const int m = band_mode();
+    if constexpr (K == 5 && A == 2) {
+        if (m == 4 && (!rs.up || rs.up == in) && (!rs.dn || rs.dn == in))
+            return launch_band16v<K, A, MODE, true, F>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s);
+    }
     if (m == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
     if (m == 2)

@@ -332,6 +332,12 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
         set_error("unsupported band OPT %d", p2 / 1000);
         return MPX_ERR_ARG;
     }
+    if (kind == 10) {
+        // separable sobel5 on the vertical-halo-sharing band kernel (conv_band16v_kernel)
+        MPX_CHECK_ARG(k == 5 && w % 4 == 0 && aligned16(in) && aligned16(out), "band16v variant: k = 5, w % 4 == 0");
+        const Taps st = make_taps(k, wx, wy, true, true);
+        return edgel::launch_band16v<5, 2, MPX_CONV_MAG2, true, edge::Sobel5SepTaps>(in, out, w, w, 0, h, 0, h - 1, st, s);
+    }
     if (kind == 9) {
         // dense band kernel, compiled-in taps (k = 2 Roberts, k = 5 sobel5_dense):
         // p1 = segment rows (0 = auto), p2 % 100 = waves per SIMD for auto, p2 / 1000 = OPT

@@ -81,6 +81,34 @@ def test_conv_band_kernel_strip_edges(gpu, filt, w):
     assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f))
 
 
+@pytest.mark.parametrize("filt", ["sobel5", "gauss5", "sobel5_dense", "gauss5_dense", "log5"])
+def test_conv_vertical_share_kernel(gpu, filt):
+    """Band mode 4 (conv_band16v_kernel: 16 vertically consecutive segments per
+    workgroup, shared halo rows handed over through LDS) on every 5-row window:
+    whole 16-segment groups, partial groups, a short last segment (its
+    neighbours fall back to memory halos), several strips, slab launches with
+    resident halo rows; every byte against the CPU reference."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    f = ops.get_filter(filt)
+    old_min, old_mode = L.mpx_conv_set_band_min(0), L.mpx_conv_set_band_mode(4)
+    try:
+        for h, w in ((4096, 4096), (512, 260), (16 * 16 + 7, 516), (16 * 3, 1024), (19, 256), (5, 64), (300, 8)):
+            img = rand_img(h, w, seed=h + w)
+            assert torch.equal(ops.conv(img.to(gpu), f).cpu(), ops.conv(img, f)), (h, w)
+        # a slab launch: logical rows [0, 200) of a buffer with 2 resident halo rows each side
+        buf = rand_img(204, 516, seed=9)
+        out_g = torch.empty((200, 516, 4), dtype=torch.uint8, device=gpu)
+        ops.conv_rows(buf.to(gpu), out_g, f, src_row0=2, out_row0=0, oy0=0, oy1=200, y_lo=-2, y_hi=201)
+        out_c = torch.empty((200, 516, 4), dtype=torch.uint8)
+        ops.conv_rows(buf, out_c, f, src_row0=2, out_row0=0, oy0=0, oy1=200, y_lo=-2, y_hi=201)
+        assert torch.equal(out_g.cpu(), out_c)
+    finally:
+        L.mpx_conv_set_band_mode(old_mode)
+        L.mpx_conv_set_band_min(old_min)
+
+
 @pytest.mark.parametrize("filt", ["roberts", "sobel3", "prewitt3", "scharr3", "laplace3", "sharpen3", "sobel5_dense",
                                   "log5"])
 def test_conv_named_taps_equal_runtime_taps(gpu, filt):

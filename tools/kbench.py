@@ -107,6 +107,9 @@ def main():
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
                                                                        per, 1, swx, swy, 0))), None if per == 18000 else sref)
+    variants["sobel5-sep/band16v"] = (  # vertical halo sharing through LDS (conv_band16v_kernel)
+        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 10, 0, 0, 1, swx, swy, 0))),
+        sref)
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
@@ -165,8 +168,9 @@ def main():
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
 
-    if args.only:
-        variants = {k: v for k, v in variants.items() if args.only in k}
+    if args.only:  # comma-separated substrings: a variant runs when its name contains any of them
+        keys = [k for k in args.only.split(",") if k]
+        variants = {k: v for k, v in variants.items() if any(s in k for s in keys)}
     # correctness first
     cpu_img = img.cpu()
     for fname in ("sobel5_dense", "roberts"):
