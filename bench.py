@@ -74,10 +74,15 @@ def parse_args(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--warmup-ms", type=float, default=30.0,
+    p.add_argument("--warmup-ms", type=float, default=0.0,
                    help="after the --warmup steps, keep running untimed steps until at least this much "
-                        "back-to-back step time has elapsed (the board's clocks settle over tens of ms of load); "
-                        "0 = exactly --warmup steps")
+                        "back-to-back step time has elapsed; 0 (default) = exactly --warmup steps. A/B on MI355X "
+                        "(profiles/lab2_conv.md, round 4): 30 ms of settling LOWERS the timed steps' rate (the "
+                        "board holds a lower clock under sustained load), so the driver's W is kept as given and "
+                        "the sustained rate is reported separately (value_sustained)")
+    p.add_argument("--sustain-ms", type=float, default=50.0,
+                   help="value_sustained: the same K rotated steps timed again after this much continuous load "
+                        "(0 = skip)")
     p.add_argument("--size", type=int, default=4096, help="image side per GPU slab")
     p.add_argument("--filter", default="sobel5")
     p.add_argument("--rotate", type=int, default=6,
@@ -215,6 +220,15 @@ def run(args) -> int:
     per_rank = parallel.all_gather_floats(mine, ctx)
     elapsed = max(per_rank)
 
+    # the same K steps after >= sustain_ms of continuous load (the clock the
+    # board holds under sustained load): reported beside `value`, not instead
+    sustained = None
+    if args.sustain_ms > 0 and graph is None:
+        settle(rot_step, len(dets), args.sustain_ms, ctx, sync, watchdog, parallel, lambda: [d.finish() for d in dets])
+        cyc[0] = 0
+        sustained = max(parallel.all_gather_floats(timed(rot_step, args.steps), ctx))
+        watchdog.beat()
+
     warm = None
     if not args.no_warm:
         warm_mine = timed(dets[0].step, args.steps)
@@ -305,6 +319,10 @@ def run(args) -> int:
             "verified_pixels": checked,
             "device": str(torch.cuda.get_device_name(ctx.device)) if ctx.device.type == "cuda" else "cpu",
         }
+        if sustained is not None:
+            rec["value_sustained"] = _sig(pixels / sustained / 1e9)
+            rec["ms_per_step_sustained"] = round(sustained * 1e3 / max(1, args.steps), 5)
+            rec["sustain_ms"] = args.sustain_ms
         if warm is not None:
             rec["value_warm_cache"] = _sig(pixels / warm / 1e9)
             rec["ms_per_step_warm_cache"] = round(warm * 1e3 / max(1, args.steps), 5)

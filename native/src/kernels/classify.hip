@@ -258,8 +258,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         for (int k = 0; k < NP; ++k) {
             o[k] = (px[k] & 0x00ffffffu) | ((B[k] & 31u) << 24);
             if (__builtin_expect(!decided(B[k], S[k], fp.T2), 0)) {
-                if (amb) atomicAdd(amb, 1u);
-                const uint32_t slot = atomicAdd(&s_namb, 1u);
+                const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count (one global add at the end)
                 if (slot < (uint32_t)kAmbCap) {  // deferred
                     s_amb[slot] = i * NP + k;
                     s_ambpx[slot] = px[k];
@@ -274,6 +273,8 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
+    // the ambiguity count: one global add per block, not one per pixel
+    if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);
     for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
         img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
     }
@@ -630,8 +631,7 @@ __global__ __launch_bounds__(256) void classify_mfma8_kernel(uint32_t *__restric
                 op[m] = (px[m] & 0x00ffffffu) | (((uint32_t)rb[m] & 31u) << 24);
                 // exact integers: the tag bits are below the shift
                 if (__builtin_expect((rs[m] >> 5) - (rb[m] >> 5) <= ip.T2, 0)) {
-                    if (amb) atomicAdd(amb, 1u);
-                    const uint32_t slot = atomicAdd(&s_namb, 1u);
+                    const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count
                     if (slot < (uint32_t)kAmb8Cap) {
                         s_amb[slot] = (ch * 32 + col) * 4 + m;
                         s_ambpx[slot] = px[m];
@@ -645,6 +645,7 @@ __global__ __launch_bounds__(256) void classify_mfma8_kernel(uint32_t *__restric
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
+    if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
     for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
 }
 

@@ -70,6 +70,10 @@ def test_bench_measurement_hygiene_fields_cpu():
     rec = _run(["--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2", "--no-stream",
                 "--warmup-ms", "5"])
     assert rec["warmup"] == 1 and rec["warmup_ms"] >= 5.0 and rec["warmup_steps_run"] >= 2
+    # the sustained-load rate rides along (same K steps after >= sustain_ms of load)
+    assert rec["value_sustained"] > 0 and rec["sustain_ms"] == 50.0
+    assert abs(rec["value_sustained"] - 64 * 64 / (rec["ms_per_step_sustained"] * 1e-3) / 1e9) \
+        < 1e-3 * max(1.0, rec["value_sustained"])
     assert rec["cpu_runs"] >= 5 and 0 < rec["cpu_ms_per_image_min"] <= rec["cpu_ms_per_image"]
     assert abs(rec["speedup_vs_cpu"] - rec["cpu_ms_per_image"] / rec["gpu_ms_per_image"]) \
         < 0.051 + 1e-3 * rec["speedup_vs_cpu"]

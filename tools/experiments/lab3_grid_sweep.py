@@ -37,7 +37,7 @@ def main():
     imgs = [torch.randint(0, 256, (size, size, 4), dtype=torch.uint8, device=dev) for _ in range(3)]
     host = imgs[0].cpu()
     ncs = [int(v) for v in os.environ.get("LAB3_NCS", "2,4,8,32").split(",")]
-    grids = [0, 256, 512, 768, 1024, 1280, 1536, 2048, 4096]
+    grids = [int(g) for g in os.environ.get("LAB3_GRIDS", "0,256,512,768,1024,1280,1536,2048,4096,8192,16384").split(",")]
     for nc in ncs:
         pts = class_points_for(size, size, nc, 64, seed=nc)
         mu, inv = ops.class_stats(host, pts)
