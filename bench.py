@@ -367,6 +367,20 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
         sdets[cyc[0] % len(sdets)].step()
         cyc[0] += 1
 
+    # each slab's frame sequence stays on one stream; different slabs' sequences
+    # are independent and overlap on `--streams` streams (device-signalled or no
+    # halos only: host-ordered RCCL exchanges keep one stream)
+    ns = args.streams if (args.streams > 1 and ctx.device.type == "cuda" and len(sdets) % args.streams == 0
+                          and all(d.independent_steps for d in sdets)) else 1
+    shandles = [torch.cuda.Stream(ctx.device) for _ in range(ns)] if ns > 1 else []
+    for st in shandles:
+        st.wait_stream(torch.cuda.current_stream(ctx.device))
+    shandles = [st.cuda_stream for st in shandles]
+    if shandles:
+        def step():  # noqa: F811 - the multi-stream form of the step above
+            i = cyc[0] % len(sdets)
+            sdets[i].step(shandles[i % ns])
+            cyc[0] += 1
     for _ in range(max(args.warmup, len(sdets))):
         step()
         watchdog.beat()
@@ -386,6 +400,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
         raise RuntimeError(f"rank {ctx.rank}: streaming halo wait timed out during the timed steps "
                            f"({'this rank' if any(bad) else 'on another rank'}; slabs {[i for i, b in enumerate(bad) if b]})")
     rec = {"value_streaming": _sig(n * args.size * args.size * args.steps / elapsed / 1e9),
+           "streams_streaming": ns,
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
            "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
            "transport_streaming": sdets[0].transport if n > 1 else None}

@@ -247,10 +247,17 @@ class SlabEdgeDetector:
 
     @property
     def independent_steps(self) -> bool:
-        """True when a step neither exchanges nor depends on the previous step
-        (one rank, or static peer halos): steps of DIFFERENT detectors may then
-        run on different streams (``step(stream=...)``)."""
-        return not self.stream and not self.pipeline and (not self.ctx.is_distributed or self.peer is not None)
+        """True when this detector's steps may run on any stream of the caller's
+        choosing (``step(stream=...)``) while OTHER detectors run on other
+        streams: no host-ordered collective is involved (one rank, static peer
+        halos, or device-signalled streaming halos). A stream-mode detector's
+        own steps still depend on each other, so the caller keeps each detector
+        on ONE stream."""
+        if self.pipeline:
+            return False
+        if self.stream:
+            return not self.ctx.is_distributed or self.slink is not None
+        return not self.ctx.is_distributed or self.peer is not None
 
     def step(self, stream: Optional[int] = None) -> torch.Tensor:
         """Exchange halos and convolve every owned row; returns the output slab.
@@ -263,7 +270,7 @@ class SlabEdgeDetector:
 
     def _step(self, stream: Optional[int] = None) -> torch.Tensor:
         if self.stream:
-            return self._step_stream()
+            return self._step_stream(stream if self.independent_steps else None)
         if self.pipeline:
             return self._step_pipelined()
         if stream is not None and self.independent_steps:
@@ -284,10 +291,11 @@ class SlabEdgeDetector:
             self._all(st)
         return self.out
 
-    def _step_stream(self) -> torch.Tensor:
+    def _step_stream(self, stream: Optional[int] = None) -> torch.Tensor:
         k = self._sk + 1
         a = (k - 1) % 2
-        st = torch.cuda.current_stream(self.bufs[0].device).cuda_stream if self.bufs[0].is_cuda else None
+        st = stream if stream is not None else (
+            torch.cuda.current_stream(self.bufs[0].device).cuda_stream if self.bufs[0].is_cuda else None)
         if self.ctx.is_distributed:
             if self.slink is not None and self.slink.fused:
                 self.slink.conv(k, st)            # ONE launch: the edge waves carry the halo protocol

@@ -14,4 +14,5 @@ for r in 1 2; do
   MPX_CONV_BAND=4 bash tools/gpu.sh run s2_band4_$r 200 $B &&
   MPX_CONV_BAND=2 bash tools/gpu.sh run s2_band2_$r 200 $B || exit 1
 done &&
-LAB3_NCS=2,4,32 LAB3_GRIDS=0,2048,4096,8192,16384 bash tools/gpu.sh run lab3_grid 400 python -u tools/experiments/lab3_grid_sweep.py
+LAB3_NCS=2,4,32 LAB3_GRIDS=0,2048,4096,8192,16384 bash tools/gpu.sh run lab3_grid 400 python -u tools/experiments/lab3_grid_sweep.py &&
+bash tools/gpu.sh prof bench_trace -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
