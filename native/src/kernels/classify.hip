@@ -175,8 +175,33 @@ __device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_
 constexpr int kAmbCap = 512;
 
 // NQ: 16-B vectors (4 pixels each) per thread and loop trip; nvec counts
-// groups of NQ vectors.
-template <int NQ>
+// groups of NQ vectors. OPT (tuning, MPX_CLS_OPT): bit 1 non-temporal loads,
+// bit 2 non-temporal stores, bit 4 wave-contiguous vectors (vector qq of a
+// thread at wave base * NQ + 64 qq + lane, so every load / store instruction
+// covers 1 KiB of consecutive bytes; nvec must then be a multiple of 64).
+typedef uint32_t cls_u32x4 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take clang vectors
+template <int OPT>
+__device__ __forceinline__ uint4 cls_load(const uint4 *p) {
+    if constexpr (OPT & 1) {
+        const cls_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const cls_u32x4 *>(p));
+        return make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return *p;
+}
+template <int OPT>
+__device__ __forceinline__ void cls_store(uint4 *p, uint4 x) {
+    if constexpr (OPT & 2)
+        __builtin_nontemporal_store(cls_u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<cls_u32x4 *>(p));
+    else
+        *p = x;
+}
+template <int NQ, int OPT>
+__device__ __forceinline__ int64_t cls_vec(int64_t i, int qq) {
+    if constexpr (OPT & 4) return (i & ~63ll) * NQ + qq * 64 + (i & 63);
+    return i * NQ + qq;
+}
+
+template <int NQ, int OPT = 0>
 __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, FastParams fp, uint32_t *amb) {
     constexpr int NP = 4 * NQ;  // pixels per thread and trip
@@ -193,7 +218,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
     // the prefetch each step exposes a full HBM round trip)
     uint4 qn[NQ];
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) qn[qq] = i < nvec ? v[i * NQ + qq] : uint4{};
+    for (int qq = 0; qq < NQ; ++qq) qn[qq] = i < nvec ? cls_load<OPT>(v + cls_vec<NQ, OPT>(i, qq)) : uint4{};
     for (; i < nvec; i += stride) {
         uint32_t px[NP];
 #pragma unroll
@@ -205,7 +230,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         }
         if (i + stride < nvec) {
 #pragma unroll
-            for (int qq = 0; qq < NQ; ++qq) qn[qq] = v[(i + stride) * NQ + qq];
+            for (int qq = 0; qq < NQ; ++qq) qn[qq] = cls_load<OPT>(v + cls_vec<NQ, OPT>(i + stride, qq));
         }
         f2_t f[NP / 2][9];
 #pragma unroll
@@ -260,7 +285,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             if (__builtin_expect(!decided(B[k], S[k], fp.T2), 0)) {
                 const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count (one global add at the end)
                 if (slot < (uint32_t)kAmbCap) {  // deferred
-                    s_amb[slot] = i * NP + k;
+                    s_amb[slot] = cls_vec<NQ, OPT>(i, k >> 2) * 4 + (k & 3);
                     s_ambpx[slot] = px[k];
                 } else {
                     o[k] = classify_direct(px[k], nc, cp);
@@ -269,7 +294,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         }
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq)
-            v[i * NQ + qq] = make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]);
+            cls_store<OPT>(v + cls_vec<NQ, OPT>(i, qq), make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]));
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
@@ -567,86 +592,197 @@ __device__ __forceinline__ void rank_regs(const i32x16 &da, const i32x16 &db, in
     (rank_reg<NREG, R>(da, db, B, S), ...);
 }
 
+// Per-wave constants of the mfma8 GEMM (weights, accumulator init, byte
+// selectors of the feature packing).
+struct Mfma8Lane {
+    long wa, wb;
+    i32x16 cinit;
+    int add, h;
+    uint32_t selA, selB, selD;
+};
+
+__device__ __forceinline__ Mfma8Lane mfma8_lane(const I8Params &ip, int lane) {
+    Mfma8Lane L;
+    L.h = lane >> 5;
+    const int col = lane & 31;
+    L.wa = (long)ip.a[col][L.h];
+    L.wb = (long)ip.b[col][L.h];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) L.cinit[r] = ip.c[(r & 3) + 8 * (r >> 2) + 4 * L.h];
+    // half 0 packs byte 1 of P + 128 (the h limbs), half 1 byte 0 of P (the l limbs)
+    L.add = L.h ? 0 : 128;
+    const uint32_t sel = L.h ? 0u : 1u;
+    L.selA = sel | ((4u + sel) << 8) | (0x0Cu << 16) | (0x0Cu << 24);  // [x.s, y.s, 0, 0]
+    L.selB = 0x0Cu | (0x0Cu << 8) | (sel << 16) | ((4u + sel) << 24);   // [0, 0, x.s, y.s]
+    L.selD = 0x0Cu | (0x0Cu << 8) | (0u << 16) | ((L.h ? 0x0Cu : 4u) << 24);  // [0, 0, x6, g | 0]
+    return L;
+}
+
+// One 128-pixel chunk (the 16 B of pixels 4 col .. +3 in every lane): the
+// provisional output (class of the best int32 key in the alpha byte) and a
+// mask of the pixels whose top-2 margin is within T2 (valid in half-wave 0).
 template <int NREG>
-__global__ __launch_bounds__(256) void classify_mfma8_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
+__device__ __forceinline__ uint32_t mfma8_chunk(const uint4 &q, const Mfma8Lane &L, int32_t T2, uint4 &o) {
+    const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+    int32_t rb[4], rs[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int p = (int)(px[m] ^ 0x80808080u);  // bytes - 128, sign-extended below
+        const int r = __builtin_amdgcn_sbfe(p, 0, 8), g = __builtin_amdgcn_sbfe(p, 8, 8),
+                  b = __builtin_amdgcn_sbfe(p, 16, 8);
+        const uint32_t P0 = (uint32_t)(r * r + L.add), P1 = (uint32_t)(g * g + L.add), P2 = (uint32_t)(b * b + L.add);
+        const uint32_t P3 = (uint32_t)(r * g + L.add), P4 = (uint32_t)(r * b + L.add), P5 = (uint32_t)(g * b + L.add);
+        const uint32_t x6 = (uint32_t)(L.h ? b : r);
+        const uint32_t d0 = __builtin_amdgcn_perm(P1, P0, L.selA) | __builtin_amdgcn_perm(P3, P2, L.selB);
+        const uint32_t d1 = __builtin_amdgcn_perm(P5, P4, L.selA) | __builtin_amdgcn_perm((uint32_t)g, x6, L.selD);
+        const long feat = (long)(((uint64_t)d1 << 32) | d0);
+        const i32x16 da = __builtin_amdgcn_mfma_i32_32x32x16_i8(L.wa, feat, i32x16{}, 0, 0, 0);
+        const i32x16 db = __builtin_amdgcn_mfma_i32_32x32x16_i8(L.wb, feat, L.cinit, 0, 0, 0);
+        int32_t B = INT32_MAX, S = INT32_MAX;
+        // key = ((da << 8) + db) << 5 | tag as two v_lshl_add_u32:
+        // (da << 13) + tag first, then (db << 5) + that
+        rank_regs<NREG>(da, db, B, S, std::make_integer_sequence<int, 16>{});
+        B |= 4 * L.h;  // row tags (r & 3) + 8 (r >> 2) never set bit 2
+        S |= 4 * L.h;
+        const auto sb = __builtin_amdgcn_permlane32_swap((uint32_t)B, (uint32_t)B, false, false);
+        const auto ss = __builtin_amdgcn_permlane32_swap((uint32_t)S, (uint32_t)S, false, false);
+        const int32_t B0 = (int32_t)sb[0], B1 = (int32_t)sb[1], S0 = (int32_t)ss[0], S1 = (int32_t)ss[1];
+        rb[m] = min(B0, B1);
+        rs[m] = min(max(B0, B1), min(S0, S1));
+    }
+    uint32_t *op = &o.x;
+    uint32_t undecided = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        op[m] = (px[m] & 0x00ffffffu) | (((uint32_t)rb[m] & 31u) << 24);
+        // exact integers: the tag bits are below the shift
+        if ((rs[m] >> 5) - (rb[m] >> 5) <= T2) undecided |= 1u << m;
+    }
+    return undecided;
+}
+
+// WIN = false: each chunk is stored as soon as it is ranked and the undecided
+// pixels are re-stored one by one after the block's grid-stride loop — after
+// their lines left L2, so every fix-up is a partial-line HBM write (56-71 MiB
+// per 8192^2 image, kernels_r3.md).
+// WIN = true (production): a block ranks kWin8 chunks per wave into LDS,
+// resolves that window's undecided pixels there (all lanes busy on the fp64
+// chain), and only then stores the window: every output byte is written once,
+// in whole 512-B chunk runs.
+constexpr int kWin8 = 4;
+constexpr int kAmb8WinCap = 1024;  // undecided pixels per window (of 4 x 4 x 128)
+
+template <int NREG, bool WIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void classify_mfma8_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
                                                              ClassParams cp, I8Params ip, uint32_t *amb) {
-    __shared__ int64_t s_amb[kAmb8Cap];
-    __shared__ uint32_t s_ambpx[kAmb8Cap];
-    __shared__ uint32_t s_namb;
-    if (threadIdx.x == 0) s_namb = 0;
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5;
     const int col = lane & 31;
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const long wa = (long)ip.a[col][h], wb = (long)ip.b[col][h];
-    i32x16 cinit;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) cinit[r] = ip.c[(r & 3) + 8 * (r >> 2) + 4 * h];
-    // half 0 packs byte 1 of P + 128 (the h limbs), half 1 byte 0 of P (the l limbs)
-    const int add = h ? 0 : 128;
-    const uint32_t sel = h ? 0u : 1u;
-    const uint32_t selA = sel | ((4u + sel) << 8) | (0x0Cu << 16) | (0x0Cu << 24);  // [x.s, y.s, 0, 0]
-    const uint32_t selB = 0x0Cu | (0x0Cu << 8) | (sel << 16) | ((4u + sel) << 24);   // [0, 0, x.s, y.s]
-    const uint32_t selD = 0x0Cu | (0x0Cu << 8) | (0u << 16) | ((h ? 0x0Cu : 4u) << 24);  // [0, 0, x6, g | 0]
+    const Mfma8Lane L = mfma8_lane(ip, lane);
     uint4 *v = reinterpret_cast<uint4 *>(img);
-    int64_t ch = wave;
-    uint4 qn = ch < nchunks ? v[ch * 32 + col] : uint4{};
-    for (; ch < nchunks; ch += nwaves) {
-        const uint4 q = qn;
-        if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
-        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
-        int32_t rb[4], rs[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int p = (int)(px[m] ^ 0x80808080u);  // bytes - 128, sign-extended below
-            const int r = __builtin_amdgcn_sbfe(p, 0, 8), g = __builtin_amdgcn_sbfe(p, 8, 8),
-                      b = __builtin_amdgcn_sbfe(p, 16, 8);
-            const uint32_t P0 = (uint32_t)(r * r + add), P1 = (uint32_t)(g * g + add), P2 = (uint32_t)(b * b + add);
-            const uint32_t P3 = (uint32_t)(r * g + add), P4 = (uint32_t)(r * b + add), P5 = (uint32_t)(g * b + add);
-            const uint32_t x6 = (uint32_t)(h ? b : r);
-            const uint32_t d0 = __builtin_amdgcn_perm(P1, P0, selA) | __builtin_amdgcn_perm(P3, P2, selB);
-            const uint32_t d1 = __builtin_amdgcn_perm(P5, P4, selA) | __builtin_amdgcn_perm((uint32_t)g, x6, selD);
-            const long feat = (long)(((uint64_t)d1 << 32) | d0);
-            const i32x16 da = __builtin_amdgcn_mfma_i32_32x32x16_i8(wa, feat, i32x16{}, 0, 0, 0);
-            const i32x16 db = __builtin_amdgcn_mfma_i32_32x32x16_i8(wb, feat, cinit, 0, 0, 0);
-            int32_t B = INT32_MAX, S = INT32_MAX;
-            // key = ((da << 8) + db) << 5 | tag as two v_lshl_add_u32:
-            // (da << 13) + tag first, then (db << 5) + that
-            rank_regs<NREG>(da, db, B, S, std::make_integer_sequence<int, 16>{});
-            B |= 4 * h;  // row tags (r & 3) + 8 (r >> 2) never set bit 2
-            S |= 4 * h;
-            const auto sb = __builtin_amdgcn_permlane32_swap((uint32_t)B, (uint32_t)B, false, false);
-            const auto ss = __builtin_amdgcn_permlane32_swap((uint32_t)S, (uint32_t)S, false, false);
-            const int32_t B0 = (int32_t)sb[0], B1 = (int32_t)sb[1], S0 = (int32_t)ss[0], S1 = (int32_t)ss[1];
-            rb[m] = min(B0, B1);
-            rs[m] = min(max(B0, B1), min(S0, S1));
-        }
-        if (h == 0) {
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    if constexpr (!WIN) {
+        __shared__ int64_t s_amb[kAmb8Cap];
+        __shared__ uint32_t s_ambpx[kAmb8Cap];
+        __shared__ uint32_t s_namb;
+        if (threadIdx.x == 0) s_namb = 0;
+        __syncthreads();
+        const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        int64_t ch = wave;
+        uint4 qn = ch < nchunks ? v[ch * 32 + col] : uint4{};
+        for (; ch < nchunks; ch += nwaves) {
+            const uint4 q = qn;
+            if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
             uint4 o;
-            uint32_t *op = &o.x;
+            const uint32_t und = mfma8_chunk<NREG>(q, L, ip.T2, o);
+            if (h == 0) {
+                const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+                uint32_t *op = &o.x;
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                op[m] = (px[m] & 0x00ffffffu) | (((uint32_t)rb[m] & 31u) << 24);
-                // exact integers: the tag bits are below the shift
-                if (__builtin_expect((rs[m] >> 5) - (rb[m] >> 5) <= ip.T2, 0)) {
-                    const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count
-                    if (slot < (uint32_t)kAmb8Cap) {
-                        s_amb[slot] = (ch * 32 + col) * 4 + m;
-                        s_ambpx[slot] = px[m];
-                    } else {
-                        op[m] = classify_direct(px[m], nc, cp);
+                for (int m = 0; m < 4; ++m) {
+                    if (__builtin_expect((und >> m) & 1u, 0)) {
+                        const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count
+                        if (slot < (uint32_t)kAmb8Cap) {
+                            s_amb[slot] = (ch * 32 + col) * 4 + m;
+                            s_ambpx[slot] = px[m];
+                        } else {
+                            op[m] = classify_direct(px[m], nc, cp);
+                        }
+                    }
+                }
+                v[ch * 32 + col] = o;
+            }
+        }
+        __syncthreads();
+        const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
+        if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
+        for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
+    } else {
+        constexpr int NW = 4;  // waves per block (launch_bounds 256)
+        __shared__ uint4 s_out[kWin8][NW][32];
+        __shared__ uint16_t s_ambi[kAmb8WinCap];  // (t, wave, col, m) of an undecided pixel
+        __shared__ uint32_t s_ambpx[kAmb8WinCap];
+        __shared__ uint32_t s_namb;
+        const int wl = threadIdx.x >> 6;
+        if (threadIdx.x == 0) s_namb = 0;
+        __syncthreads();
+        const int64_t ch0 = (int64_t)blockIdx.x * NW;  // the block's first chunk; wave wl takes ch0 + wl + t nwaves
+        // block-uniform trip count (every wave passes every barrier)
+        const int64_t trips = ch0 < nchunks ? (nchunks - ch0 + nwaves - 1) / nwaves : 0;
+        uint32_t total = 0;
+        uint4 qn = ch0 + wl < nchunks ? v[(ch0 + wl) * 32 + col] : uint4{};
+        for (int64_t t0 = 0; t0 < trips; t0 += kWin8) {
+#pragma unroll
+            for (int tt = 0; tt < kWin8; ++tt) {
+                const int64_t ch = ch0 + wl + (t0 + tt) * nwaves;
+                if (ch < nchunks) {  // wave-uniform
+                    const uint4 q = qn;
+                    if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
+                    uint4 o;
+                    const uint32_t und = mfma8_chunk<NREG>(q, L, ip.T2, o);
+                    if (h == 0) {
+                        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+                        uint32_t *op = &o.x;
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            if (__builtin_expect((und >> m) & 1u, 0)) {
+                                const uint32_t slot = atomicAdd(&s_namb, 1u);
+                                if (slot < (uint32_t)kAmb8WinCap) {
+                                    s_ambi[slot] = (uint16_t)((((tt * NW + wl) * 32 + col) << 2) | m);
+                                    s_ambpx[slot] = px[m];
+                                } else {
+                                    op[m] = classify_direct(px[m], nc, cp);
+                                }
+                            }
+                        }
+                        s_out[tt][wl][col] = o;
                     }
                 }
             }
-            v[ch * 32 + col] = o;
+            __syncthreads();
+            const uint32_t na = s_namb;
+            const uint32_t nd = min(na, (uint32_t)kAmb8WinCap);
+            for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+                const uint32_t e = s_ambi[j];
+                reinterpret_cast<uint32_t *>(&s_out[0][0][0])[e] = classify_direct(s_ambpx[j], nc, cp);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                total += na;
+                s_namb = 0;
+            }
+            // the window's chunks, whole: thread -> (tt, wave, col) over 512 uint4
+#pragma unroll
+            for (int k = 0; k < kWin8 * NW * 32 / 256; ++k) {
+                const int e = threadIdx.x + k * 256;
+                const int tt = e / (NW * 32), w2 = (e / 32) % NW, c2 = e % 32;
+                const int64_t ch = ch0 + w2 + (t0 + tt) * nwaves;
+                if (t0 + tt < trips && ch < nchunks) v[ch * 32 + c2] = s_out[tt][w2][c2];
+            }
+            __syncthreads();  // s_out and s_namb are rewritten by the next window
         }
+        if (amb && threadIdx.x == 0 && total) atomicAdd(amb, total);  // one global add per block
     }
-    __syncthreads();
-    const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
-    if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
-    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
 }
 
 // ---------------------------------------------------------------------------
@@ -925,18 +1061,30 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
     if (chosen == MPX_CLS_MFMA8) {
         const int64_t nchunks = npix / 128;
+        // MPX_CLS_MFMA8_WIN=0: the round-3 schedule (fix-ups after the loop), A/B
+        static const bool win = [] {
+            const char *e = std::getenv("MPX_CLS_MFMA8_WIN");
+            return !(e && e[0] == '0');
+        }();
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;
             const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+#define MPX_MFMA8_LAUNCH(NREG)                                                                                       \
+    do {                                                                                                             \
+        if (win)                                                                                                     \
+            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, true>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb); \
+        else                                                                                                         \
+            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, false>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb); \
+    } while (0)
             if (nc <= 8)
-                hipLaunchKernelGGL(classify_mfma8_kernel<4>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+                MPX_MFMA8_LAUNCH(4);
             else if (nc <= 16)
-                hipLaunchKernelGGL(classify_mfma8_kernel<8>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+                MPX_MFMA8_LAUNCH(8);
             else if (nc <= 24)  // registers 0-11 hold classes 0-23
-                hipLaunchKernelGGL(classify_mfma8_kernel<12>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb);
+                MPX_MFMA8_LAUNCH(12);
             else
-                hipLaunchKernelGGL(classify_mfma8_kernel<16>, dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8,
-                                   amb);
+                MPX_MFMA8_LAUNCH(16);
+#undef MPX_MFMA8_LAUNCH
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             done = nchunks * 128;
         }
@@ -975,7 +1123,14 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const char *e = std::getenv("MPX_CLS_NQ");
             return (e && e[0] == '1') ? 1 : 2;
         }();
-        const int64_t nvec = npix / (4 * nq);
+        // memory-policy / layout variant (fast32 OPT bits), A/B only for now
+        static const int opt = [] {
+            const char *e = std::getenv("MPX_CLS_OPT");
+            const int o = e ? std::atoi(e) : 0;
+            return o >= 0 && o <= 7 ? o : 0;
+        }();
+        int64_t nvec = npix / (4 * nq);
+        if (opt & 4) nvec &= ~63ll;  // whole waves only; the rest goes DIRECT
         if (nvec > 0) {
             // the kernel is compiled for 256-thread workgroups
             // (__launch_bounds__(256)): a larger caller block would not launch
@@ -983,7 +1138,19 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const int blk = block > 0 ? std::min(block, 256) : 256;
             const int64_t blocks = (nvec + blk - 1) / blk;
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, blk) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
-            if (nq == 2)
+            // wave-contiguous vectors need waves that start at multiples of 64 threads
+            const int o = (opt & 4) && blk % 64 != 0 ? opt & 3 : opt;
+            if (nq == 2 && o != 0) {
+                switch (o) {
+#define MPX_FAST32_OPT(k)                                                                                           \
+    case k:                                                                                                         \
+        hipLaunchKernelGGL((classify_fast32_kernel<2, k>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);  \
+        break;
+                    MPX_FAST32_OPT(1) MPX_FAST32_OPT(2) MPX_FAST32_OPT(3) MPX_FAST32_OPT(4) MPX_FAST32_OPT(5)
+                    MPX_FAST32_OPT(6) MPX_FAST32_OPT(7)
+#undef MPX_FAST32_OPT
+                }
+            } else if (nq == 2)
                 hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             else
                 hipLaunchKernelGGL(classify_fast32_kernel<1>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);

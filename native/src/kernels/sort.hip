@@ -693,8 +693,18 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 // waves per SIMD fit the LDS but not the registers: 80 VGPRs spill 280 B per
 // lane). TPB = 256 (variant 8): 4096-key tiles, 4 blocks per CU — twice the
 // independent barrier domains per CU for the same waves.
-template <int IN_MODE, int OUT_MODE, int TPB = kRThreads>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void radix_scatter_lean_kernel(
+// RANK 1 (variant 9): every lane takes its rank straight from a returning LDS
+// add on its wave's digit counter (ds_add_rtn_u32, one LDS instruction per
+// slice instead of the table's or / read / clear plus the counter read and the
+// leaders' add). Stable only if the LDS applies one instruction's same-address
+// lanes in ascending lane order — the GPU sort suite checks that on every
+// variant-9 sort.
+// KNOCK (tuning probe, mpx_sort_scatter_probe; output NOT sorted): bit 1 stages
+// at lane-linear positions, 2 skips the counter read, 4 the leaders' add, 8 the
+// peer-mask table (own-lane masks), 16 the write-out's digit lookup — same
+// loads and stores, so the counters attribute LDS conflicts and time per step.
+template <int IN_MODE, int OUT_MODE, int TPB = kRThreads, int RANK = 0, int KNOCK = 0, int WPE = 4>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void radix_scatter_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
     constexpr int NW = TPB / 64, TILE = TPB * kRPer;  // kRWaveKeys keys per wave either way
@@ -768,26 +778,36 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
                 if (i0 + e * 64u >= n32) key[e] = 0xffffffffu;
         }
         uint32_t rank[kRPer];
+        if constexpr (RANK == 1) {
 #pragma unroll
-        for (int g = 0; g < kRPer; g += 4) {  // 4 slices in flight: bounds the live LDS results
-            uint32_t lo[4], hi[4], before[4];
+            for (int e = 0; e < kRPer; ++e) rank[e] = atomicAdd(&s_cnt[w][(key[e] >> shift) & 255u], 1u);
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t d = (key[g + e] >> shift) & 255u;
-                atomicOr(myword + 2 * d, mybit);
-                lo[e] = tbl[2 * d];
-                hi[e] = tbl[2 * d + 1];
-                myword[2 * d] = 0;
-                before[e] = s_cnt[w][d];
-                // one add per distinct digit (its lowest lane): 64 lanes adding
-                // to one counter would serialise on skewed digits (the top byte
-                // of normally distributed floats takes a handful of values)
-                const uint64_t m = ((uint64_t)hi[e] << 32) | lo[e];
-                if (lanes_below(m) == 0) atomicAdd(&s_cnt[w][d], (uint32_t)__popcll(m));
+            for (int g = 0; g < kRPer; g += 4) {  // 4 slices in flight: bounds the live LDS results
+                uint32_t lo[4], hi[4], before[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t d = (key[g + e] >> shift) & 255u;
+                    if constexpr (KNOCK & 8) {
+                        lo[e] = lane < 32 ? mybit : 0u;
+                        hi[e] = lane < 32 ? 0u : mybit;
+                    } else {
+                        atomicOr(myword + 2 * d, mybit);
+                        lo[e] = tbl[2 * d];
+                        hi[e] = tbl[2 * d + 1];
+                        myword[2 * d] = 0;
+                    }
+                    before[e] = (KNOCK & 2) ? 0u : s_cnt[w][d];
+                    // one add per distinct digit (its lowest lane): 64 lanes adding
+                    // to one counter would serialise on skewed digits (the top byte
+                    // of normally distributed floats takes a handful of values)
+                    const uint64_t m = ((uint64_t)hi[e] << 32) | lo[e];
+                    if (!(KNOCK & 4) && lanes_below(m) == 0) atomicAdd(&s_cnt[w][d], (uint32_t)__popcll(m));
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    rank[g + e] = before[e] + __builtin_amdgcn_mbcnt_hi(hi[e], __builtin_amdgcn_mbcnt_lo(lo[e], 0u));
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                rank[g + e] = before[e] + __builtin_amdgcn_mbcnt_hi(hi[e], __builtin_amdgcn_mbcnt_lo(lo[e], 0u));
         }
         lds_barrier();
         uint32_t cnt = 0, wexcl[NW];
@@ -806,7 +826,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
         }
         lds_barrier();
 #pragma unroll
-        for (int e = 0; e < kRPer; ++e) s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rank[e]] = key[e];
+        for (int e = 0; e < kRPer; ++e) {
+            const uint32_t rk = rank[e];
+            if constexpr (KNOCK & 1)
+                s_keys[w * kRWaveKeys + e * 64 + lane] = key[e] + (s_cnt[w][0] + rk == ~0u);  // keeps rank live
+            else
+                s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rk] = key[e];
+        }
         lds_barrier();
         // this wave's staging reads of its own row are done (program order)
 #pragma unroll
@@ -816,8 +842,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4))) void r
             for (int j = 0; j < TILE / TPB; ++j) {
                 const int i = t + j * TPB;
                 const uint32_t k = s_keys[i];
-                __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout,
-                                                      (int)((s_gbase[(k >> shift) & 255u] + (uint32_t)i) * 4u), 0, 0);
+                const uint32_t gd = (KNOCK & 16) ? s_gbase[0] : s_gbase[(k >> shift) & 255u];
+                __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)((gd + (uint32_t)i) * 4u), 0, 0);
             }
         } else {
             for (int j = 0; j < TILE / TPB; ++j) {
@@ -1022,7 +1048,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // (one tile per block), 4 = reduce-then-scan with the round-2 persistent
 // scatter (radix_scatter_kernel, 256-thread scan; same-process A/B), 7 = the
 // lean persistent scatter (radix_scatter_lean_kernel, 8192-key tiles), 8 = 7
-// on 4096-key tiles (256-thread blocks, 4 per CU). Retired after round-3
+// on 4096-key tiles (256-thread blocks, 4 per CU), 9 = 7 ranked by returning
+// LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU. Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1034,22 +1061,25 @@ constexpr int64_t kTile4kMaxN = (int64_t)1 << 24;    // variant 8 up to here (me
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
-template <int TPB = kRThreads>
+template <int TPB = kRThreads, int RANK = 0, int WPE = 4>
 void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
                  const uint32_t *tot, const uint32_t *offs, int ntiles) {
     const dim3 g((unsigned)blocks), b(TPB);
     const int sh = 8 * p;
     const bool f = mode == kRawF32;
+#define MPX_LEAN(I, O) \
+    hipLaunchKernelGGL((radix_scatter_lean_kernel<I, O, TPB, RANK, 0, WPE>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles)
     if (p == 0 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawF32, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        MPX_LEAN(kRawF32, kRawKeys);
     else if (p == 0)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawI32, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        MPX_LEAN(kRawI32, kRawKeys);
     else if (p == 3 && f)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawF32, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        MPX_LEAN(kRawKeys, kRawF32);
     else if (p == 3)
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawI32, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        MPX_LEAN(kRawKeys, kRawI32);
     else
-        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, TPB>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles);
+        MPX_LEAN(kRawKeys, kRawKeys);
+#undef MPX_LEAN
 }
 
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
@@ -1060,7 +1090,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // tiles stop meeting in L2; profiles/lab5_sort.md)
     if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 8 : 7;
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
-    const int ntiles = variant == 8 ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
+    const int ntiles = variant == 8 || variant == 10 ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
         hipLaunchKernelGGL(radix_hist_kernel,
@@ -1082,7 +1112,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                r.ctr + p, r.err, ntiles);
         } else {
             // offsets in status[0 .. 256 * ntiles), digit totals in hist[0 .. 256)
-            if (variant == 8)
+            if (variant == 8 || variant == 10)
                 hipLaunchKernelGGL(radix_count_kernel<kRTileSmall>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
                                    n, 8 * p, in_mode, r.status, ntiles);
             else
@@ -1099,6 +1129,15 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 const int rounded = (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs;
                 if (variant == 7)
                     launch_lean(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
+                else if (variant == 9)
+                    launch_lean<kRThreads, 1>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status,
+                                              ntiles);
+                else if (variant == 10)
+                    launch_lean<kRThreads / 2, 1>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
+                                                  r.status, ntiles);
+                else if (variant == 11)  // 3 blocks (24 waves) per CU: the returning-add ranking frees the table's LDS
+                    launch_lean<kRThreads, 1, 6>(p, mode, std::min(kNumCUs * 3, rounded), s, src, dst, n, r.hist,
+                                                 r.status, ntiles);
                 else
                     launch_lean<kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
                                                r.status, ntiles);
@@ -1238,6 +1277,43 @@ int sort_alloc(void *data, int64_t n, int dtype, void *stream) {
     return rc;
 }
 
+// Scatter probe (tools/experiments/sort_probe.py): count + scan + one lean
+// scatter per digit on the UNCHANGED input (every pass sees the same uniform
+// keys, src -> workspace), with the KNOCK bits of radix_scatter_lean_kernel.
+// The output is not sorted; only the counters and the kernel times matter.
+template <int KNOCK>
+int scatter_probe_k(const uint32_t *x, int64_t n, void *ws, hipStream_t s) {
+    const RadixWs r = radix_layout(ws, n);
+    const int ntiles = (int)r.tiles;
+    const int blocks = std::min(kNumCUs * 2, (ntiles + kNumXCDs - 1) / kNumXCDs * kNumXCDs);
+    for (int p = 0; p < 4; ++p) {
+        hipLaunchKernelGGL(radix_count_kernel<kRTile>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, x, n, 8 * p,
+                           (int)kRawKeys, r.status, ntiles);
+        hipLaunchKernelGGL(radix_scan1024_kernel, dim3(256), dim3(kScanThreads), 0, s, r.status, ntiles, r.hist);
+        hipLaunchKernelGGL((radix_scatter_lean_kernel<kRawKeys, kRawKeys, kRThreads, 0, KNOCK>), dim3((unsigned)blocks),
+                           dim3(kRThreads), 0, s, x, r.tmp, n, 8 * p, r.hist, r.status, ntiles);
+        MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+    }
+    return MPX_OK;
+}
+
+int scatter_probe(const void *x, int64_t n, void *ws, int64_t ws_bytes, int knock, void *stream) {
+    MPX_CHECK_ARG(x && ws && n > kOnesweepMaxN && n < kRadixMaxN, "probe: 2^18 < n < 2^30 keys and a workspace");
+    MPX_CHECK_ARG(ws_bytes >= (int64_t)radix_ws_bytes(n), "probe: workspace smaller than mpx_sort_workspace_bytes");
+    const uint32_t *k = static_cast<const uint32_t *>(x);
+    hipStream_t s = as_stream(stream);
+    switch (knock) {
+        case 0: return scatter_probe_k<0>(k, n, ws, s);
+        case 1: return scatter_probe_k<1>(k, n, ws, s);
+        case 6: return scatter_probe_k<6>(k, n, ws, s);
+        case 12: return scatter_probe_k<12>(k, n, ws, s);
+        case 14: return scatter_probe_k<14>(k, n, ws, s);
+        case 16: return scatter_probe_k<16>(k, n, ws, s);
+        case 31: return scatter_probe_k<31>(k, n, ws, s);
+        default: set_error("probe knock %d: 0, 1, 6, 12, 14, 16 or 31", knock); return MPX_ERR_ARG;
+    }
+}
+
 MPX_MODULE_ANCHOR(sort)
 
 }  // namespace mpx
@@ -1259,9 +1335,14 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 8 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 or 8", variant);
+    if (variant < 0 || variant > 11 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7, 8, 9, 10 or 11", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
+}
+
+extern "C" int mpx_sort_scatter_probe(const void *data, int64_t n, void *workspace, int64_t workspace_bytes, int knock,
+                                      void *stream) {
+    return mpx::scatter_probe(data, n, workspace, workspace_bytes, knock, stream);
 }

@@ -250,12 +250,14 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8, 9])
 @pytest.mark.parametrize("kind", ["int", "float"])
 @pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
-    """Every radix schedule (1 onesweep look-back, 2 reduce-then-scan, 3 the
-    same with the persistent prefetching scatter) against the total order,
+    """Every radix schedule (1 onesweep look-back, 2 reduce-then-scan, 4 / 7 / 8
+    the same with persistent prefetching scatters, 9 the lean scatter ranked by
+    returning LDS adds — stable only if one instruction's same-address lanes
+    apply in lane order, which this checks) against the total order,
     independent of which one AUTO picks at this size."""
     from cuda_mpi_openmp_amd import _native
 
@@ -297,6 +299,16 @@ def test_retired_sort_variants_are_refused():
     from cuda_mpi_openmp_amd import _native
 
     L = _native.lib()
-    for v in (3, 5, 6, 9, -1):
+    for v in (3, 5, 6, 10, -1):
         assert L.mpx_sort_variant(None, 1 << 20, 0, None, 0, v, None) != 0
         assert b"sort variant" in L.mpx_last_error()
+
+
+def test_scatter_probe_refuses_bad_args():
+    """The tuning probe (tools/experiments/sort_probe.py) checks its inputs
+    before any launch: unknown knock masks and missing workspaces."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    assert L.mpx_sort_scatter_probe(None, 1 << 20, None, 0, 0, None) != 0
+    assert b"probe" in L.mpx_last_error()
