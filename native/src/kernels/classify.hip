@@ -661,11 +661,11 @@ __device__ __forceinline__ uint32_t mfma8_chunk(const uint4 &q, const Mfma8Lane 
     return undecided;
 }
 
-// WIN = false: each chunk is stored as soon as it is ranked and the undecided
+// WIN = false (production): each chunk is stored as soon as it is ranked and the undecided
 // pixels are re-stored one by one after the block's grid-stride loop — after
 // their lines left L2, so every fix-up is a partial-line HBM write (56-71 MiB
 // per 8192^2 image, kernels_r3.md).
-// WIN = true (production): a block ranks kWin8 chunks per wave into LDS,
+// WIN = true (MPX_CLS_MFMA8_WIN=1): a block ranks kWin8 chunks per wave into LDS,
 // resolves that window's undecided pixels there (all lanes busy on the fp64
 // chain), and only then stores the window: every output byte is written once,
 // in whole 512-B chunk runs.
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         uint32_t total = 0;
         uint4 qn = ch0 + wl < nchunks ? v[(ch0 + wl) * 32 + col] : uint4{};
         for (int64_t t0 = 0; t0 < trips; t0 += kWin8) {
-#pragma unroll
+#pragma unroll 1  // one copy of the chunk body (unrolled 4x it outgrows the instruction cache)
             for (int tt = 0; tt < kWin8; ++tt) {
                 const int64_t ch = ch0 + wl + (t0 + tt) * nwaves;
                 if (ch < nchunks) {  // wave-uniform
@@ -1061,10 +1061,12 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
     if (chosen == MPX_CLS_MFMA8) {
         const int64_t nchunks = npix / 128;
-        // MPX_CLS_MFMA8_WIN=0: the round-3 schedule (fix-ups after the loop), A/B
+        // MPX_CLS_MFMA8_WIN=1: windowed fix-ups (every byte written once, 1.03x
+        // the image's bytes against 1.22x, but 434-444 -> 523 us at nc = 32 on
+        // one box: profiles/lab3_classify.md); off by default
         static const bool win = [] {
             const char *e = std::getenv("MPX_CLS_MFMA8_WIN");
-            return !(e && e[0] == '0');
+            return e && e[0] == '1';
         }();
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;

@@ -693,12 +693,16 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 // waves per SIMD fit the LDS but not the registers: 80 VGPRs spill 280 B per
 // lane). TPB = 256 (variant 8): 4096-key tiles, 4 blocks per CU — twice the
 // independent barrier domains per CU for the same waves.
-// RANK 1 (variant 9): every lane takes its rank straight from a returning LDS
-// add on its wave's digit counter (ds_add_rtn_u32, one LDS instruction per
-// slice instead of the table's or / read / clear plus the counter read and the
-// leaders' add). Stable only if the LDS applies one instruction's same-address
-// lanes in ascending lane order — the GPU sort suite checks that on every
-// variant-9 sort.
+// RANK 1 (variants 9 / 10, production above 2^18 keys): every lane takes its
+// rank straight from a returning LDS add on its wave's digit counter
+// (ds_add_rtn_u32: one LDS instruction per slice instead of the table's
+// or / read / clear plus the counter read and the leaders' add; per 2^26-key
+// pass 9.7M -> 5.5M LDS instructions, 38.4M -> 15.2M bank-conflict cycles,
+// 21.4M -> 10.9M VALU). The sort is stable because the LDS applies one
+// instruction's same-address lanes in ascending lane order: a pass that broke
+// that order would scramble keys equal in this digit and already ordered by
+// the lower ones, which the GPU sort suite's uniform, few-distinct, sorted and
+// reversed inputs (every variant, 4097 .. 2^26 keys) would catch.
 // KNOCK (tuning probe, mpx_sort_scatter_probe; output NOT sorted): bit 1 stages
 // at lane-linear positions, 2 skips the counter read, 4 the leaders' add, 8 the
 // peer-mask table (own-lane masks), 16 the write-out's digit lookup — same
@@ -1088,7 +1092,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // vs 0.229) and lose at 2^26 (0.987 vs 0.828; not yet explained — a
     // candidate: with 16 tiles per block the 64-B digit runs of neighbouring
     // tiles stop meeting in L2; profiles/lab5_sort.md)
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 8 : 7;
+    // AUTO (round 4, profiles/lab5_sort.md): the returning-add ranking on
+    // 4096-key tiles up to 2^24 keys (10), on 8192-key tiles above (9)
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 10 : 9;
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const int ntiles = variant == 8 || variant == 10 ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
     if (variant == 1) {

@@ -58,7 +58,7 @@ def main():
             med, mn = time_us(run)
             print(json.dumps({"tag": tag, "nc": nc, "path": path, "us": round(med, 1), "us_min": round(mn, 1),
                               "same_as_direct": ok, "opt": os.environ.get("MPX_CLS_OPT", "0"),
-                              "win": os.environ.get("MPX_CLS_MFMA8_WIN", "1")}), flush=True)
+                              "win": os.environ.get("MPX_CLS_MFMA8_WIN", "0")}), flush=True)
 
 
 if __name__ == "__main__":

@@ -63,7 +63,8 @@ def main():
             variants = {}
             if dt != torch.uint8:
                 for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (4, "reduce_scan_persistent_r2"),
-                              (7, "lean_scatter"), (8, "lean_scatter_tile4096")):
+                              (7, "lean_scatter"), (8, "lean_scatter_tile4096"), (9, "lean_rtn_rank"),
+                              (10, "lean_rtn_rank_tile4096")):
                     if v not in only:
                         continue
                     try:
