@@ -707,7 +707,7 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 // at lane-linear positions, 2 skips the counter read, 4 the leaders' add, 8 the
 // peer-mask table (own-lane masks), 16 the write-out's digit lookup — same
 // loads and stores, so the counters attribute LDS conflicts and time per step.
-template <int IN_MODE, int OUT_MODE, int TPB = kRThreads, int RANK = 0, int KNOCK = 0, int WPE = 4>
+template <int IN_MODE, int OUT_MODE, int TPB = kRThreads, int RANK = 0, int KNOCK = 0, int WPE = 4, int PF = 1>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void radix_scatter_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, const uint32_t *__restrict__ offs, int ntiles) {
@@ -859,13 +859,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
     };
 
-    uint32_t a[kRPer], b[kRPer];
-    load_tile(a, tile);
-    for (; tile < t1; tile += per) {
-        if (tile + per < t1) load_tile(b, tile + per);  // in flight under this tile's work
-        do_tile(a, tile);
+    if constexpr (PF == 2) {
+        // two tiles in flight: three register sets in fixed roles (an
+        // unrolled rotation — a copy between sets would wait for the copied
+        // loads and shorten the prefetch back to one tile)
+        uint32_t a[kRPer], b[kRPer], c[kRPer];
+        load_tile(a, tile);
+        if (tile + per < t1) load_tile(b, tile + per);
+        for (;;) {
+            if (tile + 2 * per < t1) load_tile(c, tile + 2 * per);
+            do_tile(a, tile);
+            if ((tile += per) >= t1) break;
+            if (tile + 2 * per < t1) load_tile(a, tile + 2 * per);
+            do_tile(b, tile);
+            if ((tile += per) >= t1) break;
+            if (tile + 2 * per < t1) load_tile(b, tile + 2 * per);
+            do_tile(c, tile);
+            if ((tile += per) >= t1) break;
+        }
+    } else {
+        uint32_t a[kRPer], b[kRPer];
+        load_tile(a, tile);
+        for (; tile < t1; tile += per) {
+            if (tile + per < t1) load_tile(b, tile + per);  // in flight under this tile's work
+            do_tile(a, tile);
 #pragma unroll
-        for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+            for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+        }
     }
 }
 
@@ -1053,7 +1073,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // scatter (radix_scatter_kernel, 256-thread scan; same-process A/B), 7 = the
 // lean persistent scatter (radix_scatter_lean_kernel, 8192-key tiles), 8 = 7
 // on 4096-key tiles (256-thread blocks, 4 per CU), 9 = 7 ranked by returning
-// LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU. Retired after round-3
+// LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
+// 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1065,14 +1086,14 @@ constexpr int64_t kTile4kMaxN = (int64_t)1 << 24;    // variant 8 up to here (me
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
-template <int TPB = kRThreads, int RANK = 0, int WPE = 4>
+template <int TPB = kRThreads, int RANK = 0, int WPE = 4, int PF = 1>
 void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src, uint32_t *dst, int64_t n,
                  const uint32_t *tot, const uint32_t *offs, int ntiles) {
     const dim3 g((unsigned)blocks), b(TPB);
     const int sh = 8 * p;
     const bool f = mode == kRawF32;
 #define MPX_LEAN(I, O) \
-    hipLaunchKernelGGL((radix_scatter_lean_kernel<I, O, TPB, RANK, 0, WPE>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles)
+    hipLaunchKernelGGL((radix_scatter_lean_kernel<I, O, TPB, RANK, 0, WPE, PF>), g, b, 0, s, src, dst, n, sh, tot, offs, ntiles)
     if (p == 0 && f)
         MPX_LEAN(kRawF32, kRawKeys);
     else if (p == 0)
@@ -1096,7 +1117,8 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // 4096-key tiles up to 2^24 keys (10), on 8192-key tiles above (9)
     if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 10 : 9;
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
-    const int ntiles = variant == 8 || variant == 10 ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
+    const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
+    const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
     if (variant == 1) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
         hipLaunchKernelGGL(radix_hist_kernel,
@@ -1118,7 +1140,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                r.ctr + p, r.err, ntiles);
         } else {
             // offsets in status[0 .. 256 * ntiles), digit totals in hist[0 .. 256)
-            if (variant == 8 || variant == 10)
+            if (small_tiles)
                 hipLaunchKernelGGL(radix_count_kernel<kRTileSmall>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
                                    n, 8 * p, in_mode, r.status, ntiles);
             else
@@ -1144,6 +1166,12 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 else if (variant == 11)  // 3 blocks (24 waves) per CU: the returning-add ranking frees the table's LDS
                     launch_lean<kRThreads, 1, 6>(p, mode, std::min(kNumCUs * 3, rounded), s, src, dst, n, r.hist,
                                                  r.status, ntiles);
+                else if (variant == 12)  // 9 with two tiles of keys in flight
+                    launch_lean<kRThreads, 1, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
+                                                    r.status, ntiles);
+                else if (variant == 13)  // 10 with two tiles of keys in flight
+                    launch_lean<kRThreads / 2, 1, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
+                                                        r.hist, r.status, ntiles);
                 else
                     launch_lean<kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
                                                r.status, ntiles);
@@ -1341,8 +1369,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 11 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7, 8, 9, 10 or 11", variant);
+    if (variant < 0 || variant > 13 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 13", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);

@@ -42,7 +42,9 @@ case "$cmd" in
     grep '^{' "$O/bench.json" | tail -1 | cut -c1-400 ;;
   prof)
     name=$1; shift; [ "$1" = "--" ] && shift
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/$name" -o "$name" -- "$@" > "$O/$name.log" 2>&1 \
+    # one result file per process (%pid%): ranks launched as children would
+    # otherwise finalise into the same sqlite file (disk I/O error, abort, hang)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/$name" -o "${name}_%pid%" -- "$@" > "$O/$name.log" 2>&1 \
         || fail "prof $name" $? "$O/$name.log"
     find "$O/$name" -name "*kernel_stats.csv" | head -1 | xargs -r head -12 ;;
   pmc)
