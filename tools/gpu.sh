@@ -49,7 +49,7 @@ case "$cmd" in
     find "$O/$name" -name "*kernel_stats.csv" | head -1 | xargs -r head -12 ;;
   pmc)
     name=$1; ctrs=$2; shift 2; [ "$1" = "--" ] && shift
-    timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/$name" -o "$name" -- "$@" > "$O/$name.log" 2>&1 \
+    timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$O/$name" -o "${name}_%pid%" -- "$@" > "$O/$name.log" 2>&1 \
         || fail "pmc $name" $? "$O/$name.log"
     echo "pmc $name done" ;;
   profile)
