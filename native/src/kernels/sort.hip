@@ -313,6 +313,48 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const uint32_t *__restr
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
+// All four digit histograms in one read for the lean onesweep (variant 14):
+// per-wave LDS tables (no cross-wave contention on a digit's counter),
+// 16-B non-temporal key loads where the array is 16-B aligned, one global add
+// per (block, digit, non-zero count); 2 persistent blocks per CU.
+__global__ __launch_bounds__(256) void radix_hist4_kernel(const uint32_t *__restrict__ x, int64_t n, int mode,
+                                                          uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[4][4 * 256];
+    const int t = threadIdx.x;
+    for (int i = t; i < 4 * 4 * 256; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t *hw = h[t >> 6];
+    auto add = [&](uint32_t v) {
+        const uint32_t k = to_key(v, mode);
+        atomicAdd(&hw[k & 255u], 1u);
+        atomicAdd(&hw[256 + ((k >> 8) & 255u)], 1u);
+        atomicAdd(&hw[512 + ((k >> 16) & 255u)], 1u);
+        atomicAdd(&hw[768 + (k >> 24)], 1u);
+    };
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t gt = (int64_t)blockIdx.x * 256 + t;
+    int64_t done = 0;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 *xv = reinterpret_cast<const u32x4 *>(x);
+        const int64_t nv = n / 4;
+        for (int64_t i = gt; i < nv; i += stride) {
+            const u32x4 q = __builtin_nontemporal_load(xv + i);
+            add(q[0]);
+            add(q[1]);
+            add(q[2]);
+            add(q[3]);
+        }
+        done = nv * 4;
+    }
+    for (int64_t i = done + gt; i < n; i += stride) add(x[i]);
+    __syncthreads();
+    for (int i = t; i < 4 * 256; i += 256) {
+        const uint32_t c = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+        if (c) atomicAdd(&hist[i], c);
+    }
+}
+
 // exclusive scan of one value per thread over threads 0..255 (waves 0-3);
 // every thread of the block must call it (two barriers)
 __device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t *s_wsum) {
@@ -889,6 +931,178 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// Lean onesweep (variant 14): the returning-add ranking of the lean scatter
+// with decoupled look-back instead of a count pass per digit. One histogram
+// kernel reads the keys once for all four digits; each digit pass then moves
+// the keys once. Persistent blocks (2 per CU, all resident) take tiles from an
+// atomic counter in increasing order and hold at most three ids (the tile
+// being ranked, the prefetched next one, and the id whose counter add is in
+// flight); every wait is on a smaller tile id, whose holder ranks its tiles
+// in increasing order, so the smallest unfinished tile always progresses.
+// Per tile: rank into LDS (one ds_add_rtn per key) -> publish the tile's
+// digit counts (flag A, agent-scope store) -> stage in LDS -> threads 0-255
+// look back over the predecessors' status words, kLbWin at a time (one
+// round trip covers kLbWin tiles), until an inclusive prefix (flag P) ->
+// publish this tile's inclusive prefix -> write out.
+constexpr int kLbWin = 8;
+
+template <int IN_MODE, int OUT_MODE>
+__global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_onesweep_lean_kernel(
+    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
+    const uint32_t *__restrict__ tot, uint32_t *__restrict__ status, uint32_t *__restrict__ tile_ctr,
+    uint32_t *__restrict__ err, int ntiles) {
+    constexpr int TPB = kRThreads, NW = TPB / 64, TILE = kRTile;
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_cnt[NW][256];
+    __shared__ uint32_t s_gbase[256];
+    __shared__ uint32_t s_wsum[4];
+    __shared__ int s_next;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;
+    if (t == 0) s_next = (int)atomicAdd(tile_ctr, 1u);
+    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);  // its barrier publishes s_next
+    int tile = s_next;
+    if (tile >= ntiles) return;  // block-uniform
+    const uint32_t n32 = (uint32_t)n;
+    const int nbytes = (int)(n32 * 4u);
+    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(in), 0, nbytes,
+                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, nbytes, 0x00020000);
+    const int vlane = (w * kRWaveKeys + lane) * 4;
+
+    auto load_tile = [&](uint32_t (&dst)[kRPer], int tl) {
+        const int64_t tile0 = (int64_t)tl * TILE;
+        if (tile0 + TILE <= n) {
+            const uint32_t voff = (uint32_t)tile0 * 4u + (uint32_t)vlane;
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e) dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * 256u), 0, 2);
+        } else {
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e) {
+                const uint32_t i = i0 + e * 64u;
+                dst[e] = i < n32 ? __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(i * 4u), 0, 0) : 0u;
+            }
+        }
+    };
+    auto do_tile = [&](uint32_t (&key)[kRPer], int ptile) {
+        const int64_t tile0 = (int64_t)ptile * TILE;
+        const bool full = tile0 + TILE <= n;  // block-uniform
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) key[e] = to_key_t<IN_MODE>(key[e]);
+        if (!full) {  // pads rank last (digit 255 in every pass) and are never stored
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e)
+                if (i0 + e * 64u >= n32) key[e] = 0xffffffffu;
+        }
+        uint32_t rank[kRPer];
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) rank[e] = atomicAdd(&s_cnt[w][(key[e] >> shift) & 255u], 1u);
+        lds_barrier();
+        uint32_t cnt = 0, wexcl[NW];
+        if (t < 256) {
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                wexcl[ww] = cnt;
+                cnt += s_cnt[ww][t];
+            }
+            // the tile's count of digit t, visible to the successors' look-back
+            __hip_atomic_store(status + (size_t)ptile * 256 + t, (ptile == 0 ? kFlagP : kFlagA) | cnt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t dstart = scan256_excl_dpp(cnt, s_wsum);
+        if (t < 256) {
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rank[e]] = key[e];
+        if (t < 256) {
+            uint32_t excl = 0;
+            if (ptile > 0) {
+                int j = ptile - 1;  // next predecessor to consume
+                uint32_t spins = 0;
+                bool found = false;
+                while (!found) {
+                    uint32_t v[kLbWin];
+#pragma unroll
+                    for (int k = 0; k < kLbWin; ++k)
+                        v[k] = j - k >= 0 ? __hip_atomic_load(status + (size_t)(j - k) * 256 + t, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : kFlagP;  // never reached: tile 0 publishes a prefix
+                    int used = 0;
+                    bool stalled = false;
+#pragma unroll
+                    for (int k = 0; k < kLbWin; ++k) {
+                        if (found || stalled) continue;
+                        if ((v[k] & ~kCountMask) == 0) {
+                            stalled = true;
+                            continue;
+                        }
+                        excl += v[k] & kCountMask;
+                        ++used;
+                        if (v[k] & kFlagP) found = true;
+                    }
+                    j -= used;
+                    if (stalled && !found) {
+                        if (++spins > kSpinLimit) {
+                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                __hip_atomic_store(status + (size_t)ptile * 256 + t, kFlagP | (excl + cnt), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_gbase[t] = excl + dbase - dstart;
+        }
+        lds_barrier();
+        // this wave's staging reads of its own counter row are done (program order)
+#pragma unroll
+        for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
+        if (full) {
+#pragma unroll
+            for (int jj = 0; jj < TILE / TPB; ++jj) {
+                const int i = t + jj * TPB;
+                const uint32_t k = s_keys[i];
+                __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout,
+                                                      (int)((s_gbase[(k >> shift) & 255u] + (uint32_t)i) * 4u), 0, 0);
+            }
+        } else {
+            for (int jj = 0; jj < TILE / TPB; ++jj) {
+                const int i = t + jj * TPB;
+                const uint32_t k = s_keys[i];
+                const uint32_t pos = s_gbase[(k >> shift) & 255u] + (uint32_t)i;
+                if (pos < n32) __builtin_amdgcn_raw_buffer_store_b32(from_key_t<OUT_MODE>(k), rout, (int)(pos * 4u), 0, 0);
+            }
+        }
+    };
+
+    uint32_t a[kRPer], b[kRPer];
+    load_tile(a, tile);
+    lds_barrier();  // every thread has read s_next
+    if (t == 0) s_next = (int)atomicAdd(tile_ctr, 1u);
+    lds_barrier();
+    int next = s_next;
+    for (;;) {
+        // the id after next: its counter add is in flight under this tile's work
+        int grabbed = 0;
+        if (t == 0 && next < ntiles) grabbed = (int)atomicAdd(tile_ctr, 1u);
+        if (next < ntiles) load_tile(b, next);
+        do_tile(a, tile);  // ends after a barrier: every thread has read s_next
+        if (next >= ntiles) break;
+        tile = next;
+#pragma unroll
+        for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+        if (t == 0) s_next = grabbed;
+        lds_barrier();
+        next = s_next;
+    }
+}
+
 // reduce-then-scan, step 1: the tile's digit counts (per-wave LDS atomics,
 // order irrelevant), digit-major
 // (cnt[d][tile]); consecutive tiles share an XCD so their L2 merges the
@@ -1074,7 +1288,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // lean persistent scatter (radix_scatter_lean_kernel, 8192-key tiles), 8 = 7
 // on 4096-key tiles (256-thread blocks, 4 per CU), 9 = 7 ranked by returning
 // LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
-// 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2). Retired after round-3
+// 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2), 14 = the lean
+// onesweep (one histogram read, then decoupled look-back per digit pass). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1082,7 +1297,7 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
 // reduce-then-scan re-reads each tile once more but never waits.
 constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
-constexpr int64_t kTile4kMaxN = (int64_t)1 << 24;    // variant 8 up to here (measured sizes only)
+constexpr int64_t kTile4kMaxN = (int64_t)1 << 23;    // 4096-key tiles up to here (2^24: 0.187 ms both ways)
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
@@ -1113,17 +1328,23 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // vs 0.229) and lose at 2^26 (0.987 vs 0.828; not yet explained — a
     // candidate: with 16 tiles per block the 64-B digit runs of neighbouring
     // tiles stop meeting in L2; profiles/lab5_sort.md)
-    // AUTO (round 4, profiles/lab5_sort.md): the returning-add ranking on
-    // 4096-key tiles up to 2^24 keys (10), on 8192-key tiles above (9)
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 10 : 9;
+    // AUTO (round 4, profiles/lab5_sort.md): the returning-add ranking with
+    // two tiles of keys in flight, on 4096-key tiles up to 2^23 keys (13),
+    // on 8192-key tiles above (12)
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 13 : 12;
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
-    if (variant == 1) {
+    if (variant == 1 || variant == 14) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
-        hipLaunchKernelGGL(radix_hist_kernel,
-                           dim3(std::max<int64_t>(1, std::min<int64_t>((n + 4095) / 4096, kNumCUs * 8))), dim3(256), 0,
-                           s, x, n, mode, r.hist);
+        if (variant == 14)
+            hipLaunchKernelGGL(radix_hist4_kernel,
+                               dim3(std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, kNumCUs * 2))), dim3(256),
+                               0, s, x, n, mode, r.hist);
+        else
+            hipLaunchKernelGGL(radix_hist_kernel,
+                               dim3(std::max<int64_t>(1, std::min<int64_t>((n + 4095) / 4096, kNumCUs * 8))), dim3(256),
+                               0, s, x, n, mode, r.hist);
         MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     } else {
         // the give-up flag sort_ws_status reads: reduce-then-scan never waits,
@@ -1134,7 +1355,24 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
         const uint32_t *src = (p & 1) ? r.tmp : x;
         uint32_t *dst = (p & 1) ? x : r.tmp;
         const int in_mode = p == 0 ? mode : (int)kRawKeys, out_mode = p == 3 ? mode : (int)kRawKeys;
-        if (variant == 1) {
+        if (variant == 14) {
+            const dim3 g((unsigned)std::min(kNumCUs * 2, ntiles)), b(kRThreads);
+            uint32_t *st = r.status + (size_t)p * ntiles * 256;
+            const bool f = mode == kRawF32;
+#define MPX_OS(I, O) \
+    hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
+            if (p == 0 && f)
+                MPX_OS(kRawF32, kRawKeys);
+            else if (p == 0)
+                MPX_OS(kRawI32, kRawKeys);
+            else if (p == 3 && f)
+                MPX_OS(kRawKeys, kRawF32);
+            else if (p == 3)
+                MPX_OS(kRawKeys, kRawI32);
+            else
+                MPX_OS(kRawKeys, kRawKeys);
+#undef MPX_OS
+        } else if (variant == 1) {
             hipLaunchKernelGGL(radix_pass_kernel<true>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst, n,
                                8 * p, in_mode, out_mode, r.hist + 256 * p, r.status + (size_t)p * ntiles * 256,
                                r.ctr + p, r.err, ntiles);
@@ -1369,8 +1607,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 13 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 13", variant);
+    if (variant < 0 || variant > 14 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 14", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
