@@ -176,7 +176,8 @@ constexpr int kAmbCap = 512;
 
 // NQ: 16-B vectors (4 pixels each) per thread and loop trip; nvec counts
 // groups of NQ vectors. OPT (tuning, MPX_CLS_OPT): bit 1 non-temporal loads,
-// bit 2 non-temporal stores, bit 4 wave-contiguous vectors (vector qq of a
+// bit 2 non-temporal stores, bit 8 interleaved FMA chains without inline asm,
+// bit 4 wave-contiguous vectors (vector qq of a
 // thread at wave base * NQ + 64 qq + lane, so every load / store instruction
 // covers 1 KiB of consecutive bytes; nvec must then be a multiple of 64).
 typedef uint32_t cls_u32x4 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take clang vectors
@@ -259,13 +260,36 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         for (int q = 0; q < NP; ++q) B[q] = S[q] = kKeyInit;
         auto one_class = [&](int c) {
             const float *w = fp.w[c];
+            if constexpr (OPT & 8) {
+                // the pairs' FMA chains interleaved (each FMA's result is
+                // needed NP / 2 instructions later, not by the next one), the
+                // top-2 step in plain C (v_med3_u32 by pattern, no inline asm)
+                f2_t d[NP / 2];
 #pragma unroll
-            for (int h = 0; h < NP / 2; ++h) {
-                f2_t d = {w[9], w[9]};
+                for (int h = 0; h < NP / 2; ++h) d[h] = f2_t{w[9], w[9]};
 #pragma unroll
-                for (int k = 0; k < 9; ++k) d = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d);
-                rank_key(make_key_s(d.x, (uint32_t)c), B[2 * h], S[2 * h]);
-                rank_key(make_key_s(d.y, (uint32_t)c), B[2 * h + 1], S[2 * h + 1]);
+                for (int k = 0; k < 9; ++k)
+#pragma unroll
+                    for (int h = 0; h < NP / 2; ++h) d[h] = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d[h]);
+#pragma unroll
+                for (int h = 0; h < NP / 2; ++h) {
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const uint32_t k = make_key_s(q ? d[h].y : d[h].x, (uint32_t)c);
+                        uint32_t &Bq = B[2 * h + q], &Sq = S[2 * h + q];
+                        Sq = max(min(Bq, k), min(max(Bq, k), Sq));
+                        Bq = min(Bq, k);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < NP / 2; ++h) {
+                    f2_t d = {w[9], w[9]};
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) d = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d);
+                    rank_key(make_key_s(d.x, (uint32_t)c), B[2 * h], S[2 * h]);
+                    rank_key(make_key_s(d.y, (uint32_t)c), B[2 * h + 1], S[2 * h + 1]);
+                }
             }
         };
         // four classes per iteration: their weights' scalar loads issue
@@ -1129,7 +1153,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         static const int opt = [] {
             const char *e = std::getenv("MPX_CLS_OPT");
             const int o = e ? std::atoi(e) : 0;
-            return o >= 0 && o <= 7 ? o : 0;
+            return o >= 0 && o <= 15 ? o : 0;
         }();
         int64_t nvec = npix / (4 * nq);
         if (opt & 4) nvec &= ~63ll;  // whole waves only; the rest goes DIRECT
@@ -1149,7 +1173,10 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         hipLaunchKernelGGL((classify_fast32_kernel<2, k>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);  \
         break;
                     MPX_FAST32_OPT(1) MPX_FAST32_OPT(2) MPX_FAST32_OPT(3) MPX_FAST32_OPT(4) MPX_FAST32_OPT(5)
-                    MPX_FAST32_OPT(6) MPX_FAST32_OPT(7)
+                    MPX_FAST32_OPT(6) MPX_FAST32_OPT(7) MPX_FAST32_OPT(8) MPX_FAST32_OPT(10) MPX_FAST32_OPT(12)
+                    MPX_FAST32_OPT(15)
+                    default:
+                        hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
 #undef MPX_FAST32_OPT
                 }
             } else if (nq == 2)

@@ -944,9 +944,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // look back over the predecessors' status words, kLbWin at a time (one
 // round trip covers kLbWin tiles), until an inclusive prefix (flag P) ->
 // publish this tile's inclusive prefix -> write out.
-constexpr int kLbWin = 8;
-
-template <int IN_MODE, int OUT_MODE>
+template <int IN_MODE, int OUT_MODE, int kLbWin = 8>
 __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_onesweep_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, uint32_t *__restrict__ status, uint32_t *__restrict__ tile_ctr,
@@ -1289,7 +1287,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // on 4096-key tiles (256-thread blocks, 4 per CU), 9 = 7 ranked by returning
 // LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
 // 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2), 14 = the lean
-// onesweep (one histogram read, then decoupled look-back per digit pass). Retired after round-3
+// onesweep (one histogram read, then decoupled look-back per digit pass;
+// 15 / 16 look back over 16 / 32 predecessors per round trip instead of 8). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1335,9 +1334,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
-    if (variant == 1 || variant == 14) {
+    if (variant == 1 || variant >= 14) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
-        if (variant == 14)
+        if (variant >= 14)
             hipLaunchKernelGGL(radix_hist4_kernel,
                                dim3(std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, kNumCUs * 2))), dim3(256),
                                0, s, x, n, mode, r.hist);
@@ -1355,12 +1354,21 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
         const uint32_t *src = (p & 1) ? r.tmp : x;
         uint32_t *dst = (p & 1) ? x : r.tmp;
         const int in_mode = p == 0 ? mode : (int)kRawKeys, out_mode = p == 3 ? mode : (int)kRawKeys;
-        if (variant == 14) {
+        if (variant >= 14) {
             const dim3 g((unsigned)std::min(kNumCUs * 2, ntiles)), b(kRThreads);
             uint32_t *st = r.status + (size_t)p * ntiles * 256;
             const bool f = mode == kRawF32;
-#define MPX_OS(I, O) \
-    hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
+#define MPX_OS1(I, O, W) \
+    hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O, W>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
+#define MPX_OS(I, O)               \
+    do {                           \
+        if (variant == 16)         \
+            MPX_OS1(I, O, 32);     \
+        else if (variant == 15)    \
+            MPX_OS1(I, O, 16);     \
+        else                       \
+            MPX_OS1(I, O, 8);      \
+    } while (0)
             if (p == 0 && f)
                 MPX_OS(kRawF32, kRawKeys);
             else if (p == 0)
@@ -1372,6 +1380,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             else
                 MPX_OS(kRawKeys, kRawKeys);
 #undef MPX_OS
+#undef MPX_OS1
         } else if (variant == 1) {
             hipLaunchKernelGGL(radix_pass_kernel<true>, dim3((unsigned)ntiles), dim3(kRThreads), 0, s, src, dst, n,
                                8 * p, in_mode, out_mode, r.hist + 256 * p, r.status + (size_t)p * ntiles * 256,
@@ -1607,8 +1616,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 14 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 14", variant);
+    if (variant < 0 || variant > 16 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 16", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
