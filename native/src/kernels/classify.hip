@@ -162,6 +162,24 @@ __device__ __forceinline__ uint32_t finish_pixel(uint32_t p, uint32_t B, uint32_
     return classify_direct(p, nc, cp);
 }
 
+// One pixel through the proven-margin fp32 ranking (the FAST32 arithmetic,
+// unpacked): true with the class in `out` when the margin decides it.
+__device__ __forceinline__ bool classify_fp32_one(uint32_t p, int nc, const FastParams &fp, uint32_t &out) {
+    const float r = (float)(p & 0xffu) - 128.0f, g = (float)((p >> 8) & 0xffu) - 128.0f,
+                b = (float)((p >> 16) & 0xffu) - 128.0f;
+    const float f[9] = {r * r, g * g, b * b, r * g, r * b, g * b, r, g, b};
+    uint32_t B = kKeyInit, S = kKeyInit;
+    for (int c = 0; c < nc; ++c) {
+        const float *w = fp.w[c];
+        float d = w[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) d = fmaf(w[k], f[k], d);
+        rank_key(make_key(d, (uint32_t)c), B, S);
+    }
+    out = (p & 0x00ffffffu) | ((B & 31u) << 24);
+    return decided(B, S, fp.T2);
+}
+
 // ---------------------------------------------------------------------------
 // FAST32: VALU, 4 pixels per lane as two packed pairs.
 //
@@ -696,9 +714,11 @@ __device__ __forceinline__ uint32_t mfma8_chunk(const uint4 &q, const Mfma8Lane 
 constexpr int kWin8 = 4;
 constexpr int kAmb8WinCap = 1024;  // undecided pixels per window (of 4 x 4 x 128)
 
+constexpr int kAmb8Cap2 = 256;  // pixels the fp32 stage leaves to the fp64 chain, per block
+
 template <int NREG, bool WIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void classify_mfma8_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
-                                                             ClassParams cp, I8Params ip, uint32_t *amb) {
+                                                             ClassParams cp, I8Params ip, FastParams fp, uint32_t *amb) {
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5;
     const int col = lane & 31;
@@ -737,10 +757,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
                 v[ch * 32 + col] = o;
             }
         }
+        __shared__ int64_t s_amb2[kAmb8Cap2];
+        __shared__ uint32_t s_ambpx2[kAmb8Cap2];
+        __shared__ uint32_t s_namb2;
+        if (threadIdx.x == 0) s_namb2 = 0;
         __syncthreads();
         const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
         if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
-        for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) img[s_amb[j]] = classify_direct(s_ambpx[j], nc, cp);
+        // two stages, every lane busy in each: the fp32 proven-margin ranking
+        // settles all but ~1% of the int8 path's undecided pixels (its bound is
+        // ~2^-16 of the weights' against the int8 keys' 2^-8 .. 2^-16); the
+        // rest take the exact fp64 chain together
+        for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+            const uint32_t px = s_ambpx[j];
+            uint32_t o;
+            if (classify_fp32_one(px, nc, fp, o)) {
+                img[s_amb[j]] = o;
+            } else {
+                const uint32_t slot = atomicAdd(&s_namb2, 1u);
+                if (slot < (uint32_t)kAmb8Cap2) {
+                    s_amb2[slot] = s_amb[j];
+                    s_ambpx2[slot] = px;
+                } else {
+                    img[s_amb[j]] = classify_direct(px, nc, cp);
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nd2 = min(s_namb2, (uint32_t)kAmb8Cap2);
+        for (uint32_t j = threadIdx.x; j < nd2; j += blockDim.x) img[s_amb2[j]] = classify_direct(s_ambpx2[j], nc, cp);
     } else {
         constexpr int NW = 4;  // waves per block (launch_bounds 256)
         __shared__ uint4 s_out[kWin8][NW][32];
@@ -1058,10 +1103,25 @@ inline bool auto_mfma8(int nc) { return nc == 16 || nc >= kAutoMfma8MinClasses; 
 int classify_resolve(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
                      Fast64Params &fp64, I8Params &ip8) {
     if (path == MPX_CLS_DIRECT || !aligned) return MPX_CLS_DIRECT;
-    if (path == MPX_CLS_AUTO && auto_mfma8(nc) && build_i8(nc, mu, inv, ip8)) return MPX_CLS_MFMA8;
+    // mfma8 re-ranks its undecided pixels in fp32 first: its FastParams too
+    // (T2 = +inf when the fp32 bound cannot be proven: the fp64 chain then
+    // takes every undecided pixel)
+    // (MPX_CLS_MFMA8_FP32=0, A/B: every undecided pixel to the fp64 chain)
+    static const bool fp32_stage = [] {
+        const char *e = std::getenv("MPX_CLS_MFMA8_FP32");
+        return !(e && e[0] == '0');
+    }();
+    auto fp_for_i8 = [&] {
+        if (!fp32_stage || !build_fast(nc, mu, inv, fp)) fp.T2 = INFINITY;
+    };
+    if (path == MPX_CLS_AUTO && auto_mfma8(nc) && build_i8(nc, mu, inv, ip8)) {
+        fp_for_i8();
+        return MPX_CLS_MFMA8;
+    }
     const bool ok = path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
                     : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
                                             : build_fast(nc, mu, inv, fp);
+    if (path == MPX_CLS_MFMA8 && ok) fp_for_i8();
     return classify_choose(nc, path, ok);
 }
 
@@ -1098,9 +1158,9 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 #define MPX_MFMA8_LAUNCH(NREG)                                                                                       \
     do {                                                                                                             \
         if (win)                                                                                                     \
-            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, true>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb); \
+            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, true>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, fp, amb); \
         else                                                                                                         \
-            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, false>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, amb); \
+            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, false>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, fp, amb); \
     } while (0)
             if (nc <= 8)
                 MPX_MFMA8_LAUNCH(4);
