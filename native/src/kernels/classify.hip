@@ -832,8 +832,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             const uint32_t na = s_namb;
             const uint32_t nd = min(na, (uint32_t)kAmb8WinCap);
             for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
-                const uint32_t e = s_ambi[j];
-                reinterpret_cast<uint32_t *>(&s_out[0][0][0])[e] = classify_direct(s_ambpx[j], nc, cp);
+                const uint32_t e = s_ambi[j], px = s_ambpx[j];
+                uint32_t o;
+                if (!classify_fp32_one(px, nc, fp, o)) o = classify_direct(px, nc, cp);  // fp64 only where fp32 cannot decide
+                reinterpret_cast<uint32_t *>(&s_out[0][0][0])[e] = o;
             }
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -1209,11 +1211,14 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const char *e = std::getenv("MPX_CLS_NQ");
             return (e && e[0] == '1') ? 1 : 2;
         }();
-        // memory-policy / layout variant (fast32 OPT bits), A/B only for now
+        // fast32 OPT bits (MPX_CLS_OPT overrides): 8 = interleaved FMA chains,
+        // the default since round 4 (nc = 16 / 32: 307.6 -> 301.8 / 523.8 ->
+        // 519.2 us medians, two alternated rounds; profiles/lab3_classify.md);
+        // the memory-policy / layout bits measured neutral and stay off
         static const int opt = [] {
             const char *e = std::getenv("MPX_CLS_OPT");
-            const int o = e ? std::atoi(e) : 0;
-            return o >= 0 && o <= 15 ? o : 0;
+            const int o = e ? std::atoi(e) : 8;
+            return o >= 0 && o <= 15 ? o : 8;
         }();
         int64_t nvec = npix / (4 * nq);
         if (opt & 4) nvec &= ~63ll;  // whole waves only; the rest goes DIRECT

@@ -1287,8 +1287,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // on 4096-key tiles (256-thread blocks, 4 per CU), 9 = 7 ranked by returning
 // LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
 // 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2), 14 = the lean
-// onesweep (one histogram read, then decoupled look-back per digit pass;
-// 15 / 16 look back over 16 / 32 predecessors per round trip instead of 8). Retired after round-3
+// onesweep (one histogram read, then decoupled look-back per digit pass):
+// correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1360,15 +1360,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             const bool f = mode == kRawF32;
 #define MPX_OS1(I, O, W) \
     hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O, W>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
-#define MPX_OS(I, O)               \
-    do {                           \
-        if (variant == 16)         \
-            MPX_OS1(I, O, 32);     \
-        else if (variant == 15)    \
-            MPX_OS1(I, O, 16);     \
-        else                       \
-            MPX_OS1(I, O, 8);      \
-    } while (0)
+#define MPX_OS(I, O) MPX_OS1(I, O, 8)
             if (p == 0 && f)
                 MPX_OS(kRawF32, kRawKeys);
             else if (p == 0)
@@ -1616,8 +1608,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 16 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 16", variant);
+    if (variant < 0 || variant > 14 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 14", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
