@@ -18,14 +18,32 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cuda_mpi_openmp_amd import _native, ops  # noqa: E402
 
 
+STREAMS = []  # --streams S > 1: launch i goes to STREAMS[i % S] (independent pairs overlap, as in bench.py)
+
+
+def S():  # the stream handle a variant launches on (the current torch stream)
+    return torch.cuda.current_stream().cuda_stream
+
+
 def time_launch(fn, iters, cyc):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
     torch.cuda.synchronize()
     s.record()
-    for _ in range(iters):
-        cyc[0] += 1
-        fn()
+    if STREAMS:
+        main = torch.cuda.current_stream()
+        for st in STREAMS:
+            st.wait_stream(main)
+        for i in range(iters):
+            cyc[0] += 1
+            with torch.cuda.stream(STREAMS[i % len(STREAMS)]):
+                fn()
+        for st in STREAMS:
+            main.wait_stream(st)
+    else:
+        for _ in range(iters):
+            cyc[0] += 1
+            fn()
     e.record()
     e.synchronize()
     return s.elapsed_time(e) * 1e3 / iters  # us
@@ -39,7 +57,13 @@ def main():
     p.add_argument("--rotate", type=int, default=1, help="input/output pairs cycled per launch (>= 3 at 4096^2 "
                                                           "defeats the MALL)")
     p.add_argument("--only", default="", help="run only the variants whose name contains this string")
+    p.add_argument("--streams", type=int, default=1, help="alternate launches over this many HIP streams "
+                                                          "(needs --rotate divisible by it: no pair is shared)")
     args = p.parse_args()
+    if args.streams > 1:
+        if args.rotate % args.streams:
+            raise SystemExit("--rotate must be a multiple of --streams")
+        STREAMS.extend(torch.cuda.Stream() for _ in range(args.streams))
     L = _native.lib()
     T = _native.tune_lib()  # variants / probes live in libmpx_tune.so
     dev = torch.device("cuda:0")
@@ -75,7 +99,7 @@ def main():
 
         def mk(kind, p1, p2, fast, wx=wx, wy=wy, k=k):
             return lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, k, kind, p1, p2, fast,
-                                                            wx, wy, 0))
+                                                            wx, wy, S()))
 
         for seg in (8, 16, 32, 64):
             variants[f"{fname}/wave-rt/seg{seg}"] = (mk(1, seg, 0, 1), ref)
@@ -91,43 +115,43 @@ def main():
     for seg in (0, 16, 32, 48):  # alternating segment direction (production MAG2 order candidate)
         variants[f"sobel5-sep/wave-const/seg{seg}/alt"] = (
             (lambda seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 2000, 1,
-                                                              swx, swy, 0))), sref)
+                                                              swx, swy, S()))), sref)
     for seg in (0, 8, 20, 24):
         for kind, nm in ((3, "const"), (4, "rt")):
             variants[f"sobel5-sep/wave-{nm}/seg{seg}"] = (
                 (lambda kind=kind, seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5,
-                                                                             kind, seg, 0, 1, swx, swy, 0))), sref)
+                                                                             kind, seg, 0, 1, swx, swy, S()))), sref)
         variants[f"sobel5-sep/wave-const/seg{seg}/strip-major"] = (
             (lambda seg=seg: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg, 1000, 1,
-                                                              swx, swy, 0))), sref)
+                                                              swx, swy, S()))), sref)
     for seg, per in ((0, 0), (0, 2000), (24, 2000), (0, 18000), (0, 34000), (0, 66000), (0, 162000),
                      (20, 34000), (24, 34000), (12, 34000),
                      (0, 10000), (0, 10005), (0, 11005), (24, 10000), (0, 514000), (0, 514005)):
         # 18000: no apron loads — a cost probe whose strip edges are wrong (no reference check)
         variants[f"sobel5-sep/band4/seg{seg}/w{per}"] = (
             (lambda seg=seg, per=per: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 8, seg,
-                                                                       per, 1, swx, swy, 0))), None if per == 18000 else sref)
+                                                                       per, 1, swx, swy, S()))), None if per == 18000 else sref)
     variants["sobel5-sep/band16v"] = (  # vertical halo sharing through LDS (conv_band16v_kernel)
-        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 10, 0, 0, 1, swx, swy, 0))),
+        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 10, 0, 0, 1, swx, swy, S()))),
         sref)
     rf = ops.get_filter("roberts")
     rwx, rwy = rf.c_taps()
     rref = ops.conv(img, rf)
     variants["sobel5-sep/stores-nt"] = (
-        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, 3, 1, swx, swy, 0))),
+        (lambda: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, 3, 1, swx, swy, S()))),
         sref)
     for p2, nm in ((0, "buffer"), (1, "global"), (2, "global-nt")):  # row-load A/B
         variants[f"sobel5-sep/loads-{nm}"] = (
             (lambda p2=p2: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 6, 0, p2, 1,
-                                                            swx, swy, 0))), sref)
+                                                            swx, swy, S()))), sref)
         variants[f"roberts/loads-{nm}"] = (
             (lambda p2=p2: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 2, 7, 0, p2, 1,
-                                                            rwx, rwy, 0))), rref)
+                                                            rwx, rwy, S()))), rref)
     for pf in (4, 8, 12):  # prefetch ring depth (D = 5 / 10 / 15 rows)
         for seg in (0, 16, 24, 32, 40):
             variants[f"sobel5-sep/wave-const/seg{seg}/pf{pf}"] = (
                 (lambda seg=seg, pf=pf: _native.check(T.mpx_conv_variant(I().data_ptr(), O().data_ptr(), n, n, 5, 3, seg,
-                                                                         pf, 1, swx, swy, 0))), sref)
+                                                                         pf, 1, swx, swy, S()))), sref)
     for fname in ("sobel5", "gauss5"):  # separable production path (row-sum ring)
         f = ops.get_filter(fname)
         variants[f"{fname}/production"] = ((lambda f=f: ops.conv(I(), f, O())), ops.conv(img, f))
@@ -136,20 +160,20 @@ def main():
     for v, d, seg in ((2, 4, 8), (2, 4, 24), (2, 8, 24), (4, 4, 8), (4, 4, 24), (4, 8, 24), (4, 2, 24), (4, 4, 48)):
         variants[f"copy/strip-v{v}-d{d}-seg{seg}"] = (
             (lambda v=v, d=d, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
-                                                                            seg, 0))), img)
+                                                                            seg, S()))), img)
     for v, d, seg in ((2, 104, 8), (2, 104, 24), (4, 104, 8), (4, 104, 24), (4, 104, 64)):  # 16 waves per block
         variants[f"copy/strip-v{v}-d{d - 100}-seg{seg}-wpb16"] = (
             (lambda v=v, d=d, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, v, d,
-                                                                            seg, 0))), img)
+                                                                            seg, S()))), img)
     for d, nm in ((0, "plain"), (1, "nt")):  # linear 16-B-per-thread copy: the HBM floor of these bytes
         variants[f"copy/linear-{nm}"] = (
-            (lambda d=d: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, 0))), img)
+            (lambda d=d: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 0, d, 0, S()))), img)
     for seg, fl in [(sg, f) for sg in (4, 8, 12, 16, 20) for f in (2, 3, 10, 18, 26, 74)] + [
             (16, 0), (16, 4), (16, 34), (16, 42), (32, 10), (32, 42), (16, 72), (16, 106), (32, 74)]:
         if True:  # row bands, 16-B vector per thread (ref None: XOR of rows, no reference)
             variants[f"copy/band-seg{seg}-f{fl}"] = (
                 (lambda fl=fl, seg=seg: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 8,
-                                                                              fl, seg, 0))), None)
+                                                                              fl, seg, S()))), None)
     # burst tiles: R output rows per tile, all R + 4 row
     # loads of a lane issued at once, many rounds of tiles; f = flag bits
     # (1 xcd_remap, 2 NT loads, 4 NT stores), t = threads per workgroup
@@ -163,7 +187,7 @@ def main():
                 d = fl | (tcode << 4)
                 variants[f"copy/burst-r{R}-t{256 << tcode}-f{fl}"] = (
                     (lambda d=d, R=R: _native.check(T.mpx_strip_copy_probe(I().data_ptr(), O().data_ptr(), n, n, 16,
-                                                                            d, R, 0))), None)
+                                                                            d, R, S()))), None)
     rob_ref = ops.roberts(img)
     for geom in (((32, 32), (16, 16)), ((64, 4), (64, 64)), ((16, 16), (1024, 1024))):
         variants[f"roberts/geom{geom}"] = ((lambda g=geom: ops.roberts(I(), O(), geometry=g)), rob_ref)
