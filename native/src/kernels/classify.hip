@@ -195,6 +195,7 @@ constexpr int kAmbCap = 512;
 // NQ: 16-B vectors (4 pixels each) per thread and loop trip; nvec counts
 // groups of NQ vectors. OPT (tuning, MPX_CLS_OPT): bit 1 non-temporal loads,
 // bit 2 non-temporal stores, bit 8 interleaved FMA chains without inline asm,
+// bit 16 two trips of loads in flight instead of one,
 // bit 4 wave-contiguous vectors (vector qq of a
 // thread at wave base * NQ + 64 qq + lane, so every load / store instruction
 // covers 1 KiB of consecutive bytes; nvec must then be a multiple of 64).
@@ -235,22 +236,21 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
     // software-pipelined grid-stride loop: the next 16-B vector is in flight
     // while this one is ranked (a thread walks ~32 vectors at 8192^2; without
     // the prefetch each step exposes a full HBM round trip)
-    uint4 qn[NQ];
+    auto load_q = [&](uint4 (&q)[NQ], int64_t it) {
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) qn[qq] = i < nvec ? cls_load<OPT>(v + cls_vec<NQ, OPT>(i, qq)) : uint4{};
-    for (; i < nvec; i += stride) {
-        uint32_t px[NP];
+        for (int qq = 0; qq < NQ; ++qq) q[qq] = it < nvec ? cls_load<OPT>(v + cls_vec<NQ, OPT>(it, qq)) : uint4{};
+    };
+    auto unpack = [&](const uint4 (&q)[NQ], uint32_t (&px)[NP]) {
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq) {
-            px[4 * qq + 0] = qn[qq].x;
-            px[4 * qq + 1] = qn[qq].y;
-            px[4 * qq + 2] = qn[qq].z;
-            px[4 * qq + 3] = qn[qq].w;
+            px[4 * qq + 0] = q[qq].x;
+            px[4 * qq + 1] = q[qq].y;
+            px[4 * qq + 2] = q[qq].z;
+            px[4 * qq + 3] = q[qq].w;
         }
-        if (i + stride < nvec) {
-#pragma unroll
-            for (int qq = 0; qq < NQ; ++qq) qn[qq] = cls_load<OPT>(v + cls_vec<NQ, OPT>(i + stride, qq));
-        }
+    };
+    // rank the NP pixels of trip i and store them
+    auto rank_store = [&](const uint32_t (&px)[NP], int64_t i) {
         f2_t f[NP / 2][9];
 #pragma unroll
         for (int h = 0; h < NP / 2; ++h) {
@@ -337,6 +337,40 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq)
             cls_store<OPT>(v + cls_vec<NQ, OPT>(i, qq), make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]));
+    };
+    if constexpr ((OPT & 16) != 0) {
+        // two trips of loads in flight: two register sets in fixed roles (a
+        // copy between them would wait for the copied loads); each set is
+        // unpacked and re-issued for the trip after next before its pixels
+        // are ranked
+        uint4 qa[NQ], qb[NQ];
+        load_q(qa, i);
+        load_q(qb, i + stride);
+        while (i < nvec) {
+            {
+                uint32_t px[NP];
+                unpack(qa, px);
+                if (i + 2 * stride < nvec) load_q(qa, i + 2 * stride);
+                rank_store(px, i);
+            }
+            if ((i += stride) >= nvec) break;
+            {
+                uint32_t px[NP];
+                unpack(qb, px);
+                if (i + 2 * stride < nvec) load_q(qb, i + 2 * stride);
+                rank_store(px, i);
+            }
+            i += stride;
+        }
+    } else {
+        uint4 qn[NQ];
+        load_q(qn, i);
+        for (; i < nvec; i += stride) {
+            uint32_t px[NP];
+            unpack(qn, px);
+            if (i + stride < nvec) load_q(qn, i + stride);
+            rank_store(px, i);
+        }
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
@@ -1218,7 +1252,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         static const int opt = [] {
             const char *e = std::getenv("MPX_CLS_OPT");
             const int o = e ? std::atoi(e) : 8;
-            return o >= 0 && o <= 15 ? o : 8;
+            return o >= 0 && o <= 31 ? o : 8;
         }();
         int64_t nvec = npix / (4 * nq);
         if (opt & 4) nvec &= ~63ll;  // whole waves only; the rest goes DIRECT
@@ -1239,7 +1273,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         break;
                     MPX_FAST32_OPT(1) MPX_FAST32_OPT(2) MPX_FAST32_OPT(3) MPX_FAST32_OPT(4) MPX_FAST32_OPT(5)
                     MPX_FAST32_OPT(6) MPX_FAST32_OPT(7) MPX_FAST32_OPT(8) MPX_FAST32_OPT(10) MPX_FAST32_OPT(12)
-                    MPX_FAST32_OPT(15)
+                    MPX_FAST32_OPT(15) MPX_FAST32_OPT(24) MPX_FAST32_OPT(26)
                     default:
                         hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
 #undef MPX_FAST32_OPT

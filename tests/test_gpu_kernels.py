@@ -440,7 +440,7 @@ def test_roberts_rgb_gpu_matches_cpu(gpu, hw):
     assert torch.equal(ops.roberts_rgb(img.to(gpu)).cpu(), ops.roberts_rgb(img))
 
 
-@pytest.mark.parametrize("env", [{"MPX_CLS_OPT": str(o)} for o in (0, 1, 2, 3, 4, 5, 6, 7, 10, 12, 15)] + [{"MPX_CLS_MFMA8_WIN": "1"}, {"MPX_CLS_MFMA8_FP32": "0"}])
+@pytest.mark.parametrize("env", [{"MPX_CLS_OPT": str(o)} for o in (0, 1, 2, 3, 4, 5, 6, 7, 10, 12, 15, 24, 26)] + [{"MPX_CLS_MFMA8_WIN": "1"}, {"MPX_CLS_MFMA8_FP32": "0"}])
 def test_classify_env_variants_match_cpu(gpu, env, tmp_path):
     """The A/B variants read once per process from the environment (fast32
     memory policy / wave-contiguous layout bits, mfma8 fix-ups after the loop
