@@ -25,6 +25,16 @@ def main():
             for k in range(REPS + 6):
                 img, out = pairs[k % 6]
                 ops.conv(img, f, out)
+        # the LDS-tiled variant (conv_band16v_kernel: vertical halo rows shared
+        # through LDS; band mode 4, not the default) for its LDS counters
+        from cuda_mpi_openmp_amd import _native
+        L = _native.lib()
+        prev = L.mpx_conv_set_band_mode(4)
+        for k in range(REPS + 6):
+            img, out = pairs[k % 6]
+            ops.conv(img, "sobel5", out)
+        torch.cuda.synchronize()
+        L.mpx_conv_set_band_mode(prev)
         del pairs
     if "lab1" in which:
         a = torch.rand(1 << 26, device=dev)
