@@ -245,6 +245,13 @@ class SlabEdgeDetector:
         ops.conv_rows(self.buf, self.out, self.filter, src_row0=s.own_offset, out_row0=0, oy0=a, oy1=b,
                       y_lo=s.y_lo, y_hi=s.y_hi)
 
+    def cache_resident(self, flag: bool = True) -> None:
+        """Hint that this detector's input stays cache-resident between steps
+        (one small slab re-convolved): its static launches then load rows with
+        the default cache policy instead of non-temporal loads (MPX_CONV_RESIDENT)."""
+        for ln in [*self._all_b, self._all, self._interior, *self._boundary]:
+            ln.resident = flag
+
     @property
     def independent_steps(self) -> bool:
         """True when this detector's steps may run on any stream of the caller's

@@ -86,15 +86,24 @@ def _conv_args(src: torch.Tensor, out: torch.Tensor, filt: Filter, src_row0: int
     return (sp, op, w, pitch, oy0, oy1, y_lo, y_hi, filt.k, filt.anchor, filt.mode, wx, wy)
 
 
+# mode flag (native/include/mpx/common.h): the input is likely cache-resident
+CONV_RESIDENT = 32
+
+
 def conv_rows(src: torch.Tensor, out: torch.Tensor, filt: Filter, *, src_row0: int, out_row0: int,
-              oy0: int, oy1: int, y_lo: int, y_hi: int, direct: bool = False) -> None:
+              oy0: int, oy1: int, y_lo: int, y_hi: int, direct: bool = False, resident: bool = False) -> None:
     """Low-level KxK conv over logical rows [oy0, oy1).
 
     ``src`` / ``out`` are (rows, W, 4) buffers whose logical row 0 is at
     ``src_row0`` / ``out_row0``; reads are clamped into logical rows
     [y_lo, y_hi] (negative / past-the-end rows are resident halo rows).
+    ``resident``: the input is likely cache-resident (a small working set
+    re-read call after call): load it with the default cache policy instead of
+    the non-temporal loads that suit images streaming from HBM. Same results.
     """
     args = _conv_args(src, out, filt, src_row0, out_row0, oy0, oy1, y_lo, y_hi)
+    if resident and src.is_cuda:  # a GPU load-policy hint; the CPU path ignores it
+        args = args[:10] + (args[10] | CONV_RESIDENT,) + args[11:]
     if oy1 <= oy0:
         return
     L = _native.lib()
@@ -130,6 +139,20 @@ class ConvLauncher:
             self.args = (a[0], peer.up_ptr, peer.dn_ptr, peer.slab.rows) + a[1:]
             self.fn = L.mpx_conv_peer
         self._keep = (src, out, peer)
+        self._mode_at = 10 if peer is None else 13  # index of the mode in self.args
+
+    @property
+    def resident(self) -> bool:
+        """The load-policy hint (``conv_rows``'s ``resident``) of this launch."""
+        return bool(self.args[self._mode_at] & CONV_RESIDENT)
+
+    @resident.setter
+    def resident(self, flag: bool) -> None:
+        if not self.cuda:
+            return
+        m = self.args[self._mode_at] & ~CONV_RESIDENT
+        i = self._mode_at
+        self.args = self.args[:i] + (m | (CONV_RESIDENT if flag else 0),) + self.args[i + 1:]
 
     def __call__(self, stream: Optional[int] = None) -> None:
         if self.empty:
@@ -142,11 +165,14 @@ class ConvLauncher:
             self.fn(*self.args)
 
 
-def conv(img: torch.Tensor, filt="sobel5", out: Optional[torch.Tensor] = None, direct: bool = False) -> torch.Tensor:
-    """Whole-image KxK conv with clamp-to-edge borders."""
+def conv(img: torch.Tensor, filt="sobel5", out: Optional[torch.Tensor] = None, direct: bool = False,
+         resident: bool = False) -> torch.Tensor:
+    """Whole-image KxK conv with clamp-to-edge borders (``resident``: see
+    ``conv_rows``)."""
     f = get_filter(filt) if isinstance(filt, str) else filt
     h, w = check_image(img)
     if out is None:
         out = torch.empty_like(img)
-    conv_rows(img, out, f, src_row0=0, out_row0=0, oy0=0, oy1=h, y_lo=0, y_hi=h - 1, direct=direct)
+    conv_rows(img, out, f, src_row0=0, out_row0=0, oy0=0, oy1=h, y_lo=0, y_hi=h - 1, direct=direct,
+              resident=resident)
     return out

@@ -42,6 +42,15 @@ enum mpx_conv_mode {
  * first, clamp-to-edge in x and y), then one fp32 multiply by the scale.
  */
 #define MPX_CONV_SEP 16
+/*
+ * Load-policy hint: OR MPX_CONV_RESIDENT into the mode when the input rows are
+ * likely cache-resident (a small working set re-read across calls). The band
+ * kernel then loads every row with the default cache policy instead of the
+ * non-temporal interior-row loads that suit images streaming from HBM
+ * (MI355X 4096^2: one resident pair 548-567 -> 580-614 Gpixel/s, 6 rotated
+ * pairs 712-723 -> 654; profiles/lab2_conv.md). Results are identical.
+ */
+#define MPX_CONV_RESIDENT 32
 #define MPX_CONV_BASE(m) ((m) & 3)
 #define MPX_SEP_NTAPS(k) (2 * (k) + 1)
 

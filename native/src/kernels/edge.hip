@@ -114,7 +114,10 @@ int conv_impl(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, int 
     MPX_CHECK_ARG(w > 0 && pitch >= w, "bad width/pitch");
     MPX_CHECK_ARG(k >= 1 && k <= MPX_MAX_K && anchor >= 0 && anchor < k, "bad window");
     const bool sep = (mode & MPX_CONV_SEP) != 0;
-    mode = MPX_CONV_BASE(mode) | (mode & ~(MPX_CONV_SEP | 3));  // any unknown flag fails the range check
+    // the load-policy hint travels to launch_band through a thread-local (the
+    // launch is synchronous in this thread); restored on every return
+    const edgel::ResidentHint hint((mode & MPX_CONV_RESIDENT) != 0);
+    mode = MPX_CONV_BASE(mode) | (mode & ~(MPX_CONV_SEP | MPX_CONV_RESIDENT | 3));  // any unknown flag fails the range check
     MPX_CHECK_ARG(mode >= MPX_CONV_MAG2 && mode <= MPX_CONV_LIN1, "bad mode");
     MPX_CHECK_ARG(mode != MPX_CONV_MAG2 || wy, "MAG2 needs wy");
     MPX_CHECK_ARG(y_lo <= y_hi && oy0 >= 0, "bad row range");

@@ -204,6 +204,14 @@ inline int band_mode_env() {
 }
 inline std::atomic<int> g_band_mode{band_mode_env()};
 inline int band_mode() { return g_band_mode.load(std::memory_order_relaxed); }
+// MPX_CONV_RESIDENT for the launch in flight on this thread: the default mode
+// (3) then keeps plain interior-row loads (OPT 2), as mode 2 does
+inline thread_local bool tl_conv_resident = false;
+struct ResidentHint {
+    bool prev;
+    explicit ResidentHint(bool r) : prev(tl_conv_resident) { tl_conv_resident = r; }
+    ~ResidentHint() { tl_conv_resident = prev; }
+};
 // Small images (below kBandMinPixels) keep the wave kernel: with one resident
 // round of 16-row segments a 1-Mpx image is only a few hundred waves, and the
 // reference harness's cold single launches on its 0.5-2 Mpx images measured
@@ -231,7 +239,7 @@ int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     }
     if (m == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-    if (m == 2)
+    if (m == 2 || tl_conv_resident)
         return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
     return launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
 }

@@ -470,3 +470,26 @@ def test_classify_env_variants_match_cpu(gpu, env, tmp_path):
                    timeout=120)
     res = torch.load(p, weights_only=True)
     assert all(res.values()), res
+
+
+@pytest.mark.parametrize("fname", ["sobel5", "gauss5", "roberts", "sobel5_dense"])
+def test_conv_resident_hint_same_bytes(gpu, fname):
+    """MPX_CONV_RESIDENT (ops.conv(..., resident=True), ConvLauncher.resident)
+    changes only the band kernel's load policy: the bytes equal the default
+    launch's and the CPU reference's (2048^2: above the band kernel's 4 Mpx
+    threshold)."""
+    img = rand_img(2048, 2048, seed=21)
+    d = img.to(gpu)
+    a = ops.conv(d, fname)
+    b = ops.conv(d, fname, resident=True)
+    assert torch.equal(a, b)
+    assert torch.equal(a.cpu(), ops.conv(img, fname))
+    out = torch.empty_like(d)
+    ln = ops.ConvLauncher(d, out, ops.get_filter(fname), src_row0=0, out_row0=0, oy0=0, oy1=2048, y_lo=0, y_hi=2047)
+    ln.resident = True
+    assert ln.resident
+    ln()
+    torch.cuda.synchronize()
+    assert torch.equal(out, a)
+    ln.resident = False
+    assert not ln.resident
