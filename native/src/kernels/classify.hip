@@ -1280,6 +1280,10 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
                 }
             } else if (nq == 2)
                 hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            else if ((o & 24) == 24)  // 4 pixels per thread (5 waves per SIMD), two trips in flight
+                hipLaunchKernelGGL((classify_fast32_kernel<1, 24>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            else if (o & 8)
+                hipLaunchKernelGGL((classify_fast32_kernel<1, 8>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             else
                 hipLaunchKernelGGL(classify_fast32_kernel<1>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
