@@ -1123,15 +1123,17 @@ int classify_choose(int nc, int path, bool fast_ok) {
 }
 
 // AUTO runs MFMA8 (its statistics permitting) where it measured faster than
-// FAST32: exactly 16 classes (accumulator registers 0-7 all real) and from 22
-// up. Same box, 8192^2, two runs each, µs (profiles/lab3_classify.md):
-//   nc      8        12       14       16       17       18       20       22       24
-//   fast  208-211  279-285  323-330  356-361  384-386  392-395  417-422  454-457  480-490
-//   mfma8 260-282  330-341  340-344  342-342  405-408  394-405  416-418  405-415  415-430
+// FAST32: exactly 16 classes (accumulator registers 0-7 all real) and from 21
+// up. Round 4 (fast32 interleaved chains, mfma8 fp32 re-rank stage), same box,
+// 8192^2, three rotated images, two runs each, median µs
+// (profiles/raw/r4/r/, profiles/lab3_classify.md):
+//   nc      8        12       15       16       17       19       20       21       22       24       32
+//   fast  191-192  239-245  288-289  298-300  315-316  346-347  353-358  367-370  383-385  410      520
+//   mfma8 234-244  286-293  293-300  293-298  348-349  353-355  351-354  345-346  354-368  356-359  416-420
 // MFMA8's ranking cost steps with the accumulator registers it must rank
 // (8 for <= 16 classes, 12 for <= 24, 16 for <= 32), FAST32's grows
-// linearly; nc 32: 634 / 498.
-constexpr int kAutoMfma8MinClasses = 22;
+// linearly; nc = 20 is a tie and stays on FAST32.
+constexpr int kAutoMfma8MinClasses = 21;
 inline bool auto_mfma8(int nc) { return nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with

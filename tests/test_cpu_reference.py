@@ -148,10 +148,12 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
     mu14, inv14 = stats(14)
     assert ops.classify_plan(mu14, inv14, "auto")[0] == "fast"
-    # at exactly 16 and from 22 classes AUTO runs the exact int8-MFMA distance
+    # at exactly 16 and from 21 classes AUTO runs the exact int8-MFMA distance
     # GEMM (measured faster there; margin in key units)
     mu16, inv16 = stats(16)
     assert ops.classify_plan(mu16, inv16, "auto")[0] == "mfma8"
+    mu21, inv21 = stats(21)
+    assert ops.classify_plan(mu21, inv21, "auto")[0] == "mfma8"
     mu28, inv28 = stats(28)
     path28, margin28 = ops.classify_plan(mu28, inv28, "auto")
     assert path28 == "mfma8" and margin28 >= 1
