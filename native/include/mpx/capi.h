@@ -317,11 +317,6 @@ int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t works
 /* After the sort's stream drained: non-zero if a bounded look-back wait of the
  * sort that last used `workspace` gave up (hardware-fault detector). */
 int mpx_sort_ws_status(const void *workspace, int64_t n, int dtype);
-/* Tuning probe: count + scan + lean scatter for each digit of the unchanged
- * keys with step knock-outs (radix_scatter_lean_kernel KNOCK: 0, 1, 6, 12, 14,
- * 16, 31); the workspace holds garbage afterwards, `data` is not modified. */
-int mpx_sort_scatter_probe(const void *data, int64_t n, void *workspace, int64_t workspace_bytes, int knock,
-                           void *stream);
 int mpx_sort(void *data, int64_t n, int dtype, void *stream);
 
 /* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */

@@ -1,0 +1,32 @@
+/* Tuning entry points of libmpx.so (not part of the production C API in
+ * capi.h). They live beside file-local kernels that libmpx_tune.so cannot
+ * reach: the sort's schedule variants and its scatter attribution probe.
+ * Used by tools/experiments/{lab5_bench,sort_probe}.py and the GPU sort suite. */
+#ifndef MPX_TUNING_H
+#define MPX_TUNING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The sort with a fixed radix schedule (sort.hip, radix_sort32): 0 = AUTO,
+ * 1 onesweep (look-back), 2 reduce-then-scan, 4 / 7 / 8 persistent scatters
+ * (round 2-3), 9-13 the returning-add ranking (8192 / 4096-key tiles, 3 blocks
+ * per CU, two tiles in flight), 14 the lean onesweep, 15 = 12 with the
+ * peer-mask ranking for float32's last pass. */
+int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
+                     void *stream);
+
+/* Count + scan + lean scatter for each digit of the unchanged keys with step
+ * knock-outs (radix_scatter_lean_kernel KNOCK: 0, 1, 6, 12, 14, 16, 31); the
+ * workspace holds garbage afterwards, `data` is not modified. */
+int mpx_sort_scatter_probe(const void *data, int64_t n, void *workspace, int64_t workspace_bytes, int knock,
+                           void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -42,6 +42,7 @@
 #include <mutex>
 
 #include "internal.hpp"
+#include "mpx/tuning.h"
 
 namespace mpx {
 namespace {
