@@ -1289,9 +1289,7 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
 // 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2), 14 = the lean
 // onesweep (one histogram read, then decoupled look-back per digit pass):
-// correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md); 15 = 12
-// with the peer-mask ranking (RANK 0) for float32's last pass, whose few
-// distinct top bytes serialise a returning add's same-address lanes. Retired after round-3
+// correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1408,11 +1406,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 else if (variant == 11)  // 3 blocks (24 waves) per CU: the returning-add ranking frees the table's LDS
                     launch_lean<kRThreads, 1, 6>(p, mode, std::min(kNumCUs * 3, rounded), s, src, dst, n, r.hist,
                                                  r.status, ntiles);
-                else if (variant == 12 || (variant == 15 && !(p == 3 && mode == kRawF32)))  // 9, two tiles in flight
+                else if (variant == 12)  // 9 with two tiles of keys in flight
                     launch_lean<kRThreads, 1, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
                                                     r.status, ntiles);
-                else if (variant == 15)  // float32's last pass (a few top bytes): the peer-mask ranking
-                    launch_lean(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist, r.status, ntiles);
                 else if (variant == 13)  // 10 with two tiles of keys in flight
                     launch_lean<kRThreads / 2, 1, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
                                                         r.hist, r.status, ntiles);
@@ -1613,8 +1609,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 15 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 15", variant);
+    if (variant < 0 || variant > 14 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 14", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
