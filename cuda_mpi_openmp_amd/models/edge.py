@@ -122,6 +122,10 @@ class SlabEdgeDetector:
                                                            src_row0=s.own_offset, out_row0=0, oy0=lo, oy1=hi,
                                                            y_lo=s.y_lo, y_hi=s.y_hi, peer=peer)
         self._all_b = [mk(b, 0, s.rows) for b in self.bufs]
+        # the owned rows of each buffer, built once: a stream-mode step returns
+        # one of them (a fresh slice per step costs microseconds of host time
+        # against a ~23 us step)
+        self._own_views = [b[s.own_offset: s.own_offset + s.rows] for b in self.bufs]
         self._all = self._all_b[0]
         self._interior = mk(self.bufs[0], *s.interior())
         self._boundary = [mk(self.bufs[0], a, b) for a, b in s.boundary()]
@@ -168,8 +172,7 @@ class SlabEdgeDetector:
     def stream_out(self) -> torch.Tensor:
         """Stream mode: the owned rows the most recent step wrote (its output,
         the next step's input)."""
-        s = self.slab
-        return self.bufs[self._sk % 2][s.own_offset: s.own_offset + s.rows]
+        return self._own_views[self._sk % 2]
 
     @property
     def own(self) -> torch.Tensor:
