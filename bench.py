@@ -158,7 +158,7 @@ def run(args) -> int:
         if len(dets) % args.streams:
             raise SystemExit(f"--streams {args.streams} must divide --rotate {len(dets)}")
         nstreams = args.streams
-    streams = [torch.cuda.Stream(ctx.device) for _ in range(nstreams)] if nstreams > 1 else []
+    streams = hip_streams(ctx.device, nstreams) if nstreams > 1 else []
     handles = [s.cuda_stream for s in streams]
     if streams:  # every stream starts after the set-up work of the current one
         for s in streams:
@@ -355,6 +355,22 @@ def run(args) -> int:
     return 0 if ok else 1
 
 
+_STREAMS: list = []
+
+
+def hip_streams(device, k: int) -> list:
+    """The first k streams of one process-wide set, created once: both phases
+    overlap their frames on the SAME streams. HIP binds each new stream to one
+    of GPU_MAX_HW_QUEUES (4) hardware queues round-robin; two fresh streams
+    made after the static phase's landed on one queue (rocprofv3 queue_id),
+    which serialised the streaming phase's frames."""
+    import torch
+
+    while len(_STREAMS) < k:
+        _STREAMS.append(torch.cuda.Stream(device))
+    return _STREAMS[:k]
+
+
 def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     """value_streaming: K timed steps of the iterated filter over the rotated
     slabs (each step's halo rows were produced by the neighbours' previous
@@ -381,7 +397,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     want = args.stream_streams or (args.streams if n > 1 else 1)
     ns = want if (want > 1 and ctx.device.type == "cuda" and len(sdets) % want == 0
                   and all(d.independent_steps for d in sdets)) else 1
-    shandles = [torch.cuda.Stream(ctx.device) for _ in range(ns)] if ns > 1 else []
+    shandles = hip_streams(ctx.device, ns) if ns > 1 else []
     for st in shandles:
         st.wait_stream(torch.cuda.current_stream(ctx.device))
     shandles = [st.cuda_stream for st in shandles]
