@@ -100,8 +100,7 @@ def parse_args(argv=None):
                         "Only where steps are independent (one rank or static peer halos)")
     p.add_argument("--stream-streams", type=int, default=0,
                    help="HIP streams for the streaming phase's slab sequences (each sequence stays on one stream); "
-                        "0 = auto: 1 on one rank (no waits to fill: a second stream measured 1.5%% slower), "
-                        "--streams on several ranks (a second stream keeps the GPU busy while edge waves wait)")
+                        "0 = --streams (the static phase's streams, reused: N = 1 586 -> 652-663 Gpixel/s)")
     p.add_argument("--graph", type=int, default=0,
                    help="capture this many steps into one HIP graph and replay it (0 = eager launches; "
                         "in-order and peer halo modes)")
@@ -392,9 +391,9 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
         cyc[0] += 1
 
     # each slab's frame sequence stays on one stream; different slabs' sequences
-    # are independent and overlap on `--streams` streams (device-signalled or no
-    # halos only: host-ordered RCCL exchanges keep one stream)
-    want = args.stream_streams or (args.streams if n > 1 else 1)
+    # are independent and overlap on the static phase's streams (device-signalled
+    # or no halos only: host-ordered RCCL exchanges keep one stream)
+    want = args.stream_streams or args.streams
     ns = want if (want > 1 and ctx.device.type == "cuda" and len(sdets) % want == 0
                   and all(d.independent_steps for d in sdets)) else 1
     shandles = hip_streams(ctx.device, ns) if ns > 1 else []
