@@ -354,20 +354,15 @@ def run(args) -> int:
     return 0 if ok else 1
 
 
-_STREAMS: list = []
-
-
 def hip_streams(device, k: int) -> list:
-    """The first k streams of one process-wide set, created once: both phases
-    overlap their frames on the SAME streams. HIP binds each new stream to one
-    of GPU_MAX_HW_QUEUES (4) hardware queues round-robin; two fresh streams
-    made after the static phase's landed on one queue (rocprofv3 queue_id),
-    which serialised the streaming phase's frames."""
-    import torch
+    """The first k streams of the process-wide compute set (created by
+    parallel.init before any communicator): both phases overlap their frames on
+    the SAME streams, each on a hardware queue of its own. Two fresh streams
+    made after the static phase's had landed on one queue (rocprofv3
+    queue_id), which serialised the streaming phase's frames."""
+    from cuda_mpi_openmp_amd.utils.streams import compute_streams
 
-    while len(_STREAMS) < k:
-        _STREAMS.append(torch.cuda.Stream(device))
-    return _STREAMS[:k]
+    return compute_streams(device, k)
 
 
 def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:

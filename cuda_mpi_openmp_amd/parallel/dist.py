@@ -87,6 +87,11 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
             raise SystemExit(2)
         torch.cuda.set_device(local_rank % ndev)
         dev = torch.device("cuda", local_rank % ndev)
+        # the compute stream pair before any communicator creates its streams:
+        # they get hardware queues of their own (utils/streams.py)
+        from ..utils.streams import compute_streams
+
+        compute_streams(dev, 2)
     else:
         dev = torch.device("cpu")
     if backend is None:
