@@ -14,7 +14,7 @@ extern "C" {
 /* The sort with a fixed radix schedule (sort.hip, radix_sort32): 0 = AUTO,
  * 1 onesweep (look-back), 2 reduce-then-scan, 4 / 7 / 8 persistent scatters
  * (round 2-3), 9-13 the returning-add ranking (8192 / 4096-key tiles, 3 blocks
- * per CU, two tiles in flight), 14 the lean onesweep. */
+ * per CU, two tiles in flight), 14 the lean onesweep, 15 the same at one block per CU. */
 int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                      void *stream);
 

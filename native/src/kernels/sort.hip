@@ -945,7 +945,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // look back over the predecessors' status words, kLbWin at a time (one
 // round trip covers kLbWin tiles), until an inclusive prefix (flag P) ->
 // publish this tile's inclusive prefix -> write out.
-template <int IN_MODE, int OUT_MODE, int kLbWin = 8>
+// STATIC (variant 16, experiment): block b takes tiles b, b + G, b + 2G ... in
+// order, no tile counter (one atomic word saturates near 88 adds per us on
+// this chip, MI355X_MICROARCH.md). Deadlock-free only while every block of
+// the grid is resident at once (2 per CU here); a block that never starts
+// leaves its tiles' successors spinning to kSpinLimit, the error word set.
+template <int IN_MODE, int OUT_MODE, int kLbWin = 8, bool STATIC = false>
 __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) void radix_onesweep_lean_kernel(
     const uint32_t *__restrict__ in, uint32_t *__restrict__ out, int64_t n, int shift,
     const uint32_t *__restrict__ tot, uint32_t *__restrict__ status, uint32_t *__restrict__ tile_ctr,
@@ -958,9 +963,9 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     __shared__ int s_next;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;
-    if (t == 0) s_next = (int)atomicAdd(tile_ctr, 1u);
+    if (!STATIC && t == 0) s_next = (int)atomicAdd(tile_ctr, 1u);
     const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);  // its barrier publishes s_next
-    int tile = s_next;
+    int tile = STATIC ? (int)blockIdx.x : s_next;
     if (tile >= ntiles) return;  // block-uniform
     const uint32_t n32 = (uint32_t)n;
     const int nbytes = (int)(n32 * 4u);
@@ -1082,6 +1087,17 @@ __global__ __launch_bounds__(kRThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 
     uint32_t a[kRPer], b[kRPer];
     load_tile(a, tile);
+    if constexpr (STATIC) {
+        for (int next = tile + (int)gridDim.x;; next += (int)gridDim.x) {
+            if (next < ntiles) load_tile(b, next);
+            do_tile(a, tile);
+            if (next >= ntiles) break;
+            tile = next;
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+        }
+        return;
+    }
     lds_barrier();  // every thread has read s_next
     if (t == 0) s_next = (int)atomicAdd(tile_ctr, 1u);
     lds_barrier();
@@ -1335,9 +1351,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
-    if (variant == 1 || variant == 14) {
+    if (variant == 1 || variant >= 14) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
-        if (variant == 14)
+        if (variant != 1)
             hipLaunchKernelGGL(radix_hist4_kernel,
                                dim3(std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, kNumCUs * 2))), dim3(256),
                                0, s, x, n, mode, r.hist);
@@ -1355,13 +1371,22 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
         const uint32_t *src = (p & 1) ? r.tmp : x;
         uint32_t *dst = (p & 1) ? x : r.tmp;
         const int in_mode = p == 0 ? mode : (int)kRawKeys, out_mode = p == 3 ? mode : (int)kRawKeys;
-        if (variant == 14) {
-            const dim3 g((unsigned)std::min(kNumCUs * 2, ntiles)), b(kRThreads);
+        if (variant >= 14) {
+            // 15: one block per CU — half the tiles in flight, so half the
+            // predecessors a look-back walks before it meets an inclusive prefix;
+            // 16: static tile order (no counter), all blocks co-resident
+            const dim3 g((unsigned)std::min(kNumCUs * (variant == 15 ? 1 : 2), ntiles)), b(kRThreads);
             uint32_t *st = r.status + (size_t)p * ntiles * 256;
             const bool f = mode == kRawF32;
-#define MPX_OS1(I, O, W) \
-    hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O, W>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
-#define MPX_OS(I, O) MPX_OS1(I, O, 8)
+#define MPX_OS1(I, O, W, ST) \
+    hipLaunchKernelGGL((radix_onesweep_lean_kernel<I, O, W, ST>), g, b, 0, s, src, dst, n, 8 * p, r.hist + 256 * p, st, r.ctr + p, r.err, ntiles)
+#define MPX_OS(I, O)                   \
+    do {                               \
+        if (variant == 16)             \
+            MPX_OS1(I, O, 8, true);    \
+        else                           \
+            MPX_OS1(I, O, 8, false);   \
+    } while (0)
             if (p == 0 && f)
                 MPX_OS(kRawF32, kRawKeys);
             else if (p == 0)
@@ -1609,8 +1634,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 14 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 14", variant);
+    if (variant < 0 || variant > 16 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 16", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
