@@ -252,8 +252,27 @@ class SlabEdgeDetector:
         """Hint that this detector's input stays cache-resident between steps
         (one small slab re-convolved): its static launches then load rows with
         the default cache policy instead of non-temporal loads (MPX_CONV_RESIDENT)."""
-        for ln in [*self._all_b, self._all, self._interior, *self._boundary]:
+        twin = [self._twin[1]] if getattr(self, "_twin", None) else []
+        for ln in [*self._all_b, self._all, self._interior, *self._boundary, *twin]:
             ln.resident = flag
+
+    def step_twin(self, stream: int) -> torch.Tensor:
+        """The static step into a second output slab, on ``stream``: with
+        ``step`` on another stream, two steps of the SAME input run
+        concurrently without a write race (the bench's cache-resident pass:
+        one 64 MiB input + two outputs stay inside the 256 MiB MALL).
+        Independent static steps only."""
+        if self.stream or not self.independent_steps:
+            raise RuntimeError("step_twin needs independent static steps (one rank or peer halos)")
+        if getattr(self, "_twin", None) is None:
+            s = self.slab
+            out2 = torch.empty_like(self.out)
+            ln = ops.ConvLauncher(self.bufs[0], out2, self.filter, src_row0=s.own_offset, out_row0=0, oy0=0,
+                                  oy1=s.rows, y_lo=s.y_lo, y_hi=s.y_hi, peer=self.peer)
+            ln.resident = self._all.resident
+            self._twin = (out2, ln)
+        self._twin[1](stream)
+        return self._twin[0]
 
     @property
     def independent_steps(self) -> bool:

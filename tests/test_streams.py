@@ -26,3 +26,28 @@ def test_compute_streams_are_shared_and_distinct(gpu):
     for st in a:
         main.wait_stream(st)
     assert all(torch.equal(o, torch.full_like(x, 2.0)) for o in outs)
+
+
+def test_step_twin_matches_step(gpu):
+    """bench.py's cache-resident pass: step and step_twin of one input on two
+    streams write identical slabs (resident hint on and off)."""
+    from cuda_mpi_openmp_amd import parallel
+    from cuda_mpi_openmp_amd.models.edge import EdgeDetector, SlabEdgeDetector
+    from cuda_mpi_openmp_amd.utils.streams import compute_streams
+
+    ctx = parallel.DistContext(device=gpu)
+    d = SlabEdgeDetector(ctx, 512, 384, "sobel5")
+    d.fill_random(seed=3)
+    s0, s1 = compute_streams(gpu, 2)
+    main = torch.cuda.current_stream(gpu)
+    for flag in (False, True):
+        d.cache_resident(flag)
+        s0.wait_stream(main)
+        s1.wait_stream(main)
+        a = d.step(s0.cuda_stream)
+        b = d.step_twin(s1.cuda_stream)
+        main.wait_stream(s0)
+        main.wait_stream(s1)
+        assert a.data_ptr() != b.data_ptr()
+        assert torch.equal(a, b)
+        assert torch.equal(a.cpu(), EdgeDetector("sobel5").reference(d.own.cpu()))
