@@ -200,7 +200,11 @@ def run(args) -> int:
         ctx.barrier()
 
     def timed(step_fn, k: int) -> float:
-        """Exactly k steps bracketed by barrier + device sync on both sides."""
+        """Exactly k steps bracketed by barrier + device sync on both sides.
+        Each rank's clock stops at its own closing device sync, before the
+        closing barrier: the barrier (an RCCL all-reduce plus a device sync at
+        N > 1) is bracket, not step, and the max over ranks taken by the
+        caller still charges the slowest rank's steps in full."""
         ctx.barrier()
         sync()
         t0 = time.perf_counter()
@@ -214,8 +218,9 @@ def run(args) -> int:
         for d in dets:
             d.finish()
         sync()
+        dt = time.perf_counter() - t0
         ctx.barrier()
-        return time.perf_counter() - t0
+        return dt
 
     # ---- timed region: exactly `steps` steps over the rotated pairs ----
     cyc[0] = 0
