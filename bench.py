@@ -31,7 +31,8 @@ over ranks).
 an input that changes every step: the filter is iterated (step k convolves
 step k-1's output) over the same rotated working set, so for N > 1 every step
 needs halo rows the neighbours produced in the previous step — ordered on the
-device by a signalled fetch kernel (peer) or by in-order RCCL send/recv.
+device by step words the conv kernel's own slab-edge waves wait on and
+publish (peer, one dispatch per step) or by in-order RCCL send/recv.
 Verified after the timed region: the gathered N-rank result of every rotated
 slab equals a one-device whole-image run of the same frame sequence, and each
 rank's last step equals the CPU reference on its halo-filled input. Every output pixel of every rotated pair on every rank is
@@ -134,6 +135,7 @@ def run(args) -> int:
     from cuda_mpi_openmp_amd import ops, parallel
     from cuda_mpi_openmp_amd.models.edge import SlabEdgeDetector
     from cuda_mpi_openmp_amd.parallel import launch
+    from cuda_mpi_openmp_amd.utils.streams import wait_policy_in_force
 
     ctx = parallel.init(device=args.device)
     launch.check_world(args.gpus, ctx.world)
@@ -337,6 +339,7 @@ def run(args) -> int:
                 "halo_rows": [d0.filter.halo_up, d0.filter.halo_down],
                 "graph_steps": args.graph if graph is not None else 0,
                 "streams": nstreams,
+                "host_wait": wait_policy_in_force(ctx.device) if ctx.device.type == "cuda" else None,
                 "rotate": len(dets),
                 "working_set_MiB_per_gpu": round(len(dets) * 2 * args.size * args.size * 4 / 2**20, 1),
             },

@@ -89,8 +89,9 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
         dev = torch.device("cuda", local_rank % ndev)
         # the compute stream pair before any communicator creates its streams:
         # they get hardware queues of their own (utils/streams.py)
-        from ..utils.streams import compute_streams
+        from ..utils.streams import compute_streams, host_wait_policy
 
+        host_wait_policy(dev)  # MPX_HIP_WAIT: how host syncs detect completion
         compute_streams(dev, 2)
     else:
         dev = torch.device("cpu")

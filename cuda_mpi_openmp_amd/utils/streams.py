@@ -10,7 +10,9 @@ possible — ``parallel.init`` makes the first two right after selecting the
 device, before any communicator exists — and every user takes its streams
 from it.
 """
-from typing import List
+import ctypes
+import os
+from typing import List, Optional
 
 import torch
 
@@ -25,3 +27,39 @@ def compute_streams(device: torch.device, k: int) -> List[torch.cuda.Stream]:
     while len(pool) < k:
         pool.append(torch.cuda.Stream(torch.device("cuda", key)))
     return pool[:k]
+
+
+_WAIT_FLAGS = {"auto": 0, "spin": 1, "yield": 2}
+_WAIT_IN_FORCE: dict = {}
+
+
+def wait_policy_in_force(device: torch.device) -> str:
+    """The policy the last ``host_wait_policy`` call set on ``device``."""
+    return _WAIT_IN_FORCE.get(torch.device(device).index, "auto")
+
+
+def host_wait_policy(device: torch.device, mode: Optional[str] = None) -> str:
+    """How host waits on this device (``torch.cuda.synchronize``, event
+    waits) detect completion: ``hipSetDeviceFlags`` schedule flag. HIP's
+    ``auto`` picks *yield* whenever the machine has more logical CPUs than HIP
+    contexts — the waiting thread then sleeps on a completion interrupt after a
+    short active-wait window, and wakes up late. ``spin`` polls the completion
+    signal on the waiting thread (one CPU core while it waits). ``mode``
+    defaults to ``MPX_HIP_WAIT`` (auto | spin | yield). Returns the policy in
+    force."""
+    mode = (mode or os.environ.get("MPX_HIP_WAIT", "auto")).lower()
+    if mode not in _WAIT_FLAGS:
+        raise ValueError(f"MPX_HIP_WAIT must be one of {sorted(_WAIT_FLAGS)}, not {mode!r}")
+    if mode == "auto" or torch.device(device).type != "cuda":
+        return "auto"  # the runtime's own choice, untouched
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
+    idx = torch.device(device).index
+    prev = ctypes.c_int()
+    hip.hipGetDevice(ctypes.byref(prev))
+    if idx is not None:
+        hip.hipSetDevice(idx)
+    rc = hip.hipSetDeviceFlags(ctypes.c_uint(_WAIT_FLAGS[mode]))
+    hip.hipSetDevice(prev.value)
+    res = mode if rc == 0 else f"auto (hipSetDeviceFlags({mode}) returned {rc})"
+    _WAIT_IN_FORCE[idx] = res
+    return res
