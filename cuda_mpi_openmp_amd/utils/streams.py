@@ -50,7 +50,9 @@ def host_wait_policy(device: torch.device, mode: Optional[str] = None) -> str:
     mode = (mode or os.environ.get("MPX_HIP_WAIT", "auto")).lower()
     if mode not in _WAIT_FLAGS:
         raise ValueError(f"MPX_HIP_WAIT must be one of {sorted(_WAIT_FLAGS)}, not {mode!r}")
-    if mode == "auto" or torch.device(device).type != "cuda":
+    if torch.device(device).type != "cuda":
+        return "auto"
+    if mode == "auto" and torch.device(device).index not in _WAIT_IN_FORCE:
         return "auto"  # the runtime's own choice, untouched
     hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded (same soname)
     idx = torch.device(device).index
@@ -61,5 +63,8 @@ def host_wait_policy(device: torch.device, mode: Optional[str] = None) -> str:
     rc = hip.hipSetDeviceFlags(ctypes.c_uint(_WAIT_FLAGS[mode]))
     hip.hipSetDevice(prev.value)
     res = mode if rc == 0 else f"auto (hipSetDeviceFlags({mode}) returned {rc})"
-    _WAIT_IN_FORCE[idx] = res
+    if mode == "auto" and rc == 0:
+        _WAIT_IN_FORCE.pop(idx, None)
+    else:
+        _WAIT_IN_FORCE[idx] = res
     return res

@@ -1,12 +1,13 @@
-"""The process-wide compute stream set (utils/streams.py): created once,
-shared by every caller, distinct streams."""
+"""utils/streams.py: the process-wide compute stream set (created once,
+shared by every caller, distinct streams), the detector's twin-output step the
+bench's cache-resident pass runs on it, and the host wait policy."""
 
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.gpu
 def test_compute_streams_are_shared_and_distinct(gpu):
     from cuda_mpi_openmp_amd.utils.streams import compute_streams
 
@@ -28,6 +29,7 @@ def test_compute_streams_are_shared_and_distinct(gpu):
     assert all(torch.equal(o, torch.full_like(x, 2.0)) for o in outs)
 
 
+@pytest.mark.gpu
 def test_step_twin_matches_step(gpu):
     """bench.py's cache-resident pass: step and step_twin of one input on two
     streams write identical slabs (resident hint on and off)."""
@@ -53,3 +55,24 @@ def test_step_twin_matches_step(gpu):
         # bit for bit against the native CPU conv (the plain fp32 PyTorch
         # reference is within 1 of both: test_gpu_kernels.py)
         assert torch.equal(a.cpu(), ops.conv(d.own.cpu().contiguous(), "sobel5"))
+
+
+def test_host_wait_policy_names():
+    from cuda_mpi_openmp_amd.utils.streams import host_wait_policy
+
+    assert host_wait_policy(torch.device("cpu"), "spin") == "auto"  # CPU: nothing to set
+    with pytest.raises(ValueError):
+        host_wait_policy(torch.device("cpu"), "busy")
+
+
+@pytest.mark.gpu
+def test_host_wait_policy_sets_and_restores(gpu):
+    from cuda_mpi_openmp_amd.utils.streams import host_wait_policy, wait_policy_in_force
+
+    assert host_wait_policy(gpu, "spin") == "spin"
+    assert wait_policy_in_force(gpu) == "spin"
+    x = torch.ones(1 << 20, device=gpu) * 3  # a wait under the policy
+    torch.cuda.synchronize(gpu)
+    assert float(x[0]) == 3.0
+    assert host_wait_policy(gpu, "auto") == "auto"
+    assert wait_policy_in_force(gpu) == "auto"
