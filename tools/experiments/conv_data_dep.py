@@ -4,7 +4,7 @@ phase convolves uniform random frames; its streaming phase convolves frames
 the filter itself produced (iterated: gray, mostly 0 / 255 with edges). Same
 launches, same 2-stream / 6-pair rotation (ConvLauncher on the compute stream
 pair), different inputs: random, iterated 1 / 2 / 8 times, constant, and
-random gray. Median of 5 rounds of 200 frames, event-timed, us per frame.
+random gray, then three buffer layouts (static, ping-pong). Median of 5 rounds of 200 frames, event-timed, us per frame.
 One JSON line per input kind."""
 import json
 import os
@@ -43,7 +43,7 @@ def main():
         x[..., 1] = x[..., 0]
         x[..., 2] = x[..., 0]
         gray.append(x)
-    kinds = {"random": rnd, "iter1": iterate(rnd, 1), "iter2": iterate(rnd, 2), "iter8": iterate(rnd, 8),
+    kinds = {"random_first": rnd, "random": rnd, "iter1": iterate(rnd, 1), "iter2": iterate(rnd, 2), "iter8": iterate(rnd, 8),
              "const128": [torch.full_like(rnd[0], 128) for _ in range(pairs)], "random_gray": gray}
     outs = [torch.empty_like(rnd[0]) for _ in range(pairs)]
     main_s = torch.cuda.current_stream(dev)
@@ -73,6 +73,42 @@ def main():
         ts.sort()
         print(json.dumps({"input": name, "us_per_frame": round(ts[len(ts) // 2], 2), "min": round(ts[0], 2),
                           "saturated_channel_frac": round(fr["sat"] / (pairs * n * n * 3), 3)}), flush=True)
+
+    # layouts: the static phase reads halo-padded buffers into separate
+    # outputs; the streaming phase ping-pongs between two halo-padded buffers
+    # per sequence (writes land where the previous step of the sequence read)
+    pad = [torch.empty((n + 4, n, 4), dtype=torch.uint8, device=dev) for _ in range(2 * pairs)]
+    for i in range(pairs):
+        pad[2 * i][2:2 + n].copy_(rnd[i])
+        pad[2 * i + 1][2:2 + n].copy_(rnd[i])
+    mk = lambda src, out, orow: ops.ConvLauncher(src, out, f, src_row0=2, out_row0=orow, oy0=0, oy1=n,  # noqa: E731
+                                                 y_lo=0, y_hi=n - 1)
+    layouts = {
+        "static_padded_src": [[mk(pad[2 * i], outs[i], 0)] for i in range(pairs)],
+        "pingpong": [[mk(pad[2 * i], pad[2 * i + 1], 2), mk(pad[2 * i + 1], pad[2 * i], 2)] for i in range(pairs)],
+        "pingpong_one_way": [[mk(pad[2 * i], pad[2 * i + 1], 2)] for i in range(pairs)],
+    }
+    hs = [s.cuda_stream for s in streams]
+    for name, ls in layouts.items():
+        ts = []
+        for rnd_i in range(6):
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_s)
+            for s in streams:
+                s.wait_stream(main_s)
+            for k in range(frames):
+                seq = ls[k % pairs]
+                seq[(k // pairs) % len(seq)](hs[k % 2])
+            for s in streams:
+                main_s.wait_stream(s)
+            e1.record(main_s)
+            e1.synchronize()
+            if rnd_i:
+                ts.append(e0.elapsed_time(e1) * 1e3 / frames)
+        ts.sort()
+        print(json.dumps({"layout": name, "us_per_frame": round(ts[len(ts) // 2], 2), "min": round(ts[0], 2)}),
+              flush=True)
 
 
 if __name__ == "__main__":
