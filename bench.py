@@ -201,6 +201,8 @@ def run(args) -> int:
         sync()
         ctx.barrier()
 
+    issue_s = {}  # step function -> host enqueue time of its last timed run
+
     def timed(step_fn, k: int) -> float:
         """Exactly k steps bracketed by barrier + device sync on both sides.
         Each rank's clock stops at its own closing device sync, before the
@@ -219,14 +221,18 @@ def run(args) -> int:
             step_fn()
         for d in dets:
             d.finish()
+        issued = time.perf_counter() - t0  # host time to enqueue the k steps
         sync()
         dt = time.perf_counter() - t0
         ctx.barrier()
+        issue_s[step_fn] = issued
         return dt
 
     # ---- timed region: exactly `steps` steps over the rotated pairs ----
+    timed.issue_s = issue_s
     cyc[0] = 0
     mine = timed(rot_step, args.steps)
+    enqueue_ms = issue_s[rot_step] * 1e3 / max(1, args.steps)
     watchdog.beat()
     per_rank = parallel.all_gather_floats(mine, ctx)
     elapsed = max(per_rank)
@@ -315,6 +321,7 @@ def run(args) -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
+            "host_enqueue_ms_per_step": round(enqueue_ms, 5),
             "warmup_steps_run": warm_info["steps"],
             "warmup_ms": warm_info["ms"],
             "higher_is_better": True,
@@ -437,6 +444,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     settle(step, len(sdets), args.warmup_ms, ctx, sync, watchdog, parallel, lambda: None)
     cyc[0] = 0
     mine = timed(step, args.steps)
+    enqueue_ms = timed.issue_s[step] * 1e3 / max(1, args.steps)
     watchdog.beat()
     per_rank = parallel.all_gather_floats(mine, ctx)
     elapsed = max(per_rank)
@@ -450,6 +458,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     rec = {"value_streaming": _sig(n * args.size * args.size * args.steps / elapsed / 1e9),
            "streams_streaming": ns,
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
+           "host_enqueue_ms_per_step_streaming": round(enqueue_ms, 5),
            "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
            "transport_streaming": sdets[0].transport if n > 1 else None}
     if not args.no_verify:
