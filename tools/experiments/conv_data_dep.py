@@ -83,8 +83,22 @@ def main():
         pad[2 * i + 1][2:2 + n].copy_(rnd[i])
     mk = lambda src, out, orow: ops.ConvLauncher(src, out, f, src_row0=2, out_row0=orow, oy0=0, oy1=n,  # noqa: E731
                                                  y_lo=0, y_hi=n - 1)
+    # the same buffers' images at shifted bases: the output slab of a
+    # ping-pong step starts `sk` rows (16 KiB each) further from its
+    # allocation's alignment than the input slab does
+    skew = {}
+    for sk in (1, 2, 4):
+        bs = [torch.empty((n + 4 + sk, n, 4), dtype=torch.uint8, device=dev) for _ in range(pairs)]
+        for i in range(pairs):
+            bs[i][sk + 2:sk + 2 + n].copy_(rnd[i])
+        skew[sk] = [b[sk:] for b in bs]
+    aligned_out = [torch.empty((n + 4, n, 4), dtype=torch.uint8, device=dev) for _ in range(pairs)]
     layouts = {
         "static_padded_src": [[mk(pad[2 * i], outs[i], 0)] for i in range(pairs)],
+        "static_out_at_row2": [[mk(pad[2 * i], aligned_out[i], 2)] for i in range(pairs)],
+        "pingpong_skew1": [[mk(pad[2 * i], skew[1][i], 2), mk(skew[1][i], pad[2 * i], 2)] for i in range(pairs)],
+        "pingpong_skew2": [[mk(pad[2 * i], skew[2][i], 2), mk(skew[2][i], pad[2 * i], 2)] for i in range(pairs)],
+        "pingpong_skew4": [[mk(pad[2 * i], skew[4][i], 2), mk(skew[4][i], pad[2 * i], 2)] for i in range(pairs)],
         "pingpong": [[mk(pad[2 * i], pad[2 * i + 1], 2), mk(pad[2 * i + 1], pad[2 * i], 2)] for i in range(pairs)],
         "pingpong_one_way": [[mk(pad[2 * i], pad[2 * i + 1], 2)] for i in range(pairs)],
     }
