@@ -6,6 +6,7 @@ GPU/CPU speedup. Prints one JSON line per measurement.
   lab1  vsub fp32 N = 2^26 and fp64 N = 2^25        (HBM streaming)
   lab2  sobel5 / roberts / sobel3 on 4096^2 RGBA8    (see bench.py for the flagship)
   lab3  Mahalanobis classifier 8192^2, nc = 4/16/32, direct vs fp64-MFMA path
+  lab5  sort 2^26 keys: int32 / float32 radix, uint8 counting sort, vs torch.sort
   jacobi 2-D 5-point sweep, 16384^2 fp64 and fp32 (one GPU's share of the
          8-GPU north-star grid is 2048 x 16384; the full grid is timed here)
 """
@@ -132,9 +133,43 @@ def bench_jacobi(dev, n=16384):
         del u, un
 
 
+def bench_lab5(dev):
+    """lab5 sort at 2^26 keys: int32 / float32 (LSD radix) and uint8 (counting
+    sort) vs torch.sort on the same data; each timed sort starts from the same
+    unsorted copy (the copy is outside the events), median of 10."""
+    n = 1 << 26
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    srcs = {torch.int32: torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev, generator=g),
+            torch.float32: torch.randn(n, device=dev, generator=g),
+            torch.uint8: torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)}
+    for dt, x0 in srcs.items():
+        x = torch.empty_like(x0)
+
+        def timed(fn):
+            ts = []
+            for it in range(12):
+                x.copy_(x0)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn()
+                e.record()
+                e.synchronize()
+                if it >= 2:
+                    ts.append(s.elapsed_time(e) * 1e3)
+            return float(np.median(ts))
+        us = timed(lambda: ops.sort_(x))
+        ok = bool(torch.equal(x, torch.sort(x0).values))
+        ref = timed(lambda: torch.sort(x))
+        emit(workload="lab5_sort", dtype=str(dt).replace("torch.", ""), n=n, us=round(us, 1),
+             Gkeys_s=round(n / us / 1e3, 1), torch_sort_us=round(ref, 1), vs_torch_sort=round(ref / us, 2),
+             equal_to_torch_sort=ok)
+        del x
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--only", default="lab1,lab2,lab3,jacobi")
+    p.add_argument("--only", default="lab1,lab2,lab3,lab5,jacobi")
     a = p.parse_args()
     dev = torch.device("cuda:0")
     which = a.only.split(",")
@@ -144,6 +179,8 @@ def main():
         bench_lab2(dev)
     if "lab3" in which:
         bench_lab3(dev)
+    if "lab5" in which:
+        bench_lab5(dev)
     if "jacobi" in which:
         bench_jacobi(dev)
 
