@@ -264,7 +264,8 @@ def run(args) -> int:
                 d0.step(handles[0])
             wcyc[0] += 1
         if len(handles) >= 2:
-            warm_step(), warm_step()  # the twin launch is built and warmed before timing
+            for _ in range(2):  # the twin launch is built and warmed before timing
+                warm_step()
             warm = max(parallel.all_gather_floats(timed(warm_step, args.steps), ctx))
             watchdog.beat()
         warm1 = max(parallel.all_gather_floats(timed(d0.step, args.steps), ctx))
