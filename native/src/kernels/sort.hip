@@ -760,12 +760,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // slice clears the words it set, so the tables are zero again after each
     // tile and are cleared only once, here
     __shared__ uint32_t s_tbl[NW * 512];
-    __shared__ uint32_t s_cnt[NW][256];
+    // digit counters: one row per wave (RANK 0 / 1) or per half-wave (RANK 2,
+    // rows padded so a half-wave pair's rows start 32 banks apart)
+    constexpr int NR = RANK == 2 ? 2 * NW : NW, CW = RANK == 2 ? 256 + 32 : 256;
+    __shared__ uint32_t s_cnt[NR][CW];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int crow = RANK == 2 ? 2 * w + (lane >> 5) : w;  // this lane's counter row
     for (int i = t; i < NW * 512; i += TPB) s_tbl[i] = 0;
-    for (int i = t; i < NW * 256; i += TPB) (&s_cnt[0][0])[i] = 0;
+    for (int i = t; i < NR * CW; i += TPB) (&s_cnt[0][0])[i] = 0;
     const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
     const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
     const int t0 = (int)((int64_t)ntiles * xcd / kNumXCDs);
@@ -776,7 +780,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(in), 0, nbytes,
                                                                          0x00020000);
     const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, nbytes, 0x00020000);
-    const int vlane = (w * kRWaveKeys + lane) * 4;
+    // RANK 2: each half-wave owns a contiguous half of its wave's keys (slice
+    // e of lane l is key 512 (l >> 5) + 32 e + (l & 31)), so ranking each half
+    // on its own counter row keeps the order stable; otherwise slice e of lane
+    // l is key 64 e + l
+    constexpr uint32_t kSlice = RANK == 2 ? 32u : 64u;  // keys between a lane's slices
+    const int klane = RANK == 2 ? (lane >> 5) * (kRWaveKeys / 2) + (lane & 31) : lane;
+    const int vlane = (w * kRWaveKeys + klane) * 4;
     // peer-mask table: slot d = two words (lanes 0-31, 32-63) at tbl + 2d.
     // (A split layout — the lanes 0-31 words at tbl[d], the 32-63 words at
     // tbl[256 + d], so a half-wave's OR / clear spreads over 32 banks instead
@@ -801,12 +811,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 // the partial-line digit runs this tile and its XCD neighbours
                 // write (2^26 int32 0.828 -> 0.769 ms; NT output stores instead
                 // lose those merges: 1.28 ms; profiles/lab5_sort.md)
-                dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * 256u), 0, 2);
+                dst[e] = __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(voff + e * kSlice * 4u), 0, 2);
         } else {  // 32-bit indices (n < 2^30) keep the partial path's registers small
-            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + klane);
 #pragma unroll
             for (int e = 0; e < kRPer; ++e) {
-                const uint32_t i = i0 + e * 64u;
+                const uint32_t i = i0 + e * kSlice;
                 dst[e] = i < n32 ? __builtin_amdgcn_raw_buffer_load_b32(rin, (int)(i * 4u), 0, 0) : 0u;
             }
         }
@@ -819,15 +829,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int e = 0; e < kRPer; ++e) key[e] = to_key_t<IN_MODE>(key[e]);
         if (!full) {  // pads rank last (digit 255 in every pass) and are never stored
-            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + lane);
+            const uint32_t i0 = (uint32_t)tile0 + (uint32_t)(w * kRWaveKeys + klane);
 #pragma unroll
             for (int e = 0; e < kRPer; ++e)
-                if (i0 + e * 64u >= n32) key[e] = 0xffffffffu;
+                if (i0 + e * kSlice >= n32) key[e] = 0xffffffffu;
         }
         uint32_t rank[kRPer];
-        if constexpr (RANK == 1) {
+        if constexpr (RANK >= 1) {
 #pragma unroll
-            for (int e = 0; e < kRPer; ++e) rank[e] = atomicAdd(&s_cnt[w][(key[e] >> shift) & 255u], 1u);
+            for (int e = 0; e < kRPer; ++e) rank[e] = atomicAdd(&s_cnt[crow][(key[e] >> shift) & 255u], 1u);
         } else {
 #pragma unroll
             for (int g = 0; g < kRPer; g += 4) {  // 4 slices in flight: bounds the live LDS results
@@ -857,10 +867,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
         lds_barrier();
-        uint32_t cnt = 0, wexcl[NW];
+        uint32_t cnt = 0, wexcl[NR];
         if (t < 256) {
 #pragma unroll
-            for (int ww = 0; ww < NW; ++ww) {
+            for (int ww = 0; ww < NR; ++ww) {
                 wexcl[ww] = cnt;
                 cnt += s_cnt[ww][t];
             }
@@ -868,7 +878,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t dstart = scan256_excl_dpp(cnt, s_wsum);
         if (t < 256) {
 #pragma unroll
-            for (int ww = 0; ww < NW; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
+            for (int ww = 0; ww < NR; ++ww) s_cnt[ww][t] = dstart + wexcl[ww];
             s_gbase[t] = excl + dbase - dstart;
         }
         lds_barrier();
@@ -876,14 +886,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int e = 0; e < kRPer; ++e) {
             const uint32_t rk = rank[e];
             if constexpr (KNOCK & 1)
-                s_keys[w * kRWaveKeys + e * 64 + lane] = key[e] + (s_cnt[w][0] + rk == ~0u);  // keeps rank live
+                s_keys[w * kRWaveKeys + e * 64 + lane] = key[e] + (s_cnt[crow][0] + rk == ~0u);  // keeps rank live
             else
-                s_keys[s_cnt[w][(key[e] >> shift) & 255u] + rk] = key[e];
+                s_keys[s_cnt[crow][(key[e] >> shift) & 255u] + rk] = key[e];
         }
         lds_barrier();
-        // this wave's staging reads of its own row are done (program order)
+        // this wave's staging reads of its own row(s) are done (program order)
 #pragma unroll
-        for (int i = lane; i < 256; i += 64) s_cnt[w][i] = 0;
+        for (int i = lane; i < 256; i += 64) {
+            if constexpr (RANK == 2) {
+                s_cnt[2 * w][i] = 0;
+                s_cnt[2 * w + 1][i] = 0;
+            } else {
+                s_cnt[w][i] = 0;
+            }
+        }
         if (full) {
 #pragma unroll
             for (int j = 0; j < TILE / TPB; ++j) {
@@ -1305,7 +1322,9 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // LDS adds (RANK 1), 10 = 9 on 4096-key tiles, 11 = 9 with 3 blocks per CU,
 // 12 / 13 = 9 / 10 with two tiles of keys in flight (PF 2), 14 = the lean
 // onesweep (one histogram read, then decoupled look-back per digit pass):
-// correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md). Retired after round-3
+// correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md); 15 / 16 its
+// one-block-per-CU and static-order experiments; 17 = 12 with one counter row
+// per half-wave (RANK 2: skewed digits contend half as much). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1351,7 +1370,8 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
-    if (variant == 1 || variant >= 14) {
+    const bool onesweep = variant >= 14 && variant <= 16;
+    if (variant == 1 || onesweep) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
         if (variant != 1)
             hipLaunchKernelGGL(radix_hist4_kernel,
@@ -1371,7 +1391,7 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
         const uint32_t *src = (p & 1) ? r.tmp : x;
         uint32_t *dst = (p & 1) ? x : r.tmp;
         const int in_mode = p == 0 ? mode : (int)kRawKeys, out_mode = p == 3 ? mode : (int)kRawKeys;
-        if (variant >= 14) {
+        if (onesweep) {
             // 15: one block per CU — half the tiles in flight, so half the
             // predecessors a look-back walks before it meets an inclusive prefix;
             // 16: static tile order (no counter), all blocks co-resident
@@ -1433,6 +1453,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                                  r.status, ntiles);
                 else if (variant == 12)  // 9 with two tiles of keys in flight
                     launch_lean<kRThreads, 1, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
+                                                    r.status, ntiles);
+                else if (variant == 17)  // 12 with a counter row per half-wave (skewed digits contend half as much)
+                    launch_lean<kRThreads, 2, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
                                                     r.status, ntiles);
                 else if (variant == 13)  // 10 with two tiles of keys in flight
                     launch_lean<kRThreads / 2, 1, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
@@ -1634,8 +1657,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 16 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 16", variant);
+    if (variant < 0 || variant > 17 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 17", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);
