@@ -26,6 +26,9 @@ methodology) as ``value_warm_cache_1stream``.
 
 ``value`` is the whole-job pixel throughput (N * 4096^2 * K / time, max time
 over ranks).
+``host_enqueue_ms_per_step`` (rank 0) is the host time to enqueue the timed
+steps, beside the step time: it shows the GPU, not the host, sets the rate.
+``config.host_wait`` names the host wait policy (``MPX_HIP_WAIT``).
 
 ``value_streaming`` (``--stream``, on by default) times the same K steps with
 an input that changes every step: the filter is iterated (step k convolves
