@@ -75,6 +75,9 @@ def test_bench_measurement_hygiene_fields_cpu():
     assert abs(rec["value_sustained"] - 64 * 64 / (rec["ms_per_step_sustained"] * 1e-3) / 1e9) \
         < 1e-3 * max(1.0, rec["value_sustained"])
     assert rec["cpu_runs"] >= 5 and 0 < rec["cpu_ms_per_image_min"] <= rec["cpu_ms_per_image"]
+    # the host's enqueue time of the timed steps rides along, never above the step time
+    assert 0 < rec["host_enqueue_ms_per_step"] <= rec["ms_per_step"]
+    assert rec["config"]["host_wait"] is None  # CPU: no HIP wait policy
     assert abs(rec["speedup_vs_cpu"] - rec["cpu_ms_per_image"] / rec["gpu_ms_per_image"]) \
         < 0.051 + 1e-3 * rec["speedup_vs_cpu"]
     if os.path.exists(os.path.join(ROOT, "labs", "lab2", "src", "cpu_exe")):
