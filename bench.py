@@ -24,8 +24,10 @@ resident input (cache-assisted; the second stream writes a twin output) are
 reported as ``value_warm_cache``, and on one stream and one pair (the round-1
 methodology) as ``value_warm_cache_1stream``.
 
-``value`` is the whole-job pixel throughput (N * 4096^2 * K / time, max time
-over ranks).
+``value`` is the whole-job pixel throughput N * 4096^2 * K / job span, where
+the job span is max(t_end) - min(t_start) over the ranks on the node's shared
+CLOCK_MONOTONIC (parallel/timing.py): start skew between ranks is charged.
+``max_rank_span_ms`` (the slowest rank's own span) and the skews ride along.
 ``host_enqueue_ms_per_step`` (rank 0) is the host time to enqueue the timed
 steps, beside the step time: it shows the GPU, not the host, sets the rate.
 ``config.host_wait`` names the host wait policy (``MPX_HIP_WAIT``).
@@ -111,6 +113,10 @@ def parse_args(argv=None):
                         "in-order and peer halo modes)")
     p.add_argument("--watchdog", type=float, default=None,
                    help="abort (exit 75) when no step completes for this many seconds; default 300 s for N > 1")
+    p.add_argument("--clocks", type=float, default=0.0,
+                   help="sample the board's clocks / power / temperature at this rate (Hz) on every rank's GPU and "
+                        "report their medians per timed phase under clocks (utils/clocks.py; 0 = off: the sampler "
+                        "thread shares the host with the enqueue loop)")
     p.add_argument("--no-warm", action="store_true", help="skip the cache-resident (single pair) comparison run")
     p.add_argument("--stream", dest="stream", action="store_true", default=True,
                    help="also time the streaming (iterated-filter) run: value_streaming (default on)")
@@ -138,11 +144,18 @@ def run(args) -> int:
     from cuda_mpi_openmp_amd import ops, parallel
     from cuda_mpi_openmp_amd.models.edge import SlabEdgeDetector
     from cuda_mpi_openmp_amd.parallel import launch
+    from cuda_mpi_openmp_amd.parallel.timing import clock_ns, gather_span, start_delay
     from cuda_mpi_openmp_amd.utils.streams import wait_policy_in_force
 
     ctx = parallel.init(device=args.device)
     launch.check_world(args.gpus, ctx.world)
     n = ctx.world
+    sampler = None
+    phases = {}  # phase name -> this rank's (t0, t1) on CLOCK_MONOTONIC
+    if args.clocks > 0 and ctx.device.type == "cuda":
+        from cuda_mpi_openmp_amd.utils.clocks import ClockSampler
+
+        sampler = ClockSampler(hz=args.clocks, bdf=device_id(ctx.device)).start()
 
     def sync():
         if ctx.device.type == "cuda":
@@ -206,15 +219,17 @@ def run(args) -> int:
 
     issue_s = {}  # step function -> host enqueue time of its last timed run
 
-    def timed(step_fn, k: int) -> float:
+    def timed(step_fn, k: int):
         """Exactly k steps bracketed by barrier + device sync on both sides.
-        Each rank's clock stops at its own closing device sync, before the
-        closing barrier: the barrier (an RCCL all-reduce plus a device sync at
-        N > 1) is bracket, not step, and the max over ranks taken by the
-        caller still charges the slowest rank's steps in full."""
+        Every rank reads the node's shared CLOCK_MONOTONIC when it leaves the
+        opening barrier + sync (t0) and at its own closing device sync (t1);
+        the returned Span (parallel/timing.py) gives the job's time
+        max(t1) - min(t0), which charges start skew between ranks, and the
+        slowest rank's own span beside it (VERDICT r4 Next #1)."""
         ctx.barrier()
         sync()
-        t0 = time.perf_counter()
+        start_delay(ctx.rank)  # MPX_BENCH_START_DELAY test hook (no-op unless set)
+        t0 = clock_ns()
         done = 0
         if graph is not None and step_fn is rot_step:  # every replay runs args.graph complete steps
             while done + args.graph <= k:
@@ -224,21 +239,22 @@ def run(args) -> int:
             step_fn()
         for d in dets:
             d.finish()
-        issued = time.perf_counter() - t0  # host time to enqueue the k steps
+        issued = (clock_ns() - t0) / 1e9  # host time to enqueue the k steps
         sync()
-        dt = time.perf_counter() - t0
+        t1 = clock_ns()
         ctx.barrier()
         issue_s[step_fn] = issued
-        return dt
+        phases[timed.phase] = (t0, t1)
+        return gather_span(t0, t1, ctx)
 
     # ---- timed region: exactly `steps` steps over the rotated pairs ----
     timed.issue_s = issue_s
+    timed.phase = "timed"
     cyc[0] = 0
-    mine = timed(rot_step, args.steps)
+    span = timed(rot_step, args.steps)
     enqueue_ms = issue_s[rot_step] * 1e3 / max(1, args.steps)
     watchdog.beat()
-    per_rank = parallel.all_gather_floats(mine, ctx)
-    elapsed = max(per_rank)
+    elapsed = span.job_s  # the job's time: first rank's start to last rank's end
 
     # the same K steps after >= sustain_ms of continuous load (the clock the
     # board holds under sustained load): reported beside `value`, not instead
@@ -246,7 +262,8 @@ def run(args) -> int:
     if args.sustain_ms > 0 and graph is None:
         settle(rot_step, len(dets), args.sustain_ms, ctx, sync, watchdog, parallel, lambda: [d.finish() for d in dets])
         cyc[0] = 0
-        sustained = max(parallel.all_gather_floats(timed(rot_step, args.steps), ctx))
+        timed.phase = "sustained"
+        sustained = timed(rot_step, args.steps).job_s
         watchdog.beat()
 
     warm = warm1 = None
@@ -269,9 +286,11 @@ def run(args) -> int:
         if len(handles) >= 2:
             for _ in range(2):  # the twin launch is built and warmed before timing
                 warm_step()
-            warm = max(parallel.all_gather_floats(timed(warm_step, args.steps), ctx))
+            timed.phase = "warm_cache"
+            warm = timed(warm_step, args.steps).job_s
             watchdog.beat()
-        warm1 = max(parallel.all_gather_floats(timed(d0.step, args.steps), ctx))
+        timed.phase = "warm_cache_1stream"
+        warm1 = timed(d0.step, args.steps).job_s
         d0.cache_resident(False)
         watchdog.beat()
         if warm is None:
@@ -294,10 +313,21 @@ def run(args) -> int:
     stream_rec = None
     if args.stream:
         graph = None
+        timed.phase = "streaming"
         stream_rec = run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel)
         ok &= stream_rec.get("verified_bit_exact", True) is not False
 
     watchdog.stop()
+    clocks = None
+    if sampler is not None:
+        from cuda_mpi_openmp_amd.utils.clocks import key_fields
+
+        sampler.stop()
+        # a K-step phase lasts well under one sample period: widen each window by
+        # 3 ms on both sides so it holds the samples around it
+        mine_clk = {ph: key_fields(sampler.summary(a, b, pad_ns=3_000_000)) for ph, (a, b) in phases.items()}
+        mine_clk["sampler"] = {"source": sampler.source, "error": sampler.error, "hz": sampler.rate_hz()}
+        clocks = parallel.all_gather_object(mine_clk, ctx)
     cpu_ms = None
     if ctx.rank == 0 and not args.no_cpu_baseline:
         cpu_ms = cpu_baseline_ms(d0, args.size, ops)
@@ -358,11 +388,13 @@ def run(args) -> int:
             "rank_devices": rank_devices,
             "distinct_devices": len(set(rank_devices)),
             "rehearsal": rehearsal,
-            "per_rank_ms_per_step": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
+            **span.fields(args.steps),
             "verified_bit_exact": ok and (args.no_verify or checked == n * len(dets) * args.size * args.size),
             "verified_pixels": checked,
             "device": str(torch.cuda.get_device_name(ctx.device)) if ctx.device.type == "cuda" else "cpu",
         }
+        if clocks is not None:
+            rec["clocks"] = clocks  # one entry per rank
         if sustained is not None:
             rec["value_sustained"] = _sig(pixels / sustained / 1e9)
             rec["ms_per_step_sustained"] = round(sustained * 1e3 / max(1, args.steps), 5)
@@ -447,11 +479,10 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     ctx.barrier()
     settle(step, len(sdets), args.warmup_ms, ctx, sync, watchdog, parallel, lambda: None)
     cyc[0] = 0
-    mine = timed(step, args.steps)
+    span = timed(step, args.steps)
     enqueue_ms = timed.issue_s[step] * 1e3 / max(1, args.steps)
     watchdog.beat()
-    per_rank = parallel.all_gather_floats(mine, ctx)
-    elapsed = max(per_rank)
+    elapsed = span.job_s
     # a device-side halo wait that gave up on ANY rank fails every rank here,
     # before the gathers below (a rank raising alone would leave the others
     # blocked in them until the watchdog fires: ADVICE r3)
@@ -463,7 +494,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
            "streams_streaming": ns,
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
            "host_enqueue_ms_per_step_streaming": round(enqueue_ms, 5),
-           "per_rank_ms_per_step_streaming": [round(t * 1e3 / max(1, args.steps), 5) for t in per_rank],
+           **span.fields(args.steps, "_streaming"),
            "transport_streaming": sdets[0].transport if n > 1 else None}
     if not args.no_verify:
         ok, checked = True, 0

@@ -185,8 +185,15 @@ class SlabJacobi:
         corrupt = _fault_hook(self.ctx.rank, self.iteration)
         if not self._halos_valid:
             self.sync_halos()
-        if corrupt:  # injected silent error: one value off by one (peer mode: this
-            # rank's first owned row, the one its upper neighbour's halo comes from)
+        if corrupt:  # injected silent error: one value off by one.
+            # Host-exchanged halos (RCCL / gloo): the received halo row itself — a
+            # cross-rank halo error. Peer mailboxes: the neighbour reads
+            # this rank's edge row from the mailbox slot the previous sweep wrote,
+            # which the host cannot change without racing that read, so the error
+            # goes into this rank's first owned row instead: it is wrong here at
+            # once and reaches the upper neighbour one sweep later, through the
+            # mailbox row this sweep writes (the update spreads it to the adjacent
+            # columns). Either way the N-rank == one-device check must fail.
             row = 1 if self.peer is not None else 0 if self.slab.has_up else self.slab.rows + 1
             self.u[row, self.cols // 2] += 1.0
         track = (self.iteration + 1) % self.check_every == 0

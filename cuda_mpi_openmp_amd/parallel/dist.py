@@ -54,6 +54,33 @@ class DistContext:
 
 _CTX: Optional[DistContext] = None
 
+VISIBILITY_VARS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def select_device(local_rank: int, local_world: Optional[int], ndev: int, env=None) -> Optional[int]:
+    """The device index this rank drives, or None when node-local ranks would
+    silently share GPUs (decide on node-local values, never on the
+    global WORLD_SIZE, so multi-node jobs pass).
+
+    * local_world <= ndev (or unknown and local_rank < ndev): device local_rank;
+    * the launcher isolated devices per rank (a visibility variable set and
+      fewer devices than node-local ranks, e.g. HIP_VISIBLE_DEVICES=<rank>):
+      every rank sees its own GPU(s) from index 0 — device local_rank % ndev
+      (0 for one GPU per rank). Ranks that were all handed the SAME GPU are
+      still caught later: RCCL refuses duplicate devices and bench.py checks
+      distinct PCI ids;
+    * otherwise (not isolated, more node-local ranks than devices): None.
+    """
+    env = os.environ if env is None else env
+    if ndev <= 0:
+        return None
+    lw = local_world if local_world is not None else local_rank + 1
+    if lw <= ndev:
+        return local_rank
+    if any(env.get(v, "").strip() for v in VISIBILITY_VARS):
+        return local_rank % ndev
+    return None
+
 
 def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float = 300.0) -> DistContext:
     """Initialise (once) from the torchrun environment.
@@ -75,18 +102,21 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
         ndev = torch.cuda.device_count()
         if ndev == 0:
             raise RuntimeError("device='cuda' requested but no GPU is visible")
-        if world > ndev and not rehearsal:
-            # ranks would silently share devices (local_rank % ndev): refuse, as
-            # the launcher does before spawning (sysfs may list GPUs
-            # this container cannot open)
-            import sys
+        lw_env = os.environ.get("LOCAL_WORLD_SIZE")
+        idx = select_device(local_rank, int(lw_env) if lw_env else None, ndev)
+        if idx is None:
+            if not rehearsal:
+                # node-local ranks would silently share devices: refuse, as the
+                # launcher does before spawning
+                import sys
 
-            print(f"[dist] WORLD_SIZE={world} but only {ndev} GPU(s) are usable in this process; refusing to put "
-                  f"several ranks on one device (MPX_DIST_CONTRACT=nccl or MPX_DIST_BACKEND=gloo rehearse that)",
-                  file=sys.stderr)
-            raise SystemExit(2)
-        torch.cuda.set_device(local_rank % ndev)
-        dev = torch.device("cuda", local_rank % ndev)
+                print(f"[dist] {lw_env or local_rank + 1} ranks on this node (LOCAL_RANK={local_rank}) but only "
+                      f"{ndev} GPU(s) are usable in this process; refusing to put several ranks on one device "
+                      f"(MPX_DIST_CONTRACT=nccl or MPX_DIST_BACKEND=gloo rehearse that)", file=sys.stderr)
+                raise SystemExit(2)
+            idx = local_rank % ndev
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
         # the compute stream pair before any communicator creates its streams:
         # they get hardware queues of their own (utils/streams.py)
         from ..utils.streams import compute_streams, host_wait_policy

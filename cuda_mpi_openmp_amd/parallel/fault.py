@@ -14,8 +14,12 @@ reference has no timeouts at all (its harness waits on subprocess.run). Here:
 * ``MPX_FAULT_INJECT="rank:iteration"`` (models/jacobi.py) raises
   :class:`FaultInjected` on one rank, which the tests use to check the path;
   ``MPX_FAULT_INJECT="halo:rank:iteration"`` instead corrupts that rank's
-  received halo row before that iteration's sweep (silently wrong data), which
-  the N-rank == one-device verification must catch.
+  received halo row before that iteration's sweep (silently wrong data; with
+  peer mailboxes its first owned row, which reaches the neighbour one sweep
+  later — models/jacobi.py), which the N-rank == one-device verification must
+  catch.
+* ``MPX_BENCH_START_DELAY="rank:ms"`` (parallel/timing.py) delays one rank's
+  start of a timed region: the job-span accounting must charge it.
 """
 
 from __future__ import annotations

@@ -1179,10 +1179,13 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
                 band4_walk<K, A, MODE, FAST, F, false, OPT, true>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW,
                                                                   taps, rs, mbf, mbl, sp.n_first, sp.n_last);
             // every write-through store of this wave acknowledged, then count the
-            // wave; the last edge wave of the step publishes c + 1 (release)
+            // wave; the last edge wave of the step publishes c + 1 (release). The
+            // count is acq_rel at system scope: each wave's increment
+            // releases its own mailbox rows and the last wave acquires them all
+            // before its publish, whatever memory kind the mailbox fell back to
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if ((threadIdx.x & 63) == 0) {
-                const uint32_t n = __hip_atomic_fetch_add(sp.sync + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t n = __hip_atomic_fetch_add(sp.sync + 32, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (n + 1 == (uint32_t)sp.n_edge) {
                     __hip_atomic_store(sp.sync + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     peer::publish(sp.sync, c + 1);

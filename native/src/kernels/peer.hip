@@ -145,9 +145,13 @@ __global__ __launch_bounds__(256) void halo_fetch_kernel(mpx_halo_fetch f) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores acknowledged
     __syncthreads();
-    // (2) the later of the two blocks publishes the step (release)
+    // (2) the later of the two blocks publishes the step (release). The count is
+    // acq_rel at system scope: each block's increment releases its
+    // own mailbox stores, and the last block's acquire of the count makes the
+    // other block's stores part of what its publish releases — whatever memory
+    // kind the mailbox fell back to
     if (threadIdx.x == 0) {
-        const uint32_t c = __hip_atomic_fetch_add(f.sync + kSyncCtr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t c = __hip_atomic_fetch_add(f.sync + kSyncCtr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
         if (c == 1u) {
             __hip_atomic_store(f.sync + kSyncCtr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             peer::publish(f.sync + kSyncStep, f.step);

@@ -19,14 +19,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(args, nproc=None, rc=0):
+def _run(args, nproc=None, rc=0, env=None):
     cmd = [sys.executable]
     if nproc:
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr",
                 "127.0.0.1", "--master-port", str(_port())]
     cmd += [os.path.join(ROOT, "bench.py"), *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
-                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+                       env=dict(os.environ, OMP_NUM_THREADS="1", **(env or {})))
     if rc:  # torchrun reports a failed rank as 1 whatever the rank's own code
         assert r.returncode != 0, r.stdout[-2000:]
         return r
@@ -132,3 +132,61 @@ def test_bench_self_launches_ranks_cpu():
 def test_bench_refuses_world_mismatch_cpu():
     r = _run(["--gpus", "3", "--device", "cpu", "--size", "64", "--steps", "1", "--warmup", "0"], nproc=2, rc=2)
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def _torchrun(script, args, nproc, env):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, script), *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, OMP_NUM_THREADS="1", **env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_job_span_charges_injected_start_skew():
+    """VERDICT r4 Next #1: rates come from the job span max(t1) - min(t0) on the
+    node's shared clock. A 300 ms start delay injected on rank 1 of an
+    independent-steps job (lab1 vsub: no inter-rank traffic in the timed
+    region) lands in job_span_ms and lowers value; the slowest rank's own span
+    (the round-4 figure) does not see it."""
+    args = ["--workload", "vsub", "--device", "cpu", "--elems", "4096", "--steps", "3", "--warmup", "1"]
+    base = _torchrun("tools/bench_workloads.py", args, 2, {})
+    rec = _torchrun("tools/bench_workloads.py", args, 2, {"MPX_BENCH_START_DELAY": "1:300"})
+    for r in (base, rec):
+        assert r["verified"] is True and r["job_span_ms"] >= r["max_rank_span_ms"] > 0
+        assert len(r["per_rank_ms_per_step"]) == 2
+        # value and ms_per_step come from the job span
+        assert abs(r["ms_per_step"] * r["steps"] - r["job_span_ms"]) <= 1e-3 * r["job_span_ms"] + 1e-4
+    assert rec["job_span_ms"] >= 300.0 and rec["start_skew_ms"] >= 295.0
+    assert rec["max_rank_span_ms"] < 150.0  # no rank's own span holds the delay
+    assert rec["value"] < base["value"] * (base["job_span_ms"] / 300.0)
+
+
+def test_bench_value_is_job_span_with_start_skew():
+    """bench.py: with a 200 ms start delay on rank 1 the job span holds the
+    delay and value = N * size^2 * K / job span (the slowest-rank figure and
+    the skews ride along)."""
+    rec = _run(["--gpus", "2", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2",
+                "--no-stream", "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"], nproc=2,
+               env={"MPX_BENCH_START_DELAY": "1:200"})
+    assert rec["job_span_ms"] >= 200.0 and rec["start_skew_ms"] >= 195.0
+    assert rec["job_span_ms"] >= rec["max_rank_span_ms"]
+    assert abs(rec["ms_per_step"] * 2 - rec["job_span_ms"]) <= 1e-3 * rec["job_span_ms"] + 1e-4
+    assert abs(rec["value"] - 2 * 64 * 64 * 2 / (rec["job_span_ms"] * 1e-3) / 1e9) < 1e-3 * max(1e-3, rec["value"])
+
+
+def test_scale_driver_job_is_the_driver_command():
+    """SCALE N = 1 equals BENCH: tools/scale.py's conv/driver job runs exactly
+    the driver's bench.py --gpus N --steps K --warmup W."""
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("scale", os.path.join(ROOT, "tools", "scale.py"))
+    scale = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(scale)
+    a = argparse.Namespace(device="auto", rehearse=False, contract=False, quick=False, driver_steps=20,
+                           driver_warmup=5)
+    for n in (1, 2, 8):
+        job = [j for j in scale.plan(n, a, 8) if j["name"] == "conv/driver"][0]
+        assert job["cmd"][1:] == ["bench.py", "--gpus", str(n), "--steps", "20", "--warmup", "5"]
+        assert job["skip"] is None

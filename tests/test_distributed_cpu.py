@@ -271,3 +271,22 @@ def test_fault_injection_raises(monkeypatch):
     with pytest.raises(FaultInjected):
         sol.run(10)
     assert sol.iteration == 3
+
+
+def test_select_device_uses_node_local_values():
+    """the same-device refusal is decided on node-local values
+    (LOCAL_WORLD_SIZE, LOCAL_RANK), never on the global WORLD_SIZE."""
+    from cuda_mpi_openmp_amd.parallel.dist import select_device
+
+    # one node of 8 GPUs, 8 ranks: rank k drives GPU k
+    assert [select_device(r, 8, 8, env={}) for r in range(8)] == list(range(8))
+    # a multi-node job (WORLD_SIZE 16, 8 ranks per node): node-local values pass
+    assert select_device(7, 8, 8, env={}) == 7
+    # per-rank isolation (HIP_VISIBLE_DEVICES=<rank>): one visible GPU, index 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        assert [select_device(r, 8, 1, env={var: str(r)}) for r in range(8)] == [0] * 8
+    # not isolated, more node-local ranks than devices: refused (None)
+    assert select_device(1, 2, 1, env={}) is None
+    assert select_device(3, None, 2, env={}) is None
+    assert select_device(0, None, 1, env={}) == 0
+    assert select_device(0, 1, 0, env={}) is None

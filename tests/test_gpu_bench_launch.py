@@ -36,4 +36,4 @@ def test_bench_workloads_two_ranks(gpu, workload, extra):
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
-    assert rec["n_gpus"] == 2 and rec["verified"] is True and len(rec["per_rank_ms"]) == 2
+    assert rec["n_gpus"] == 2 and rec["verified"] is True and len(rec["per_rank_ms_per_step"]) == 2 and rec["job_span_ms"] >= rec["max_rank_span_ms"]

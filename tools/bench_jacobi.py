@@ -26,6 +26,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cuda_mpi_openmp_amd.parallel.timing import clock_ns, gather_span, start_delay  # noqa: E402
 from cuda_mpi_openmp_amd import parallel  # noqa: E402
 from cuda_mpi_openmp_amd.models import SlabJacobi  # noqa: E402
 
@@ -80,14 +81,15 @@ def main() -> int:
         sol.run(a.warmup, graph=a.graph)
     sync()
     ctx.barrier()
-    t0 = time.perf_counter()
+    start_delay(ctx.rank)  # MPX_BENCH_START_DELAY test hook
+    t0 = clock_ns()
     sol.run(a.iters, graph=a.graph)
     sync()
-    mine = time.perf_counter() - t0  # the clock stops at this rank's sync (bench.py timed())
+    t1 = clock_ns()  # this rank's end; the job span is max(t1) - min(t0) (bench.py timed())
     ctx.barrier()
     sol.check_peer()
-    el = parallel.max_over_ranks(mine, ctx)
-    per_rank = parallel.all_gather_floats(mine, ctx)  # collective: every rank
+    span = gather_span(t0, t1, ctx)  # collective: every rank
+    el = span.job_s
     verified = None
     if ctx.world > 1 and not a.no_verify and a.halo != "none":  # the ablation is wrong by design
         got = sol.gather()
@@ -108,7 +110,7 @@ def main() -> int:
             "transport": sol.transport,
             "halo": ("one-launch" if sol.peer is not None else "overlap" if sol.overlap else "inorder")
             if ctx.world > 1 else None,
-            "per_rank_ms": [round(t * 1e3 / a.iters, 5) for t in per_rank],
+            **span.fields(a.iters),
             "hip_graph": bool(a.graph and ctx.device.type == "cuda"),
             "peer_probe": ("ok" if sol.peer is not None else "fallback")
             if ctx.world > 1 and a.halo in ("auto", "peer") and ctx.device.type == "cuda" else None,

@@ -13,18 +13,19 @@ bench.py, the Jacobi stencil tools/bench_jacobi.py).
   every rank holds the reference's fp64 statistics; a 64-row band of every
   rank's classes is compared with the OpenMP CPU reference.
 
-Prints one JSON line on rank 0 (whole-job throughput, max time over ranks).
+Prints one JSON line on rank 0 (whole-job throughput over the job span
+max(t_end) - min(t_start) on the node's shared monotonic clock).
 """
 import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cuda_mpi_openmp_amd import ops, parallel  # noqa: E402
+from cuda_mpi_openmp_amd.parallel.timing import clock_ns, gather_span, start_delay  # noqa: E402
 from cuda_mpi_openmp_amd.models import ShardedVectorSub, SlabPixelClassifier  # noqa: E402
 from cuda_mpi_openmp_amd.models.classifier import class_points_for  # noqa: E402
 
@@ -70,14 +71,15 @@ def main() -> int:
         step()
     sync()
     ctx.barrier()
-    t0 = time.perf_counter()
+    start_delay(ctx.rank)  # MPX_BENCH_START_DELAY test hook
+    t0 = clock_ns()
     for _ in range(a.steps):
         step()
     sync()
-    mine = time.perf_counter() - t0  # the clock stops at this rank's sync (bench.py timed())
+    t1 = clock_ns()  # this rank's end; the job span is max(t1) - min(t0) (bench.py timed())
     ctx.barrier()
-    per_rank = parallel.all_gather_floats(mine, ctx)
-    el = max(per_rank)
+    span = gather_span(t0, t1, ctx)
+    el = span.job_s
 
     if a.workload == "vsub":
         ok = bool(torch.equal(m.c, m.a - m.b))
@@ -94,7 +96,7 @@ def main() -> int:
     if ctx.rank == 0:
         print(json.dumps({"workload": a.workload, "n_gpus": n_ranks, "steps": a.steps, "warmup": a.warmup,
                           "value": float(f"{value:.6g}"), "unit": unit, "ms_per_step": round(el * 1e3 / a.steps, 5),
-                          "per_rank_ms": [round(t * 1e3 / a.steps, 5) for t in per_rank], "scaling": "weak",
+                          **span.fields(a.steps), "scaling": "weak",
                           "verified": ok, **extra}), flush=True)
     parallel.shutdown()
     return 0 if ok else 1

@@ -13,7 +13,8 @@
 #   O=...             bash tools/gpu.sh mgpu [ARGS...]              # native runtime: N-rank == one-device
 #   O=...             bash tools/gpu.sh jpeer [N...]                # device-signalled Jacobi: peer vs no-exchange
 #   O=...             bash tools/gpu.sh run NAME SECONDS CMD...     # any command, logged, time-bounded
-#   O=...             bash tools/gpu.sh checkpoint                  # tests + smoke + bench
+#   O=...             bash tools/gpu.sh checkpoint [NAME]           # tests + smoke + bench, or ckpt_NAME
+#                                                                   # of tools/checkpoints/*.sh
 #
 # Counter groups respect the per-block limits (<= 8 SQ, 4 TCC, 2 GRBM per pass);
 # FETCH_SIZE / WRITE_SIZE get passes of their own. tools/pmc_median.py merges
@@ -95,7 +96,16 @@ case "$cmd" in
     timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1 || fail "$name" $? "$O/$name.log"
     tail -3 "$O/$name.log" ;;
   checkpoint)
-    bash "$0" tests && bash "$0" smoke && bash "$0" bench ;;
+    # no name: tests + smoke + bench; NAME: the function ckpt_NAME of the
+    # checkpoint table (tools/checkpoints/*.sh: r5.sh this round, r4_archive.sh)
+    if [ $# -eq 0 ]; then
+      bash "$0" tests && bash "$0" smoke && bash "$0" bench
+    else
+      here=$(dirname "$0")
+      for f in "$here"/checkpoints/*.sh; do . "$f"; done
+      declare -F "ckpt_$1" >/dev/null || { echo "[gpu.sh] no checkpoint $1"; exit 2; }
+      "ckpt_$1"
+    fi ;;
   *)
     sed -n 2,21p "$0"; exit 2 ;;
 esac

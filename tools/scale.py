@@ -18,7 +18,10 @@ and writes ``<out>/scaling.json`` (one record per run: N, value, ms/step,
 efficiency vs N = 1, transport, world size the job saw), ``scaling.csv`` and
 ``scaling.png`` (weak-scaling throughput and strong-scaling speedup against
 the ideal lines). Efficiency: weak = value_N / (N * value_1); strong =
-t_1 / (N * t_N). Runs that cannot execute here (fewer devices than N, RCCL
+t_1 / (N * t_N); every rate comes from the job span max(t_end) - min(t_start)
+(parallel/timing.py), and ``efficiency_max_rank`` shows the same ratio on the
+slowest rank's own span. ``conv/driver`` is the round-end driver's exact
+``bench.py --gpus N --steps K --warmup W``, so its N = 1 point equals BENCH. Runs that cannot execute here (fewer devices than N, RCCL
 with several ranks on one GPU) are recorded as skipped with the reason.
 
 ``--rehearse``: several ranks share the GPUs (gloo control plane, peer halos
@@ -90,6 +93,14 @@ def plan(n: int, a, ndev: int) -> List[dict]:
     dev = ["--device", "cpu"] if cpu else []
     jobs = []
     lacks = None if shared or n <= ndev else f"needs {n} GPUs, {ndev} visible"
+    # the driver's own command (BENCH at N = 1, SCALE at every N): bench.py with
+    # exactly --gpus N --steps K --warmup W, so this curve's N = 1 point is the
+    # BENCH number (VERDICT r4 Next #1)
+    drv = [py, "bench.py", "--gpus", str(n), "--steps", str(a.driver_steps), "--warmup", str(a.driver_warmup)]
+    if not cpu:
+        assert drv[1:] == driver_command(n, a.driver_steps, a.driver_warmup), drv
+    jobs.append({"name": "conv/driver", "kind": "weak", "skip": lacks,
+                 "cmd": drv + (dev + ["--size", "128", "--rotate", "2"] if cpu else [])})
     for halo in ("peer", "rccl"):
         skip = lacks
         if n > 1 and halo == "rccl" and a.rehearse and not cpu and not a.contract:
@@ -125,6 +136,11 @@ def plan(n: int, a, ndev: int) -> List[dict]:
                      "cmd": [mg, "jacobi", "--halo", "peer", *(["--shared"] if sh else []), "--gpus", str(n),
                              "--iters", steps[1], "--warmup", steps[3]]})
     return jobs
+
+
+def driver_command(n: int, steps: int, warmup: int) -> List[str]:
+    """The round-end driver's bench invocation (task contract), argv after the interpreter."""
+    return ["bench.py", "--gpus", str(n), "--steps", str(steps), "--warmup", str(warmup)]
 
 
 def value_of(rec: dict) -> Optional[float]:
@@ -166,6 +182,9 @@ def efficiencies(rows: List[dict], rehearse: bool = False) -> None:
             continue
         if r["kind"] == "weak" and r.get("value") is not None and b.get("value"):
             r["efficiency"] = round(r["value"] / (r["n"] * b["value"]), 4)
+            if r.get("value_max_rank") and b.get("value_max_rank"):
+                # the round-4 accounting (slowest rank's own span): shows what start skew costs
+                r["efficiency_max_rank"] = round(r["value_max_rank"] / (r["n"] * b["value_max_rank"]), 4)
             if rehearse:
                 r["retained"] = round(r["value"] / b["value"], 4)
         elif r["kind"] == "strong" and r.get("ms") is not None and b.get("ms"):
@@ -194,6 +213,8 @@ def main(argv=None) -> int:
     p.add_argument("--quick", action="store_true", help="fewer steps per run")
     p.add_argument("--only", default="", help="run only jobs whose name contains this string")
     p.add_argument("--timeout", type=float, default=600.0, help="seconds per job")
+    p.add_argument("--driver-steps", type=int, default=20, help="K of the driver's bench command (conv/driver)")
+    p.add_argument("--driver-warmup", type=int, default=5, help="W of the driver's bench command (conv/driver)")
     a = p.parse_args(argv)
     ns = [int(x) for x in a.gpus.split(",") if x.strip()]
     out = a.out if os.path.isabs(a.out) else os.path.join(ROOT, a.out)
@@ -230,6 +251,12 @@ def main(argv=None) -> int:
                             rec.get("halo")
                         row["world_size_seen"] = rec.get("world_size_seen")
                         row["verified"] = rec.get("verified_bit_exact", rec.get("verified"))
+                        row["job_span_ms"] = rec.get("job_span_ms")
+                        row["max_rank_span_ms"] = rec.get("max_rank_span_ms")
+                        row["start_skew_ms"] = rec.get("start_skew_ms")
+                        if row["value"] and rec.get("job_span_ms") and rec.get("max_rank_span_ms") \
+                                and row["kind"] == "weak":
+                            row["value_max_rank"] = row["value"] * rec["job_span_ms"] / rec["max_rank_span_ms"]
                     else:
                         row["stderr_tail"] = res.get("stderr_tail")
                 rows.append(row)
@@ -256,8 +283,8 @@ def main(argv=None) -> int:
             "host": os.uname().nodename, "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
     with open(os.path.join(out, "scaling.json"), "w") as f:
         json.dump({"meta": meta, "runs": rows}, f, indent=1)
-    cols = ["name", "kind", "n", "status", "value", "unit", "ms", "efficiency", "speedup", "retained", "transport",
-            "verified", "reason"]
+    cols = ["name", "kind", "n", "status", "value", "unit", "ms", "efficiency", "efficiency_max_rank", "speedup",
+            "retained", "job_span_ms", "max_rank_span_ms", "start_skew_ms", "transport", "verified", "reason"]
     with open(os.path.join(out, "scaling.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=cols, extrasaction="ignore")
         w.writeheader()
