@@ -9,7 +9,9 @@ run_test.py:58-60). Unknown ``--key value`` options go to the lab processor.
 New flags: ``--binary_path_hip`` (alias), ``--timeout`` per run, ``--timing``
 (cold | warm | median:N — exported as MPX_TIMING to the GPU binary), and the
 default ``--metadata_columns2plot`` is ``[]`` (the reference default raised a
-KeyError in the plot).
+KeyError in the plot); ``--compat`` restores the
+reference's output-changing behaviour for a literal replay
+(processors.COMPAT_DEVIATIONS).
 """
 
 from __future__ import annotations
@@ -41,6 +43,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timing", type=str, default=None, help="GPU timing policy: cold | warm | median:N")
     p.add_argument("--warmup", type=int, default=None,
                    help="untimed launches before the timed one(s) in the GPU binary (MPX_WARMUP)")
+    p.add_argument("--compat", action="store_true",
+                   help="literal replay of the reference harness: lab1 array2string stdin and no lab1 check, "
+                        "sidecars next to the inputs, the reference CSV schema (processors.COMPAT_DEVIATIONS)")
     p.add_argument("--n_gpus", type=int, default=1,
                    help="split each run over N GPUs inside the GPU binary (MPX_NGPUS); reported time is the "
                         "slowest device's kernel time")
@@ -71,6 +76,11 @@ def main(argv: Optional[List[str]] = None) -> int:
     print(f"kwargs=<{json.dumps(kwargs, indent=2)}>")
     print(f"metadata_columns2plot=<{json.dumps(meta, indent=2)}>")
     print(f"n_gpus=<{args.n_gpus}>")
+    if args.compat:
+        from .processors import COMPAT_DEVIATIONS
+
+        print("compat=<True>: reference behaviour restored for " + "; ".join(f"#{k}" for k in COMPAT_DEVIATIONS))
+        kwargs["compat"] = True
     if lab_name in ("lab2", "lab3", "lab5") and "dir_to_data" not in kwargs:
         kwargs["lab_dir"] = lab_dir
     env = {}
@@ -97,7 +107,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     env = env or None
     tester = Tester(binary_path_gpu=args.binary_path_cuda, k_times=args.k_times, kernel_sizes=kernel_sizes,
                     metadata_columns2plot=meta, binary_path_cpu=args.binary_path_cpu, return_inp=args.return_inp,
-                    return_task_res=args.return_task_res, timeout=args.timeout, gpu_env=env)
+                    return_task_res=args.return_task_res, timeout=args.timeout, gpu_env=env, compat=args.compat)
     processor = PROCESSORS[lab_name](**kwargs)
     df = tester.run_experiments(processor)
     return 0 if len(df) else 1

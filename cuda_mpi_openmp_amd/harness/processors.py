@@ -13,6 +13,14 @@ with the lab's 1e-10 relative precision (#3); list kwargs work (#5); sidecar
 files go to a cache directory, not the input directory (#8); lab3's
 ``count_classes`` / ``count_pts`` opt into random classes (#12). New:
 ``synthetic="WxH"`` generates a seeded random image as an extra input.
+
+``compat=True`` (``run_test.py --compat``, VERDICT r4 Next #7) switches the
+output-changing fixes back for a literal replay of the reference harness —
+every deviation in one place, :data:`COMPAT_DEVIATIONS`:
+lab1 stdin is ``np.array2string`` text (summarised beyond 1000 elements:
+the binaries then read 3 values and garbage), lab1 verification always
+passes, and the image labs write their ``.data`` / ``.txt`` / ``.png`` sidecars
+next to the inputs, the ground truth and the outputs.
 """
 
 from __future__ import annotations
@@ -40,6 +48,29 @@ DEFAULT_LAB3_CLASSES = [
     np.array([[1, 2], [1, 0], [2, 2], [2, 1]]),
     np.array([[0, 0], [0, 1], [1, 1], [2, 0]]),
 ]
+
+
+# Appendix B items switched back by compat=True (processors) and by the
+# Tester's compat mode (CSV schema / file names). Everything else — the
+# kwargs fix (#1), list kwargs (#5), PNG conversion (#9), the native
+# programs' fixes (#10, #11, #16) — cannot change a result the reference
+# could produce, so it stays on.
+COMPAT_DEVIATIONS = {
+    2: "lab1 stdin: np.array2string(separator=' ', max_line_width=inf, precision=precision_array)[1:-1] "
+       "(lab1_processor.py:37-48), summarised with '...' beyond 1000 elements — the reference programs then "
+       "read 3 values and garbage, ours refuse the short input (checked I/O, #11 stays fixed), so such runs "
+       "are recorded as failed instead of passing on garbage",
+    3: "lab1 verification always True (lab1_processor.py:60-67)",
+    6: "the CPU binary's CSV is stats_<bin>.csv even when it shares the GPU binary's name (tester.py:267-269)",
+    8: "sidecar .data/.txt/.png written next to every input, ground truth and output (utils/converter.py:32-53)",
+    "csv": "CSV columns exactly the reference's: no device / wall_ms / n_gpus / throughput / pixels columns and "
+           "no speedup_<bin>.csv (tester.py:224-285)",
+}
+
+
+def compat_vector_text(v: np.ndarray, precision: int) -> str:
+    """The reference's lab1 vector text (lab1_processor.py:37-48)."""
+    return np.array2string(v, separator=" ", max_line_width=np.inf, precision=precision)[1:-1].strip()
 
 
 class LabProcessor:
@@ -70,8 +101,10 @@ def fmt_vector(v: np.ndarray) -> str:
 
 class Lab1Processor(LabProcessor):
     def __init__(self, seed: int = 42, min_vector_size: int = 1024, max_vector_size: int = 3072, atol: float = 1e-10,
-                 precision_array: int = 10, rtol: float = 1e-10, lo: float = -1e100, hi: float = 1e100, **_):
+                 precision_array: int = 10, rtol: float = 1e-10, lo: float = -1e100, hi: float = 1e100,
+                 compat: bool = False, **_):
         super().__init__(seed)
+        self.compat = bool(compat)
         self.min_vector_size, self.max_vector_size = int(min_vector_size), int(max_vector_size)
         self.atol, self.rtol, self.precision_array = atol, rtol, precision_array
         self.lo, self.hi = lo, hi
@@ -86,13 +119,16 @@ class Lab1Processor(LabProcessor):
         n = int(self.rng.randint(lo, hi)) if hi > lo else int(lo)
         a = self.rng.uniform(self.lo, self.hi, n)
         b = self.rng.uniform(self.lo, self.hi, n)
-        return f"{n}\n{fmt_vector(a)}\n{fmt_vector(b)}", {"first_vector": a, "second_vector": b}, {"vector_size": n}
+        fmt = (lambda v: compat_vector_text(v, self.precision_array)) if self.compat else fmt_vector
+        return f"{n}\n{fmt(a)}\n{fmt(b)}", {"first_vector": a, "second_vector": b}, {"vector_size": n}
 
     def get_task_result(self, payload: str, **kwargs):
         payload = payload.strip()
         return np.array(payload.split(), dtype=np.float64) if payload else np.zeros(0)
 
     def verify_result(self, result, **kwargs) -> bool:
+        if self.compat:
+            return True  # reference lab1_processor.py:60-67 (allclose commented out)
         expect = kwargs["first_vector"] - kwargs["second_vector"]
         if result.shape != expect.shape:
             print(f"[verify_result] lab1: expected {expect.size} values, got {result.size}")
@@ -111,9 +147,11 @@ class _ImageLabProcessor(LabProcessor):
     def __init__(self, seed: int = 42, atol: float = 1e-10, precision_array: int = 10,
                  extra_links_to_png: Optional[List[str]] = None, dir_to_data: Optional[str] = None,
                  dir_to_data_out: Optional[str] = None, dir_to_data_out_gt: Optional[str] = None,
-                 lab_dir: Optional[str] = None, synthetic: Optional[str] = None, verify: str = "auto", **_):
+                 lab_dir: Optional[str] = None, synthetic: Optional[str] = None, verify: str = "auto",
+                 compat: bool = False, **_):
         super().__init__(seed)
         self.atol, self.precision_array = atol, precision_array
+        self.compat = bool(compat)
         # verify: "gt" = ground truth where it exists, other images pass (the
         # reference, lab2_processor.py:139-144); "cpu" = every image without GT
         # is compared byte for byte with the OpenMP CPU reference program's
@@ -153,12 +191,20 @@ class _ImageLabProcessor(LabProcessor):
         self.inputs: Dict[int, ImgData] = {}
         self.ground_truth: Dict[int, ImgData] = {}
         for i, p in enumerate(paths):
-            self.inputs[i] = ImgData(p, idx=i, cache_dir=cache)
+            # compat: the converted .data and the .txt / .png sidecars next to the
+            # input (reference utils/converter.py:32-53), else in the cache dir
+            side = os.path.dirname(os.path.abspath(p)) if self.compat else None
+            self.inputs[i] = ImgData(p, idx=i, cache_dir=side or cache)
+            if side:
+                self.inputs[i].write_sidecars(side, keep=p)
             stem = self.inputs[i].data_name
             for ext in ("txt", "data", "png"):
                 g = os.path.join(gt_dir, f"{stem}.{ext}")
                 if os.path.exists(g):
-                    self.ground_truth[i] = ImgData(g, idx=i)
+                    gside = os.path.dirname(os.path.abspath(g)) if self.compat else None
+                    self.ground_truth[i] = ImgData(g, idx=i, cache_dir=gside)
+                    if gside:
+                        self.ground_truth[i].write_sidecars(gside, keep=g)
                     break
         self.cursor = 0
 
@@ -189,7 +235,10 @@ class _ImageLabProcessor(LabProcessor):
                 "pixels": item.width * item.height}
 
     def get_task_result(self, payload: str, **kwargs):
-        return ImgData(kwargs["out_path_res"])
+        res = ImgData(kwargs["out_path_res"])
+        if self.compat:  # the reference converts every output, writing .txt / .png beside it
+            res.write_sidecars(os.path.dirname(os.path.abspath(kwargs["out_path_res"])), keep=kwargs["out_path_res"])
+        return res
 
     def task_stdin(self, item: ImgData, out_path: str) -> str:
         """The CPU program's stdin for ``item`` (the task without launch geometry)."""

@@ -36,7 +36,7 @@ class Tester:
     def __init__(self, binary_path_gpu: str, k_times: int, kernel_sizes: List[List[Any]],
                  metadata_columns2plot: Optional[List[str]] = None, binary_path_cpu: Optional[str] = None,
                  return_inp: bool = False, return_task_res: bool = False, timeout: Optional[float] = None,
-                 gpu_env: Optional[Dict[str, str]] = None, gpu_label: str = "HIP"):
+                 gpu_env: Optional[Dict[str, str]] = None, gpu_label: str = "HIP", compat: bool = False):
         self.binary_path_gpu = binary_path_gpu
         self.binary_path_cpu = binary_path_cpu
         self.k_times = int(k_times)
@@ -47,6 +47,9 @@ class Tester:
         self.timeout = timeout
         self.gpu_env = gpu_env
         self.gpu_label = gpu_label
+        # compat (run_test.py --compat): the reference's CSV schema and file
+        # names for a literal replay (processors.COMPAT_DEVIATIONS)
+        self.compat = bool(compat)
         self.dir2save = os.path.dirname(os.path.abspath(binary_path_gpu))
 
     # ------------------------------------------------------------------
@@ -71,9 +74,17 @@ class Tester:
                 }
                 if self.return_task_res:
                     row["task_result"] = rec.task_result
+                if self.compat:  # reference order: asdict(SubProcessResult) puts task_result second
+                    row = {k: row[k] for k in ("idx_run_time", "bin_name", "kernel_size", "test_verification_result",
+                                               "task_result", "time_kernel_exe_ms", "status", "err") if k in row}
                 row.update(processor.get_attr())
-                row.update(rec.debug_data)
+                row.update({k: v for k, v in rec.debug_data.items() if not (self.compat and k == "pixels")})
                 row["time_exe_ms_from_start_run_time_bin_name"] = (time.time() - t_start) * 1e3
+                if self.compat:
+                    rows.append(row)
+                    print(f"[Experiment bin_name=<{bin_name}> task={i} kernel_size=<{[k1, k2]}>] finished with "
+                          f"`time_kernel_exe_ms`: {rec.time_kernel_exe_ms} ms")
+                    continue
                 row["wall_ms"] = rec.wall_ms
                 row["device"] = device
                 row["n_gpus"] = int((env or {}).get("MPX_NGPUS", 1)) if device == self.gpu_label else 0
@@ -85,12 +96,14 @@ class Tester:
                       f"`time_kernel_exe_ms`: {rec.time_kernel_exe_ms} ms")
         df = pd.DataFrame(rows)
         ok = bool(rows) and all(bool(r["test_verification_result"]) for r in rows)
-        prefix = "cpu_" if (device != self.gpu_label and self.binary_path_gpu and
+        prefix = "cpu_" if (not self.compat and device != self.gpu_label and self.binary_path_gpu and
                             os.path.basename(binary_path) == os.path.basename(self.binary_path_gpu)) else ""
         if ok:
             print_stats([r["time_kernel_exe_ms"] for r in rows])
             df.to_csv(os.path.join(self.dir2save, f"stats_{prefix}{bin_name}.csv"), index=False)
             print(f"[Experiment bin_name=<{bin_name}>] SUCCESS!")
+            if self.compat:  # the plot groups by device, added after the CSV (reference tester.py:313-317)
+                df = df.assign(device=device)
             return df
         failed = df[~df["test_verification_result"].fillna(False).astype(bool)] if len(df) else df
         print(f"[Experiment bin_name=<{bin_name}>] FAILED: len={len(failed)}!")
@@ -117,7 +130,8 @@ class Tester:
         df = pd.concat([f for f in frames if len(f)], ignore_index=True) if any(len(f) for f in frames) else \
             pd.DataFrame()
         if len(df):
-            self.report_speedup(df)
+            if not self.compat:
+                self.report_speedup(df)
             self.plot(df)
         print(f"[Experiments] FINISH time exe: {time.time() - t0}")
         return df

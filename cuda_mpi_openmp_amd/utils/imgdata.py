@@ -136,9 +136,16 @@ class ImgData:
     def size_kb(self) -> float:
         return sys.getsizeof(self.raw) / 1024
 
-    def write_sidecars(self, out_dir: str) -> None:
-        """The reference's .txt/.png side files, but into ``out_dir``."""
+    def write_sidecars(self, out_dir: str, keep: Optional[str] = None) -> None:
+        """The reference's .txt/.png side files, but into ``out_dir``. ``keep``:
+        a source file that must not be overwritten by its own sidecar (a .txt or
+        .png input converted in place, as the reference does)."""
         os.makedirs(out_dir, exist_ok=True)
-        with open(os.path.join(out_dir, f"{self.data_name}.txt"), "w") as f:
-            f.write(self.hex)
-        rgba_to_png(self.pixels, os.path.join(out_dir, f"{self.data_name}.png"))
+        keep = os.path.abspath(keep) if keep else None
+        txt = os.path.join(out_dir, f"{self.data_name}.txt")
+        if os.path.abspath(txt) != keep:
+            with open(txt, "w") as f:
+                f.write(self.hex)
+        png = os.path.join(out_dir, f"{self.data_name}.png")
+        if os.path.abspath(png) != keep:
+            rgba_to_png(self.pixels, png)

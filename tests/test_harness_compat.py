@@ -1,0 +1,127 @@
+"""run_test.py --compat (VERDICT r4 Next #7): a literal replay of the reference
+harness's output-changing behaviour — lab1 array2string stdin, lab1 checks
+off, sidecars next to the inputs, the reference CSV schema — with the fixture
+outputs still byte-identical to the ground truth.
+
+Expected columns are the ones the survey recorded from the reference harness
+run on its own CPU programs (SURVEY §4 "verified test outcomes"; reference
+tester.py:224-285): idx_run_time, bin_name, kernel_size,
+test_verification_result, time_kernel_exe_ms, status, err, get_attr(),
+debug columns, time_exe_ms_from_start_run_time_bin_name.
+"""
+
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+
+from cuda_mpi_openmp_amd.harness.processors import COMPAT_DEVIATIONS, Lab1Processor, compat_vector_text
+
+from .helpers import ROOT, hex_bytes
+
+LAB1_COLS = ["idx_run_time", "bin_name", "kernel_size", "test_verification_result", "time_kernel_exe_ms", "status",
+             "err", "min_vector_size", "max_vector_size", "atol", "vector_size",
+             "time_exe_ms_from_start_run_time_bin_name"]
+LAB2_COLS = ["idx_run_time", "bin_name", "kernel_size", "test_verification_result", "time_kernel_exe_ms", "status",
+             "err", "precision_array", "atol", "filename", "time_exe_ms_from_start_run_time_bin_name"]
+
+
+def _copy_lab(tmp_path, lab):
+    dst = tmp_path / "labs" / lab
+    shutil.copytree(os.path.join(ROOT, "labs", lab, "src"), dst / "src", ignore=shutil.ignore_patterns("*.csv", "*.png"))
+    for sub in ("data", "data_out_gt"):
+        if os.path.isdir(os.path.join(ROOT, "labs", lab, sub)):
+            shutil.copytree(os.path.join(ROOT, "labs", lab, sub), dst / sub)
+    return dst
+
+
+def _run_test(args, cwd):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "run_test.py"), *args], cwd=cwd, capture_output=True,
+                          text=True, timeout=600)
+
+
+def test_compat_lab1_stdin_is_reference_array2string():
+    """The reference's exact text (seeded draw order randint, uniform, uniform;
+    lab1_processor.py:27-48), summarised with '...' beyond 1000 elements; the
+    default (fixed) form is the full round-trip text."""
+    p = Lab1Processor(compat=True)
+    text, kw, dbg = p.pre_process(device_info="x")
+    rs = np.random.RandomState(42)  # the reference seeds the global RNG with 42 (tester.py:60-62)
+    n = rs.randint(1024, 3072)
+    a = rs.uniform(-1e100, 1e100, n)
+    b = rs.uniform(-1e100, 1e100, n)
+    want = (f"{n}\n" + np.array2string(a, separator=" ", max_line_width=np.inf, precision=10)[1:-1].strip() + "\n" +
+            np.array2string(b, separator=" ", max_line_width=np.inf, precision=10)[1:-1].strip())
+    assert text == want and dbg == {"vector_size": n}
+    assert "..." in text.splitlines()[1]  # n > 1000: the reference's truncated input (Appendix B #2)
+    assert p.verify_result(np.zeros(3), **kw) is True  # checks off (Appendix B #3)
+    fixed = Lab1Processor()
+    t2, _, _ = fixed.pre_process(device_info="x")
+    assert "..." not in t2 and len(t2.splitlines()[1].split()) == n
+    assert compat_vector_text(np.array([1.0, -2.5]), 10) == "1.  -2.5"
+    assert {2, 3, 6, 8, "csv"} <= set(COMPAT_DEVIATIONS)
+
+
+def test_compat_lab1_csv_schema(tmp_path):
+    lab = _copy_lab(tmp_path, "lab1")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", "2", "--kernel_sizes", "[[null, null]]", "--compat",
+                   "--min_vector_size", "100", "--max_vector_size", "900"], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for name in ("stats_cpu_omp_exe.csv", "stats_cpu_exe.csv"):
+        df = pd.read_csv(lab / "src" / name)
+        assert list(df.columns) == LAB1_COLS
+        assert df["test_verification_result"].all() and df["status"].all()
+    assert not os.path.exists(lab / "src" / "speedup_cpu_omp_exe.csv")  # not a reference artefact
+
+
+def test_compat_lab1_summarised_input_is_refused_loudly(tmp_path):
+    """At the default sizes the reference's text holds 3 values per vector:
+    its programs read garbage and "pass" (checks off); ours refuse the short
+    input (checked I/O, Appendix B #11), so the run is recorded as failed."""
+    lab = _copy_lab(tmp_path, "lab1")
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_exe"), "--k_times", "1", "--kernel_sizes",
+                   "[[null, null]]", "--compat"], tmp_path)
+    assert "got 3" in r.stdout
+    df = pd.read_csv(lab / "src" / "failed_cpu_exe.csv")
+    assert list(df.columns)[:7] == LAB1_COLS[:7] and not df["status"].any()
+
+
+def test_compat_lab2_outputs_gt_and_sidecars(tmp_path):
+    from cuda_mpi_openmp_amd.harness.processors import LAB_IMAGE_FILES
+
+    lab = _copy_lab(tmp_path, "lab2")
+    before = set(os.listdir(lab / "data"))
+    n_inputs = sum(f in before for f in LAB_IMAGE_FILES)  # one round-robin pass reaches test_01 / test_02
+    r = _run_test(["--binary_path_cuda", str(lab / "src" / "cpu_omp_exe"), "--binary_path_cpu",
+                   str(lab / "src" / "cpu_exe"), "--k_times", str(n_inputs), "--kernel_sizes", "[[null, null]]",
+                   "--compat",
+                   "--metadata_columns2plot", '["filename"]'], tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "SUCCESS" in r.stdout and "FAILED" not in r.stdout
+    for name in ("stats_cpu_omp_exe.csv", "stats_cpu_exe.csv"):
+        df = pd.read_csv(lab / "src" / name)
+        assert list(df.columns) == LAB2_COLS
+    # the fixture outputs are byte-identical to the ground truth
+    for stem in ("test_01", "test_02"):
+        out = lab / "data_out" / "cpu_omp_exe_None_None" / f"{stem}.data"
+        with open(out, "rb") as f:
+            got = f.read()
+        assert got == hex_bytes(str(lab / "data_out_gt" / f"{stem}.txt"))
+        # ... and get their .txt / .png sidecars beside them (converter.py:32-38)
+        assert os.path.exists(out.with_suffix(".txt")) and os.path.exists(out.with_suffix(".png"))
+    # sidecars next to the inputs (converter.py:32-53): .data for .txt/.png inputs, .txt/.png for .data inputs
+    after = set(os.listdir(lab / "data"))
+    assert before <= after
+    assert "test_01.data" in after and "test_01.png" in after
+    for f in before:
+        stem, ext = os.path.splitext(f)
+        if ext == ".data":
+            assert f"{stem}.txt" in after and f"{stem}.png" in after
+    # the inputs themselves are unchanged
+    for f in before:
+        with open(lab / "data" / f, "rb") as a, open(os.path.join(ROOT, "labs", "lab2", "data", f), "rb") as b:
+            assert a.read() == b.read(), f
