@@ -105,6 +105,7 @@ _SIGNATURES = {
     "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_scatter_probe": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_ws_status": (c_int, [c_vp, c_i64, c_int]),
+    "mpx_sort_lane_order_ok": (c_int, [c_vp]),
     "mpx_cpu_sort": (None, [c_vp, c_i64, c_int]),
     "mpx_rows_checksum": (c_int, [c_vp, c_i64, c_int, c_i64, c_int, c_vp, c_vp]),
     "mpx_peer_probe_run": (c_int, [c_vp, c_vp]),

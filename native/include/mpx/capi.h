@@ -318,6 +318,12 @@ int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, int64_t works
  * sort that last used `workspace` gave up (hardware-fault detector). */
 int mpx_sort_ws_status(const void *workspace, int64_t n, int dtype);
 int mpx_sort(void *data, int64_t n, int dtype, void *stream);
+/* 1 when the current device applies same-address returning LDS adds in
+ * ascending lane order (the stability premise of the production radix
+ * ranking; probed once per device, synchronising the stream), 0 when not,
+ * negative when the probe could not run. AUTO falls back to the peer-mask
+ * ranking unless 1. */
+int mpx_sort_lane_order_ok(void *stream);
 
 /* ---------------- CPU references (OpenMP, -O3, same numerics) ---------------- */
 int mpx_cpu_threads(void);

@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <utility>
 #include <cstdlib>
+#include <cstring>
 
 #include "internal.hpp"
 
@@ -891,6 +892,185 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
 }
 
 // ---------------------------------------------------------------------------
+// MFMA8S: the same exact int8 distance GEMM for nc <= 8 classes on
+// v_mfma_i32_4x4x4_16b_i8 (16 blocks of 4 x 4 x 4; VERDICT r4 Next #4), one
+// pixel per lane.
+//   The 32x32 form above gives every pixel to two lanes (the two K halves)
+//   and spends 75% of its rows on absent classes below 9 classes: the
+//   per-pixel feature bytes are built twice and the ranking merges half-waves.
+//   Here the 16-byte feature vector of a pixel is four dwords (K = 4 per
+//   instruction, four chained instructions per row set) that ONE lane builds,
+//   and every result of the pixel lands in that lane:
+//     A (weights): lane l supplies row l & 3 of every block (the blocks share
+//                  the weights): row r of row set s = limb r & 1 (0: a, 1: b)
+//                  of class 2 s + (r >> 1), slots 4 t .. 4 t + 3 for step t;
+//     B (features): lane l supplies column l & 3 of block l >> 2 — its pixel;
+//     D: lane l, register r = row r of its own pixel's column.
+//   (Layout measured on gfx950 with tools/experiments/mfma4_layout.hip.)
+//   Features (build_i8's slots): F0 = h(rr gg bb rg), F1 = h(rb gb) r g,
+//   F2 = l(rr gg bb rg), F3 = l(rb gb) b 0, from three v_pk_mad-style 16-bit
+//   products P + 128 of the centred channels: h = byte 1 of P + 128, l = byte 0
+//   of P = byte 0 of (P + 128) ^ 0x80.
+//   Keys as in MFMA8: ((D_a << 8) + D_b) << 5 | class — two v_lshl_add per
+//   class — then the running top-2 in the lane; no cross-lane merge.
+//   NS = row sets (2 classes each) with real classes: 1, 2, 3 or 4.
+// ---------------------------------------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+struct Mfma8sLane {
+    int w[4][4];     // [row set][step]: 4 int8 weights of this lane's row
+    i32x4 cinit[4];  // [row set]: {0, c(2s), 0, c(2s + 1)}
+};
+
+__device__ __forceinline__ Mfma8sLane mfma8s_lane(const I8Params &ip, int lane) {
+    Mfma8sLane L;
+    const int r = lane & 3;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int c = 2 * s + (r >> 1);
+        const uint64_t *limb = (r & 1) ? ip.b[c] : ip.a[c];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) L.w[s][t] = (int)(uint32_t)(limb[t >> 1] >> (32 * (t & 1)));
+        L.cinit[s] = i32x4{0, ip.c[2 * s], 0, ip.c[2 * s + 1]};
+    }
+    return L;
+}
+
+__device__ __forceinline__ uint32_t s16x2_bits(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// the four feature dwords of pixel p (build_i8's slot order)
+__device__ __forceinline__ void mfma8s_features(uint32_t p, int (&F)[4]) {
+    const uint32_t x = p ^ 0x80808080u;  // centred channels as signed bytes
+    const int xi = (int)x;
+    const short r = (short)__builtin_amdgcn_sbfe(xi, 0, 8), g = (short)__builtin_amdgcn_sbfe(xi, 8, 8),
+                b = (short)__builtin_amdgcn_sbfe(xi, 16, 8);
+    const s16x2 c128 = {128, 128};
+    const s16x2 U = {r, g}, V = {b, r}, W = {b, g}, Z = {b, b};
+    const uint32_t P01 = s16x2_bits(U * U + c128);  // [rr | gg] + 128
+    const uint32_t P23 = s16x2_bits(V * W + c128);  // [bb | rg] + 128
+    const uint32_t P45 = s16x2_bits(U * Z + c128);  // [rb | gb] + 128
+    F[0] = (int)__builtin_amdgcn_perm(P23, P01, 0x07050301u);                  // h(rr gg bb rg)
+    F[1] = (int)__builtin_amdgcn_perm(x, P45, 0x05040301u);                    // h(rb gb), r, g
+    F[2] = (int)(__builtin_amdgcn_perm(P23, P01, 0x06040200u) ^ 0x80808080u);  // l(rr gg bb rg)
+    F[3] = (int)(__builtin_amdgcn_perm(x, P45, 0x0C060200u) ^ 0x00008080u);    // l(rb gb), b, 0
+}
+
+// rank one pixel: provisional output and whether its top-2 margin is within T2
+template <int NS>
+__device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane &L, int32_t T2k, bool &undecided) {
+    int F[4];
+    mfma8s_features(p, F);
+    i32x4 D[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) D[s] = L.cinit[s];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) D[s] = __builtin_amdgcn_mfma_i32_4x4x4i8(L.w[s][t], F[t], D[s], 0, 0, 0);
+    int32_t B = INT32_MAX, S = INT32_MAX;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // v_lshl_or_b32 + v_lshl_add_u32 per class (the empty asm keeps the
+            // compiler from re-associating them into shift, shift-add and or;
+            // it costs an s_nop 0, a cycle of this wave, not a VALU slot)
+            uint32_t x = ((uint32_t)D[s][2 * h + 1] << 5) | (uint32_t)(2 * s + h);
+            asm volatile("" : "+v"(x));
+            const int32_t key = (int32_t)(((uint32_t)D[s][2 * h] << 13) + x);
+            S = max(min(B, key), min(max(B, key), S));
+            B = min(B, key);
+        }
+    }
+    // (S >> 5) - (B >> 5) <= T2, tested conservatively on the tagged keys:
+    // S - B <= 32 T2 + 31 (T2k) holds whenever the exact test does
+    undecided = (uint32_t)(S - B) <= (uint32_t)T2k;
+    return __builtin_amdgcn_perm((uint32_t)B & 31u, p, 0x04020100u);
+}
+
+// The deferred list holds one entry per (lane, trip) with any undecided
+// pixel: the 16-B vector index and a 4-bit mask of its undecided pixels —
+// one append per trip instead of one per pixel (with ~0.4% of the pixels
+// undecided at nc = 4, a quarter of the trips have one). The pixels are
+// re-read from the image after the loop: their RGB bytes are untouched.
+constexpr int kAmb8sCap = 1024;
+
+template <int NS>
+__global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
+                                                              ClassParams cp, I8Params ip, FastParams fp,
+                                                              uint32_t *amb) {
+    const Mfma8sLane L = mfma8s_lane(ip, threadIdx.x & 63);
+    const int32_t T2k = ip.T2 * 32 + 31;
+    __shared__ int64_t s_amb[kAmb8sCap];  // vector index << 4 | undecided-pixel mask
+    __shared__ uint32_t s_namb, s_npx;
+    if (threadIdx.x == 0) s_namb = s_npx = 0;
+    __syncthreads();
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 qn = i < nvec ? v[i] : uint4{};
+    for (; i < nvec; i += stride) {
+        const uint4 q = qn;
+        if (i + stride < nvec) qn = v[i + stride];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        uint32_t o[4];
+        bool u[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o[m] = mfma8s_pixel<NS>(px[m], L, T2k, u[m]);
+        // the test on the four compare masks (scalar ORs); the entry's bit mask
+        // is built only inside the rare branch
+        if (__builtin_expect(u[0] | u[1] | u[2] | u[3], 0)) {
+            const uint32_t mask = (uint32_t)u[0] | ((uint32_t)u[1] << 1) | ((uint32_t)u[2] << 2) | ((uint32_t)u[3] << 3);
+            const uint32_t slot = atomicAdd(&s_namb, 1u);
+            if (slot < (uint32_t)kAmb8sCap) {
+                s_amb[slot] = (i << 4) | mask;
+            } else {  // list full: the exact chain inline (never at the benchmark's rates)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if ((mask >> m) & 1u) o[m] = classify_direct(px[m], nc, cp);
+            }
+        }
+        v[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    // the deferred pixels: the fp32 proven-margin ranking first, the exact fp64
+    // chain for what it leaves (as in MFMA8, every lane busy in each stage)
+    __shared__ int64_t s_amb2[kAmb8Cap2];
+    __shared__ uint32_t s_ambpx2[kAmb8Cap2];
+    __shared__ uint32_t s_namb2;
+    if (threadIdx.x == 0) s_namb2 = 0;
+    __syncthreads();
+    const uint32_t nd = min(s_namb, (uint32_t)kAmb8sCap);
+    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+        const int64_t e = s_amb[j];
+        const int64_t vi = e >> 4;
+        const uint32_t mask = (uint32_t)e & 15u;
+        atomicAdd(&s_npx, (uint32_t)__popc(mask));
+        const uint4 q = v[vi];  // this thread's own vector: written above in program order
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        for (int m = 0; m < 4; ++m) {
+            if (!((mask >> m) & 1u)) continue;
+            uint32_t o;
+            if (classify_fp32_one(px[m], nc, fp, o)) {
+                img[vi * 4 + m] = o;
+            } else {
+                const uint32_t slot = atomicAdd(&s_namb2, 1u);
+                if (slot < (uint32_t)kAmb8Cap2) {
+                    s_amb2[slot] = vi * 4 + m;
+                    s_ambpx2[slot] = px[m];
+                } else {
+                    img[vi * 4 + m] = classify_direct(px[m], nc, cp);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (amb && threadIdx.x == 0 && s_npx) atomicAdd(amb, s_npx);  // one global add per block
+    const uint32_t nd2 = min(s_namb2, (uint32_t)kAmb8Cap2);
+    for (uint32_t j = threadIdx.x; j < nd2; j += blockDim.x) img[s_amb2[j]] = classify_direct(s_ambpx2[j], nc, cp);
+}
+
+// ---------------------------------------------------------------------------
 // Host: expanded fp32 weights and the rigorous decision margin.
 // ---------------------------------------------------------------------------
 typedef long double ld;
@@ -1051,39 +1231,63 @@ bool build_i8(int nc, const double *mu, const double *inv, I8Params &ip) {
                 mag = std::fmax(mag, std::fabs(w[c][kSlotW[s]]) * kPhiMax[kSlotW[s]]);
             }
     if (!(vmax > 0) || !(mag < 1e30L)) return false;
-    ld u = vmax / 32639;
+    // The decision bound uses the weights' ACTUAL rounding errors (round 5):
+    // per class, u (sum_s |delta_cs| Fmax_s + |delta_c|) with delta = the
+    // integer minus the exact scaled weight, instead of the worst case u / 2
+    // per unit — and the scale u is chosen among 256 candidates just above the
+    // smallest that fits for the smallest margin in value units (T2 u), so
+    // fewer pixels fall inside it and take the exact fallback.
     long long v[MPX_MAX_CLASSES][kSlots], cc[MPX_MAX_CLASSES];
-    for (int attempt = 0;; ++attempt) {
-        if (attempt > 60) return false;
-        bool fits = true;
-        for (int c = 0; c < nc && fits; ++c) {
+    auto fits_at = [&](ld u, long long (*vv)[kSlots], long long *cv) -> bool {
+        for (int c = 0; c < nc; ++c) {
             ld tot = 0;
             for (int s = 0; s < kSlots; ++s) {
-                v[c][s] = kSlotW[s] >= 0 ? std::llround(w[c][kSlotW[s]] * kSlotScale[s] / u) : 0;
-                if (std::llabs(v[c][s]) > 32639) fits = false;
-                tot += kSlotFmax[s] * (ld)std::llabs(v[c][s]);
+                vv[c][s] = kSlotW[s] >= 0 ? std::llround(w[c][kSlotW[s]] * kSlotScale[s] / u) : 0;
+                if (std::llabs(vv[c][s]) > 32639) return false;
+                tot += kSlotFmax[s] * (ld)std::llabs(vv[c][s]);
             }
             const ld cw = w[c][9] / u;
-            if (!(std::fabs(cw) < (ld)(1 << 26))) {
-                fits = false;
-                break;
-            }
-            cc[c] = std::llround(cw);
-            tot += (ld)std::llabs(cc[c]);
-            if (!(tot < (ld)(1 << 26) - 64)) fits = false;  // key = ((D_a << 8) + D_b) << 5 | tag
+            if (!(std::fabs(cw) < (ld)(1 << 26))) return false;
+            cv[c] = std::llround(cw);
+            tot += (ld)std::llabs(cv[c]);
+            if (!(tot < (ld)(1 << 26) - 64)) return false;  // key = ((D_a << 8) + D_b) << 5 | tag
         }
-        if (fits) break;
-        u *= 2;
+        return true;
+    };
+    // margin in key units at scale u (the integers already in vv / cv)
+    auto t2_at = [&](ld u, long long (*vv)[kSlots], const long long *cv) -> ld {
+        ld tmax = 0;
+        for (int c = 0; c < nc; ++c) {
+            ld q = std::fabs((ld)cv[c] - w[c][9] / u);  // constant rounding, <= 1/2
+            for (int s = 0; s < kSlots; ++s)
+                if (kSlotW[s] >= 0) q += kSlotFmax[s] * std::fabs((ld)vv[c][s] - w[c][kSlotW[s]] * kSlotScale[s] / u);
+            // weight + constant rounding (exact integer arithmetic otherwise) + reference chain + long-double slack
+            const ld t = (u * q + refb[c] + psd[c] + 1e-15L * mag * 16) * 1.001L + u * 1e-6L;
+            tmax = std::fmax(tmax, t);
+        }
+        return std::ceil(2 * tmax / u) + 1;
+    };
+    ld u0 = vmax / 32639;
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 60) return false;
+        if (fits_at(u0, v, cc)) break;
+        u0 *= 2;
     }
-    ld tmax = 0;
-    for (int c = 0; c < nc; ++c) {
-        ld fsum = 0;
-        for (int s = 0; s < kSlots; ++s) fsum += kSlotFmax[s];
-        // weight rounding + constant rounding + reference chain + long-double slack
-        const ld t = (u / 2 * fsum + u / 2 + refb[c] + psd[c] + 1e-15L * mag * 16) * 1.001L;
-        tmax = std::fmax(tmax, t);
+    ld best_u = u0, t2 = t2_at(u0, v, cc);
+    {
+        long long vv[MPX_MAX_CLASSES][kSlots], cv[MPX_MAX_CLASSES];
+        for (int k = 1; k < 256; ++k) {
+            const ld u = u0 * (1 + (ld)k / 1024);
+            if (!fits_at(u, vv, cv)) continue;
+            const ld t = t2_at(u, vv, cv);
+            if (t * u < t2 * best_u) {
+                best_u = u;
+                t2 = t;
+                std::memcpy(v, vv, sizeof(v));
+                std::memcpy(cc, cv, sizeof(cc));
+            }
+        }
     }
-    const ld t2 = std::ceil(2 * tmax / u) + 1;
     if (!(t2 < (ld)(1 << 24))) return false;  // nothing would ever be decided
     ip.T2 = (int32_t)t2;
     for (int c = 0; c < MPX_MAX_CLASSES; ++c) {
@@ -1181,7 +1385,31 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     I8Params ip8;
     const int chosen = classify_resolve(nc, mu, inv, path, aligned16(img), fp, fp64, ip8);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
-    if (chosen == MPX_CLS_MFMA8) {
+    // MFMA8 below 9 classes: the one-pixel-per-lane 4x4x4 form (MFMA8S);
+    // MPX_CLS_MFMA8_SMALL=0 keeps the 32x32 form there (A/B)
+    static const bool small8 = [] {
+        const char *e = std::getenv("MPX_CLS_MFMA8_SMALL");
+        return !(e && e[0] == '0');
+    }();
+    if (chosen == MPX_CLS_MFMA8 && nc <= 8 && small8) {
+        const int64_t nvec = npix / 4;
+        if (nvec > 0) {
+            const int64_t blocks = (nvec + 255) / 256;
+            const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256)
+                                   : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            const int ns = (nc + 1) / 2;
+            if (ns == 1)
+                hipLaunchKernelGGL(classify_mfma8s_kernel<1>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+            else if (ns == 2)
+                hipLaunchKernelGGL(classify_mfma8s_kernel<2>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+            else if (ns == 3)
+                hipLaunchKernelGGL(classify_mfma8s_kernel<3>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+            else
+                hipLaunchKernelGGL(classify_mfma8s_kernel<4>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nvec * 4;
+        }
+    } else if (chosen == MPX_CLS_MFMA8) {
         const int64_t nchunks = npix / 128;
         // MPX_CLS_MFMA8_WIN=1: windowed fix-ups (every byte written once, 1.03x
         // the image's bytes against 1.22x, but 434-444 -> 523 us at nc = 32 on

@@ -39,6 +39,7 @@
 //     / mpx_sort_ws): the Python op takes it from torch's caching allocator on
 //     the tensor's stream, so concurrent sorts on different streams or devices
 //     never share scratch.
+#include <atomic>
 #include <mutex>
 
 #include "internal.hpp"
@@ -1357,8 +1358,68 @@ void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src
 #undef MPX_LEAN
 }
 
+// Lane order of same-address returning LDS adds. The RANK >= 1
+// scatters (variants 9-17, AUTO above 2^18 keys) are stable only because one
+// ds_add_rtn_u32 applies its same-address lanes in ascending lane order —
+// observed on gfx950, not promised by the ISA. This probe checks it once per
+// device before the first such sort: four waves, three address patterns
+// (every lane on one counter; lane % 3; a scattered 5-way split), each lane's
+// returned count must equal the number of lower lanes on its counter. On a
+// failure AUTO falls back to the peer-mask ranking (variants 7 / 8, which
+// rank with explicit lane masks) and the explicit RANK variants refuse.
+__global__ __launch_bounds__(256) void lds_rtn_order_probe_kernel(uint32_t *bad) {
+    __shared__ uint32_t cnt[4][3][8];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = lane; i < 24; i += 64) (&cnt[w][0][0])[i] = 0;
+    __syncthreads();
+    uint32_t err = 0;
+    const int addr[3] = {0, lane % 3, (lane * 7) % 5};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t got = atomicAdd(&cnt[w][k][addr[k]], 1u);
+        uint32_t want = 0;
+        for (int j = 0; j < lane; ++j) {
+            const int aj = k == 0 ? 0 : k == 1 ? j % 3 : (j * 7) % 5;
+            want += aj == addr[k];
+        }
+        err |= got != want;
+    }
+    if (err) bad[0] = 1u;  // vector store; any lane of any wave
+}
+
+// 1 = ascending lane order holds on the current device, 0 = it does not,
+// negative = the probe could not run (treated as "does not hold")
+int lds_rtn_order_ok(hipStream_t s) {
+    static std::atomic<int> cache[64];
+    static std::once_flag init;
+    std::call_once(init, [] {
+        for (auto &c : cache) c.store(-2);
+    });
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    int v = cache[dev].load();
+    if (v != -2) return v;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+        return -1;  // no synchronous probe inside a graph capture (not cached: the next eager sort probes)
+    uint32_t *d = nullptr, h = 1u;
+    int ok = -1;
+    if (hipMalloc(&d, sizeof(uint32_t)) == hipSuccess) {
+        if (hipMemsetAsync(d, 0, sizeof(uint32_t), s) == hipSuccess) {
+            hipLaunchKernelGGL(lds_rtn_order_probe_kernel, dim3(1), dim3(256), 0, s, d);
+            if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                hipStreamSynchronize(s) == hipSuccess)
+                ok = h == 0u ? 1 : 0;
+        }
+        (void)hipFree(d);
+    }
+    cache[dev].store(ok);
+    return ok;
+}
+
 int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStream_t s) {
     const RadixWs r = radix_layout(ws, n);
+    const bool auto_variant = variant == 0;
     // 4096-key tiles win up to 2^24 keys (2^20: 0.070 vs 0.075 ms, 2^24: 0.221
     // vs 0.229) and lose at 2^26 (0.987 vs 0.828; not yet explained — a
     // candidate: with 16 tiles per block the 64-B digit runs of neighbouring
@@ -1367,6 +1428,12 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // two tiles of keys in flight, on 4096-key tiles up to 2^23 keys (13),
     // on 8192-key tiles above (12)
     if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 13 : 12;
+    // the returning-add ranking needs ascending lane order (probe above)
+    const bool rtn_rank = (variant >= 9 && variant <= 17);
+    if (rtn_rank && lds_rtn_order_ok(s) != 1) {
+        if (!auto_variant) return MPX_ERR_UNSUPPORTED;
+        variant = n <= kTile4kMaxN ? 8 : 7;
+    }
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
@@ -1668,3 +1735,5 @@ extern "C" int mpx_sort_scatter_probe(const void *data, int64_t n, void *workspa
                                       void *stream) {
     return mpx::scatter_probe(data, n, workspace, workspace_bytes, knock, stream);
 }
+
+extern "C" int mpx_sort_lane_order_ok(void *stream) { return mpx::lds_rtn_order_ok(mpx::as_stream(stream)); }

@@ -292,6 +292,23 @@ def test_classify_random_pixels_and_fallback_rate(gpu, path):
         assert amb.item() == 0
 
 
+@pytest.mark.parametrize("nc", [1, 2, 3, 4, 6, 7, 8])
+def test_classify_mfma8_small_class_counts(gpu, nc):
+    """mfma8 below 9 classes runs the one-pixel-per-lane 4x4x4 int8 MFMA form
+    (classify_mfma8s_kernel, every row-set count 1-4): uniform random pixels,
+    classes identical to the CPU reference, the exact fallback rare."""
+    img = rand_img(517, 643, seed=nc)  # 332431 pixels: vector body + 3-pixel tail
+    mu, inv = ops.class_stats(img, _random_classes(img, nc, 64, 100 + nc))
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    assert ops.classify_plan(mu, inv, "mfma8")[0] == "mfma8"
+    d = img.to(gpu)
+    amb = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.classify_(d, mu, inv, path="mfma8", ambiguous=amb)
+    assert torch.equal(d.cpu(), cpu)
+    assert amb.item() < 0.04 * img.shape[0] * img.shape[1]
+
+
 @pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8"])
 def test_classify_exact_ties_all_fall_back(gpu, path):
     """Duplicated classes tie exactly on every pixel: every pixel must take the

@@ -20,3 +20,39 @@ ckpt_r5_sustain() {
     mkdir -p "$O"
     bash tools/gpu.sh run sustain 300 python -u tools/experiments/sustain_clocks.py --out "$O/sustain" "$@"
 }
+
+# C: lab3 small class counts on the 4x4x4 int8 MFMA form (VERDICT r4 Next #4):
+# the layout probe, the classifier GPU tests, then 8192^2 timings alternated
+# (fast32 / mfma8s / the 32x32 mfma8 form) and the MFMA counters of the new path.
+ckpt_r5_lab3() {
+    export O=${O:-gpurun_out/r5/lab3}
+    mkdir -p "$O"
+    timeout -k 10 60 bin/mfma4_layout > "$O/mfma4_layout.json" &&
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    for r in 1 2; do
+        LAB3_NCS=2,4,6,8,12,16 LAB3_PATHS=fast,mfma8 LAB3_TAG=small$r \
+            bash tools/gpu.sh run lab3_new$r 300 python -u tools/experiments/lab3_ab.py &&
+        MPX_CLS_MFMA8_SMALL=0 LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 LAB3_TAG=old$r \
+            bash tools/gpu.sh run lab3_old$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done &&
+    LAB3_NCS=4 LAB3_PATHS=mfma8 bash tools/gpu.sh prof lab3_trace -- python tools/experiments/lab3_ab.py &&
+    LAB3_NCS=4 LAB3_PATHS=mfma8 bash tools/gpu.sh pmc lab3_pmc \
+        "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" -- \
+        python tools/experiments/lab3_ab.py
+}
+
+# D: after the tighter int8 bound and the per-trip deferral: classifier +
+# sort GPU tests, lab3 8192^2 fast vs mfma8 alternated, the AUTO sweep.
+ckpt_r5_lab3b() {
+    export O=${O:-gpurun_out/r5/lab3b}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py tests/test_lab5_sort.py \
+        -k "classify or sort" &&
+    for r in 1 2; do
+        LAB3_NCS=2,3,4,5,6,8,12,16,20,24,32 LAB3_PATHS=fast,mfma8 LAB3_TAG=r$r \
+            bash tools/gpu.sh run lab3_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done &&
+    LAB3_NCS=4 LAB3_PATHS=mfma8 bash tools/gpu.sh pmc lab3_pmc \
+        "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" -- \
+        python tools/experiments/lab3_ab.py
+}

@@ -146,7 +146,38 @@ def run_one(name, args, dev, streams, cs):
     return rec
 
 
+def render(path: str) -> str:
+    """Markdown tables of a sustain_clocks.json: per workload and round, the
+    burst / steady / after-load step times and the board state in each phase."""
+    d = json.load(open(path))
+    out = ["| workload | round | burst µs (clock MHz) | 0-10 ms | 10-20 ms | 20-50 ms | 50-100 ms | 0.5-1 s | 1-2 s "
+           "(MHz, W) | K=20 after 2 s µs | after / burst |", "|---|---|---|---|---|---|---|---|---|---|---|"]
+    for r in d["runs"]:
+        bins = {tuple(b["ms"]): b for b in r["bins"]}
+
+        def cell(lo, hi, clocks=False):
+            b = bins.get((lo, hi))
+            if not b:
+                return "–"
+            c = b.get("clocks") or {}
+            extra = f" ({c.get('gfxclk_mhz', 0):.0f}, {c.get('power_w', 0):.0f})" if clocks else ""
+            return f"{b['us_per_step']:.2f}{extra}"
+        bc = r.get("burst_clocks") or {}
+        out.append(f"| {r['workload']} | {r['round']} | {r['burst_us']:.2f} ({bc.get('gfxclk_mhz', 0):.0f}) | "
+                   f"{cell(0, 10)} | {cell(10, 20)} | {cell(20, 50)} | {cell(50, 100)} | {cell(500, 1000)} | "
+                   f"{cell(1000, 2000, True)} | {r['after_us']:.2f} | {r['after_retained']:.3f} |")
+    m = d["meta"]
+    out.append("")
+    out.append(f"Sampler: {m['sampler']} at {m['sampler_hz']:.0f} Hz ({m['samples']} samples, "
+               f"{m['read_us_med']:.0f} µs per read); chunks of {m['args']['chunk']} steps; "
+               f"{m['args']['idle_ms']:.0f} ms idle before each workload.")
+    return "\n".join(out)
+
+
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--render":
+        print(render(sys.argv[2]))
+        return
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--workloads", default="copy,vsub,roberts,sobel5")
     p.add_argument("--size", type=int, default=4096)
@@ -193,6 +224,8 @@ def main():
             f.write("t_ms," + ",".join(keys) + "\n")
             for t, m in cs.samples:
                 f.write(f"{(t - t00) / 1e6:.3f}," + ",".join(f"{m[k]:.6g}" if k in m else "" for k in keys) + "\n")
+    with open(os.path.join(a.out, "sustain_clocks.md"), "w") as f:
+        f.write(render(os.path.join(a.out, "sustain_clocks.json")) + "\n")
     print(json.dumps({"meta": meta}), flush=True)
 
 

@@ -20,6 +20,7 @@
 # FETCH_SIZE / WRITE_SIZE get passes of their own. tools/pmc_median.py merges
 # the passes (median per kernel); tools/prof_summary.py writes the tables.
 set -o pipefail
+O_GIVEN=${O:-}
 O=${O:-gpurun_out/scratch}
 mkdir -p "$O"
 cd /tmp 2>/dev/null && cd - >/dev/null
@@ -104,7 +105,9 @@ case "$cmd" in
       here=$(dirname "$0")
       for f in "$here"/checkpoints/*.sh; do . "$f"; done
       declare -F "ckpt_$1" >/dev/null || { echo "[gpu.sh] no checkpoint $1"; exit 2; }
-      "ckpt_$1"
+      [ -n "$O_GIVEN" ] || unset O  # the checkpoint's own default output directory
+      name=$1; shift
+      "ckpt_$name" "$@"
     fi ;;
   *)
     sed -n 2,21p "$0"; exit 2 ;;
