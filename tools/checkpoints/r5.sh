@@ -56,3 +56,50 @@ ckpt_r5_lab3b() {
         "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" -- \
         python tools/experiments/lab3_ab.py
 }
+
+# E: the per-dispatch shader clock (GRBM_GUI_ACTIVE / duration) along the
+# sustain protocol, sobel5 vs roberts vs copy (one counter, kernel trace only).
+ckpt_r5_dclk() {
+    export O=${O:-gpurun_out/r5/dclk}
+    mkdir -p "$O"
+    timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace -d "$O/dclk" -o "dclk_%pid%" -- \
+        python tools/experiments/sustain_clocks.py --workloads sobel5,roberts,copy --rounds 1 --sustain-ms 1500 \
+        --hz 50 --out "$O/sustain" > "$O/dclk.log" 2>&1 &&
+    for k in conv_band4 conv_wave linear_copy; do
+        python tools/experiments/dispatch_clock.py "$(ls "$O"/dclk/*_results.db | head -1)" --grep "$k" \
+            --csv "$O/dispatch_$k.csv" > "$O/dispatch_$k.md" || return 1
+    done
+}
+
+# F: the value_streaming gap (VERDICT r4 Next #5): layouts and data in one
+# process, interleaved rounds, then the same under a kernel trace.
+ckpt_r5_gap() {
+    export O=${O:-gpurun_out/r5/gap}
+    mkdir -p "$O"
+    bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py &&
+    GAP_ROUNDS=4 bash tools/gpu.sh prof gap_trace -- python tools/experiments/stream_gap.py
+}
+
+# G (final tree): smoke, the driver's bench, and the per-kernel profile
+# (kernel trace + the standard counter passes over tools/prof_all.py),
+# summarised on the box (the rocpd databases exceed gpurun's 64 MiB return).
+ckpt_r5_final() {
+    export O=${O:-gpurun_out/r5/final}
+    mkdir -p "$O"
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh profile kfinal -- python3 tools/prof_all.py &&
+    python tools/experiments/kprof_table.py "$O" > "$O/kernels_table.md" &&
+    python tools/pmc_median.py "$O"/kfinal.pmc* > "$O/medians.md" &&
+    python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
+    du -sh "$O" && find "$O" -name "*.db" -delete && du -sh "$O"
+}
+
+# H: the same-methodology harness comparison (VERDICT r4 Next #3), lab2 + the
+# 4096^2 synthetic bucket in one call, lab1 in another
+ckpt_r5_hcmp2() {
+    timeout -k 10 1100 bash tools/harness_compare.sh lab2 lab2xl
+}
+ckpt_r5_hcmp1() {
+    timeout -k 10 1100 bash tools/harness_compare.sh lab1
+}

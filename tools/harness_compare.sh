@@ -5,8 +5,10 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-# usage: harness_compare.sh [lab2] [lab1]   (default: both)
-WHICH="${*:-lab2 lab1}"
+# usage: harness_compare.sh [lab2] [lab2xl] [lab1]   (default: all three)
+#   lab2xl: the BASELINE shape through the same harness — one synthetic 4096^2
+#   random RGBA8 image (--synthetic 4096x4096, seeded), no other input
+WHICH="${*:-lab2 lab2xl lab1}"
 O=$PWD/gpurun_out/harness_cmp
 mkdir -p $O
 GEOMS2='[[[16,16],[1024,1024]],[[16,16],[32,32]],[[2,2],[16,16]],[[32,32],[16,16]],[[32,32],[64,64]],[[0,0],[0,0]]]'
@@ -17,6 +19,18 @@ for bucket in $([[ " $WHICH " == *" lab2 "* ]] && echo small medium large); do
     timeout -k 10 600 python run_test.py --binary_path_cuda $W/src/to_plot_hip_exe --binary_path_cpu $W/src/cpu_exe \
       --k_times 12 --kernel_sizes "$GEOMS2" --timing $timing --dir_to_data labs/lab2/metric_calc/$bucket --dir_to_data_out $W/data_out \
       --metadata_columns2plot '["filename"]' > $W/run.log 2>&1 || { tail -20 $W/run.log; exit 1; }
+    grep -E "SUCCESS|FAILED|Speedup" $W/run.log | head -5
+    rm -rf $W/data_out $W/src/*.png
+  done
+done
+for bucket in $([[ " $WHICH " == *" lab2xl "* ]] && echo xl4096); do
+  mkdir -p $O/empty_inputs
+  for timing in cold warm; do
+    W=$O/lab2_${bucket}_${timing}/lab2; mkdir -p $W/src
+    cp labs/lab2/src/to_plot_hip_exe labs/lab2/src/cpu_exe $W/src/
+    timeout -k 10 900 python run_test.py --binary_path_cuda $W/src/to_plot_hip_exe --binary_path_cpu $W/src/cpu_exe \
+      --k_times 6 --kernel_sizes "$GEOMS2" --timing $timing --dir_to_data $O/empty_inputs --synthetic 4096x4096 \
+      --dir_to_data_out $W/data_out --metadata_columns2plot '["filename"]' > $W/run.log 2>&1 || { tail -20 $W/run.log; exit 1; }
     grep -E "SUCCESS|FAILED|Speedup" $W/run.log | head -5
     rm -rf $W/data_out $W/src/*.png
   done
