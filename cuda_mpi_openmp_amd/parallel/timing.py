@@ -10,8 +10,12 @@ beside it: it never charges start skew between ranks (a rank that leaves the
 barrier late, or whose first launch stalls, while its neighbours already run
 independent steps), so it can only over-state the rate.
 
+:func:`aligned_start` starts every rank at one agreed instant of that clock
+after the opening barrier + device sync, so the ranks' host wake-up jitter
+out of the barrier does not count as start skew.
+
 ``MPX_BENCH_START_DELAY="rank:ms[,rank:ms...]"`` sleeps on the named ranks
-between the opening barrier and ``t0``: a fault-injection hook that creates a
+between the aligned start and ``t0``: a fault-injection hook that creates a
 known start skew for the tests (tests/test_bench_contract.py).
 
 Reference: the reference times only events around one kernel launch
@@ -25,12 +29,28 @@ import time
 from dataclasses import dataclass, field
 from typing import List
 
-from .collectives import all_gather_floats
+from .collectives import all_gather_floats, max_over_ranks
 
 
 def clock_ns() -> int:
     """The node-wide monotonic clock every rank shares."""
     return time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+
+
+def aligned_start(ctx, margin_ns: int = 1_000_000) -> int:
+    """A common start instant for every rank: the latest rank's clock reading
+    plus ``margin_ns``, agreed with one all-reduce, then each rank spins on the
+    shared clock until it passes. A barrier's exit times differ by the host
+    wake-up latencies (tens of µs — a sizeable share of a 20-step window at
+    ~23 µs per step); this start differs by the spin's resolution. A rank that
+    learns the agreed instant only after it has passed starts late, and the
+    job span charges it. Returns this rank's start reading."""
+    if not getattr(ctx, "is_distributed", False):
+        return clock_ns()
+    t = max_over_ranks(float(clock_ns()), ctx) + margin_ns
+    while clock_ns() < t:
+        pass
+    return clock_ns()
 
 
 def start_delay(rank: int) -> float:

@@ -158,6 +158,9 @@ def test_job_span_charges_injected_start_skew():
         # value and ms_per_step come from the job span
         assert abs(r["ms_per_step"] * r["steps"] - r["job_span_ms"]) <= 1e-3 * r["job_span_ms"] + 1e-4
     assert rec["job_span_ms"] >= 300.0 and rec["start_skew_ms"] >= 295.0
+    # without the hook the ranks leave at one agreed instant (aligned_start): the
+    # skew is the spin's resolution plus scheduling noise, not barrier wake-ups
+    assert base["start_skew_ms"] < 20.0
     assert rec["max_rank_span_ms"] < 150.0  # no rank's own span holds the delay
     assert rec["value"] < base["value"] * (base["job_span_ms"] / 300.0)
 

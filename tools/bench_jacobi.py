@@ -26,7 +26,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cuda_mpi_openmp_amd.parallel.timing import clock_ns, gather_span, start_delay  # noqa: E402
+from cuda_mpi_openmp_amd.parallel.timing import aligned_start, clock_ns, gather_span, start_delay  # noqa: E402
 from cuda_mpi_openmp_amd import parallel  # noqa: E402
 from cuda_mpi_openmp_amd.models import SlabJacobi  # noqa: E402
 
@@ -81,6 +81,7 @@ def main() -> int:
         sol.run(a.warmup, graph=a.graph)
     sync()
     ctx.barrier()
+    aligned_start(ctx)  # every rank leaves at one agreed instant of the shared clock
     start_delay(ctx.rank)  # MPX_BENCH_START_DELAY test hook
     t0 = clock_ns()
     sol.run(a.iters, graph=a.graph)

@@ -25,7 +25,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cuda_mpi_openmp_amd import ops, parallel  # noqa: E402
-from cuda_mpi_openmp_amd.parallel.timing import clock_ns, gather_span, start_delay  # noqa: E402
+from cuda_mpi_openmp_amd.parallel.timing import aligned_start, clock_ns, gather_span, start_delay  # noqa: E402
 from cuda_mpi_openmp_amd.models import ShardedVectorSub, SlabPixelClassifier  # noqa: E402
 from cuda_mpi_openmp_amd.models.classifier import class_points_for  # noqa: E402
 
@@ -71,6 +71,7 @@ def main() -> int:
         step()
     sync()
     ctx.barrier()
+    aligned_start(ctx)  # every rank leaves at one agreed instant of the shared clock
     start_delay(ctx.rank)  # MPX_BENCH_START_DELAY test hook
     t0 = clock_ns()
     for _ in range(a.steps):
