@@ -103,3 +103,19 @@ ckpt_r5_hcmp2() {
 ckpt_r5_hcmp1() {
     timeout -k 10 1100 bash tools/harness_compare.sh lab1
 }
+
+# I: lab3 A/B after the host parameter cache (the uncached int8 bound search
+# made the back-to-back timing host-bound), then the stream-gap and the
+# per-dispatch clock experiments (E, F) in the same call.
+ckpt_r5_b2() {
+    export O=${O:-gpurun_out/r5/b2}
+    mkdir -p "$O"
+    for r in 1 2; do
+        LAB3_NCS=2,3,4,6,8,12,16,20,24,32 LAB3_PATHS=fast,mfma8 LAB3_TAG=r$r \
+            bash tools/gpu.sh run lab3_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done &&
+    MPX_CLS_MFMA8_SMALL=0 LAB3_NCS=4,8 LAB3_PATHS=mfma8 LAB3_TAG=old \
+        bash tools/gpu.sh run lab3_old 300 python -u tools/experiments/lab3_ab.py &&
+    O=$O/gap ckpt_r5_gap &&
+    O=$O/dclk ckpt_r5_dclk
+}
