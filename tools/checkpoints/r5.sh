@@ -119,3 +119,11 @@ ckpt_r5_b2() {
     O=$O/gap ckpt_r5_gap &&
     O=$O/dclk ckpt_r5_dclk
 }
+
+# J: the streaming layout: output row alignment against the input's
+ckpt_r5_gap2() {
+    export O=${O:-gpurun_out/r5/gap2}
+    mkdir -p "$O"
+    GAP_MODES=static,pingpong,static_outpad,pingpong_skew1,pingpong_skew2,pingpong_skew3,pingpong_skew4,pingpong_skew8 \
+        bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py
+}

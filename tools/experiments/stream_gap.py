@@ -15,7 +15,13 @@ timed in interleaved rounds so clock drift and allocation order cancel:
                   frame k - 2 read, never the one frame k - 1 read;
 * ``pingpong_rand`` ping-pong whose buffers are re-filled with random data
                   before each round (layout of the streaming phase, data of
-                  the static one).
+                  the static one);
+* ``static_outpad`` static, but the output rows written at the halo offset of
+                  a padded buffer (the input's row alignment, as in ping-pong);
+* ``pingpong_skewS`` ping-pong whose second buffer starts S rows (S x 16 KiB)
+                  later in its allocation than the first.
+
+GAP_MODES (comma list) picks the modes; GAP_ROUNDS the rounds.
 
 Prints one JSON line per (round, mode) and a summary (median µs per step).
 """
@@ -69,6 +75,19 @@ def main():
     for i in range(ROT):
         for b in pp[i] + tr[i] + ppr[i]:
             b.copy_(rand_in[i])
+    outpad = [padded() for _ in range(ROT)]
+    skews = (1, 2, 3, 4, 8)
+    skewed = {}
+    for S in skews:
+        bb = []
+        for i in range(ROT):
+            a = padded()
+            big = torch.empty((N + 2 * HALO + S, N, 4), dtype=torch.uint8, device=dev)
+            b = big[S:]
+            a.copy_(rand_in[i])
+            b.copy_(rand_in[i])
+            bb.append([a, b])
+        skewed[S] = bb
     torch.cuda.synchronize()
 
     L = {
@@ -77,7 +96,19 @@ def main():
         "pingpong": [[launcher(pp[i][a], pp[i][1 - a], HALO) for a in range(2)] for i in range(ROT)],
         "triple": [[launcher(tr[i][a], tr[i][(a + 1) % 3], HALO) for a in range(3)] for i in range(ROT)],
         "pingpong_rand": [[launcher(ppr[i][a], ppr[i][1 - a], HALO) for a in range(2)] for i in range(ROT)],
+        "static_outpad": [[launcher(rand_in[i], outpad[i], HALO)] for i in range(ROT)],
     }
+    for S in skews:
+        L[f"pingpong_skew{S}"] = [[launcher(skewed[S][i][a], skewed[S][i][1 - a], HALO) for a in range(2)]
+                                  for i in range(ROT)]
+    mod = 1 << 21  # where each buffer starts within a 2 MiB frame (the row offset a launch adds comes on top)
+    print(json.dumps({"base_mod_2MiB_KiB": {
+        "static_in": rand_in[0].data_ptr() % mod // 1024, "static_out": outs[0].data_ptr() % mod // 1024,
+        "pingpong": [b.data_ptr() % mod // 1024 for b in pp[0]],
+        **{f"skew{S}": [b.data_ptr() % mod // 1024 for b in skewed[S][0]] for S in skews}}}), flush=True)
+    want = [m for m in os.environ.get("GAP_MODES", "").split(",") if m]
+    if want:
+        L = {m: L[m] for m in want}
     k = {m: [0] * ROT for m in L}
 
     def run(mode, nsteps):
