@@ -47,14 +47,16 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``fast``   — fp32 packed-VALU distances;
       * ``mfma``   — fp32 MFMA distance GEMM (v_mfma_f32_32x32x2f32);
       * ``mfma64`` — fp64 MFMA distance GEMM (v_mfma_f64_16x16x4_f64);
-      * ``mfma8``  — exact int8 MFMA distance GEMM (v_mfma_i32_32x32x16_i8,
-        16-bit fixed-point weights in two int8 limbs, int32 keys);
-      * ``auto``   — ``mfma8`` at exactly 16 classes and from 21 (where it
-        measured faster on MI355X, round-4 sweep: 293-298 vs 298-300 us at
-        nc = 16, 345 vs 367-370 at nc = 21, 416-420 vs 520 at nc = 32,
-        8192^2), else ``fast`` (the f32 MFMA shares the VALU's fp32 datapath
-        on gfx950; the int8 path's ranking cost steps with the accumulator
-        registers it ranks, so fast32 wins below 16 and at 17-20).
+      * ``mfma8``  — exact int8 MFMA distance GEMM (16-bit fixed-point weights
+        in two int8 limbs, int32 keys): v_mfma_i32_32x32x16_i8 from 9
+        classes, and one pixel per lane on v_mfma_i32_4x4x4_16b_i8 below;
+      * ``auto``   — ``mfma8`` below 9 classes, at exactly 16 and from 20
+        (where it measured faster on MI355X, round-5 sweep at 8192^2, median
+        µs: nc = 4 128 vs 134, 8 176 vs 188, 16 280-283 vs 295-303, 20
+        341 vs 352, 32 407-413 vs 510-517), else ``fast`` (the f32 MFMA
+        shares the VALU's fp32 datapath on gfx950; the 32x32 int8 form's
+        ranking cost steps with the accumulator registers it ranks, so fast32
+        wins at 9-15 and 17-19).
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes

@@ -1330,18 +1330,19 @@ int classify_choose(int nc, int path, bool fast_ok) {
 }
 
 // AUTO runs MFMA8 (its statistics permitting) where it measured faster than
-// FAST32: exactly 16 classes (accumulator registers 0-7 all real) and from 21
-// up. Round 4 (fast32 interleaved chains, mfma8 fp32 re-rank stage), same box,
+// FAST32. Round 5 (the one-pixel-per-lane 4x4x4 form below 9 classes, the
+// int8 bound from the actual weight rounding, host parameter cache), one box,
 // 8192^2, three rotated images, two runs each, median µs
-// (profiles/raw/r4/r/, profiles/lab3_classify.md):
-//   nc      8        12       15       16       17       19       20       21       22       24       32
-//   fast  191-192  239-245  288-289  298-300  315-316  346-347  353-358  367-370  383-385  410      520
-//   mfma8 234-244  286-293  293-300  293-298  348-349  353-355  351-354  345-346  354-368  356-359  416-420
-// MFMA8's ranking cost steps with the accumulator registers it must rank
-// (8 for <= 16 classes, 12 for <= 24, 16 for <= 32), FAST32's grows
-// linearly; nc = 20 is a tie and stays on FAST32.
-constexpr int kAutoMfma8MinClasses = 21;
-inline bool auto_mfma8(int nc) { return nc == 16 || nc >= kAutoMfma8MinClasses; }
+// (profiles/raw/r5/b2/, profiles/lab3_classify.md):
+//   nc      2        3        4        6        8        12       16       20       24       32
+//   fast  132-139  127-128  134      162-166  188-189  241-245  295-303  352-353  402-410  510-517
+//   mfma8 123-128  126      128-129  149-153  176      277-281  280-283  341-342  340-341  407-413
+// The 4x4x4 form's cost grows with its row sets (two classes each), the
+// 32x32 form's with its ranked accumulator registers (8 for <= 16 classes,
+// 12 for <= 24, 16 for <= 32) and FAST32's linearly: MFMA8 below 9 classes,
+// at exactly 16 and from 20 (nc = 12 and, round 4, 17-19 stay on FAST32).
+constexpr int kAutoMfma8MinClasses = 20;
+inline bool auto_mfma8(int nc) { return nc <= 8 || nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.

@@ -140,15 +140,19 @@ def test_classify_plan_routes():
         return ops.class_stats(img, [rng.integers(0, 64, (30, 2)) for _ in range(nc)])
 
     mu, inv = stats(4)
+    # below 9 classes AUTO runs the one-pixel-per-lane int8 MFMA form (round 5)
     path, margin = ops.classify_plan(mu, inv, "auto")
-    assert path == "fast" and 0 < margin < 1e-2
+    assert path == "mfma8" and margin >= 1
+    assert ops.classify_plan(mu, inv, "fast")[0] == "fast" and 0 < ops.classify_plan(mu, inv, "fast")[1] < 1e-2
     assert ops.classify_plan(mu, inv, "mfma")[0] == "mfma"
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
     mu20, inv20 = stats(20)
-    assert ops.classify_plan(mu20, inv20, "auto")[0] == "fast"
+    assert ops.classify_plan(mu20, inv20, "auto")[0] == "mfma8"
+    mu19, inv19 = stats(19)
+    assert ops.classify_plan(mu19, inv19, "auto")[0] == "fast"
     mu14, inv14 = stats(14)
     assert ops.classify_plan(mu14, inv14, "auto")[0] == "fast"
-    # at exactly 16 and from 21 classes AUTO runs the exact int8-MFMA distance
+    # at exactly 16 and from 20 classes AUTO runs the exact int8-MFMA distance
     # GEMM (measured faster there; margin in key units)
     mu16, inv16 = stats(16)
     assert ops.classify_plan(mu16, inv16, "auto")[0] == "mfma8"
