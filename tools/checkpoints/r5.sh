@@ -127,3 +127,11 @@ ckpt_r5_gap2() {
     GAP_MODES=static,pingpong,static_outpad,pingpong_skew1,pingpong_skew2,pingpong_skew3,pingpong_skew4,pingpong_skew8 \
         bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py
 }
+
+# K: the streaming gap vs the load policy (NT interior loads vs plain)
+ckpt_r5_gap3() {
+    export O=${O:-gpurun_out/r5/gap3}
+    mkdir -p "$O"
+    GAP_MODES=static,pingpong,static_plain,pingpong_plain,triple \
+        bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py
+}

@@ -19,7 +19,9 @@ timed in interleaved rounds so clock drift and allocation order cancel:
 * ``static_outpad`` static, but the output rows written at the halo offset of
                   a padded buffer (the input's row alignment, as in ping-pong);
 * ``pingpong_skewS`` ping-pong whose second buffer starts S rows (S x 16 KiB)
-                  later in its allocation than the first.
+                  later in its allocation than the first;
+* ``static_plain`` / ``pingpong_plain``: those layouts with plain loads of
+                  every row instead of the default non-temporal interior loads.
 
 GAP_MODES (comma list) picks the modes; GAP_ROUNDS the rounds.
 
@@ -98,6 +100,15 @@ def main():
         "pingpong_rand": [[launcher(ppr[i][a], ppr[i][1 - a], HALO) for a in range(2)] for i in range(ROT)],
         "static_outpad": [[launcher(rand_in[i], outpad[i], HALO)] for i in range(ROT)],
     }
+    # the same layouts with plain loads of every row (the resident-input policy,
+    # OPT 2) instead of non-temporal loads of the rows no neighbour re-reads
+    pl = {"static_plain": [[launcher(rand_in[i], outs[i], 0)] for i in range(ROT)],
+          "pingpong_plain": [[launcher(pp[i][a], pp[i][1 - a], HALO) for a in range(2)] for i in range(ROT)]}
+    for ls in pl.values():
+        for row in ls:
+            for ln in row:
+                ln.resident = True
+    L.update(pl)
     for S in skews:
         L[f"pingpong_skew{S}"] = [[launcher(skewed[S][i][a], skewed[S][i][1 - a], HALO) for a in range(2)]
                                   for i in range(ROT)]
