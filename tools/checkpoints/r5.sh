@@ -135,3 +135,20 @@ ckpt_r5_gap3() {
     GAP_MODES=static,pingpong,static_plain,pingpong_plain,triple \
         bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py
 }
+
+# L: the job-span accounting on the one-GPU rehearsal (VERDICT r4 Next #1):
+# the driver's bench command at 2 and 4 ranks sharing the GPU (gloo control
+# plane, peer halos), Jacobi and lab1 at 2 / 4 ranks; every JSON carries
+# job_span_ms, max_rank_span_ms and the start / end skews.
+ckpt_r5_scale() {
+    export O=${O:-gpurun_out/r5/scale}
+    mkdir -p "$O"
+    export MPX_DIST_BACKEND=gloo
+    for n in 2 4; do
+        bash tools/gpu.sh run bench$n 400 python bench.py --gpus $n --steps 20 --warmup 5 --no-cpu-baseline &&
+        bash tools/gpu.sh run jacobi$n 300 python -u tools/bench_jacobi.py --gpus $n --halo peer --iters 200 \
+            --warmup 20 &&
+        bash tools/gpu.sh run vsub$n 300 python -u tools/bench_workloads.py --workload vsub --gpus $n --steps 50 \
+            --warmup 5 || return 1
+    done
+}
