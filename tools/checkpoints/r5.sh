@@ -132,7 +132,7 @@ ckpt_r5_gap2() {
 ckpt_r5_gap3() {
     export O=${O:-gpurun_out/r5/gap3}
     mkdir -p "$O"
-    GAP_MODES=static,pingpong,static_plain,pingpong_plain,triple \
+    GAP_MODES=static,pingpong,static_plain,pingpong_plain,static_m1,pingpong_m1 \
         bash tools/gpu.sh run stream_gap 300 python -u tools/experiments/stream_gap.py
 }
 

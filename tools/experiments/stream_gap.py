@@ -21,7 +21,8 @@ timed in interleaved rounds so clock drift and allocation order cancel:
 * ``pingpong_skewS`` ping-pong whose second buffer starts S rows (S x 16 KiB)
                   later in its allocation than the first;
 * ``static_plain`` / ``pingpong_plain``: those layouts with plain loads of
-                  every row instead of the default non-temporal interior loads.
+                  every row instead of the default non-temporal interior loads;
+* ``static_m1`` / ``pingpong_m1``: band mode 1 — plain output stores too.
 
 GAP_MODES (comma list) picks the modes; GAP_ROUNDS the rounds.
 
@@ -109,6 +110,12 @@ def main():
             for ln in row:
                 ln.resident = True
     L.update(pl)
+    # band mode 1 (plain output stores and plain loads; mpx_conv_set_band_mode):
+    # the same launchers, the mode switched around their runs
+    L["static_m1"] = L["static"]
+    L["pingpong_m1"] = [[launcher(pp[i][a], pp[i][1 - a], HALO) for a in range(2)] for i in range(ROT)]
+    from cuda_mpi_openmp_amd import _native
+    NL = _native.lib()
     for S in skews:
         L[f"pingpong_skew{S}"] = [[launcher(skewed[S][i][a], skewed[S][i][1 - a], HALO) for a in range(2)]
                                   for i in range(ROT)]
@@ -141,11 +148,14 @@ def main():
                     for b in ppr[i]:
                         b.copy_(rand_in[i])
                 torch.cuda.synchronize()
+            prev = NL.mpx_conv_set_band_mode(1) if mode.endswith("_m1") else None
             run(mode, W)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             run(mode, K)
             torch.cuda.synchronize()
+            if prev is not None:
+                NL.mpx_conv_set_band_mode(prev)
             us = (time.perf_counter() - t0) * 1e6 / K
             res[mode].append(us)
             print(json.dumps({"round": rnd, "mode": mode, "us_per_step": round(us, 3)}), flush=True)
