@@ -999,7 +999,10 @@ __device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane &L
 // re-read from the image after the loop: their RGB bytes are untouched.
 constexpr int kAmb8sCap = 1024;
 
-template <int NS>
+// PF: trips of loads in flight (1: the next trip's 16 B under this trip's
+// ranking; 2: two register sets in fixed roles, the trip after next issued
+// before this one is ranked — twice the bytes in flight per lane)
+template <int NS, int PF = 1>
 __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, I8Params ip, FastParams fp,
                                                               uint32_t *amb) {
@@ -1012,10 +1015,7 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
     uint4 *v = reinterpret_cast<uint4 *>(img);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint4 qn = i < nvec ? v[i] : uint4{};
-    for (; i < nvec; i += stride) {
-        const uint4 q = qn;
-        if (i + stride < nvec) qn = v[i + stride];
+    auto trip = [&](const uint4 q, int64_t vi) {
         const uint32_t px[4] = {q.x, q.y, q.z, q.w};
         uint32_t o[4];
         bool u[4];
@@ -1027,14 +1027,39 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
             const uint32_t mask = (uint32_t)u[0] | ((uint32_t)u[1] << 1) | ((uint32_t)u[2] << 2) | ((uint32_t)u[3] << 3);
             const uint32_t slot = atomicAdd(&s_namb, 1u);
             if (slot < (uint32_t)kAmb8sCap) {
-                s_amb[slot] = (i << 4) | mask;
+                s_amb[slot] = (vi << 4) | mask;
             } else {  // list full: the exact chain inline (never at the benchmark's rates)
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
                     if ((mask >> m) & 1u) o[m] = classify_direct(px[m], nc, cp);
             }
         }
-        v[i] = make_uint4(o[0], o[1], o[2], o[3]);
+        v[vi] = make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    if constexpr (PF == 2) {
+        uint4 qa = i < nvec ? v[i] : uint4{};
+        uint4 qb = i + stride < nvec ? v[i + stride] : uint4{};
+        while (i < nvec) {
+            {
+                const uint4 q = qa;
+                if (i + 2 * stride < nvec) qa = v[i + 2 * stride];
+                trip(q, i);
+            }
+            if ((i += stride) >= nvec) break;
+            {
+                const uint4 q = qb;
+                if (i + 2 * stride < nvec) qb = v[i + 2 * stride];
+                trip(q, i);
+            }
+            i += stride;
+        }
+    } else {
+        uint4 qn = i < nvec ? v[i] : uint4{};
+        for (; i < nvec; i += stride) {
+            const uint4 q = qn;
+            if (i + stride < nvec) qn = v[i + stride];
+            trip(q, i);
+        }
     }
     // the deferred pixels: the fp32 proven-margin ranking first, the exact fp64
     // chain for what it leaves (as in MFMA8, every lane busy in each stage)
@@ -1457,14 +1482,27 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256)
                                    : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
             const int ns = (nc + 1) / 2;
+            // MPX_CLS_MFMA8S_PF=2: two trips of loads in flight (A/B; read once)
+            static const int pf = [] {
+                const char *e = std::getenv("MPX_CLS_MFMA8S_PF");
+                return (e && e[0] == '2') ? 2 : 1;
+            }();
+#define MPX_MFMA8S(NS)                                                                                             \
+    do {                                                                                                           \
+        if (pf == 2)                                                                                               \
+            hipLaunchKernelGGL((classify_mfma8s_kernel<NS, 2>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb); \
+        else                                                                                                       \
+            hipLaunchKernelGGL((classify_mfma8s_kernel<NS, 1>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb); \
+    } while (0)
             if (ns == 1)
-                hipLaunchKernelGGL(classify_mfma8s_kernel<1>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+                MPX_MFMA8S(1);
             else if (ns == 2)
-                hipLaunchKernelGGL(classify_mfma8s_kernel<2>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+                MPX_MFMA8S(2);
             else if (ns == 3)
-                hipLaunchKernelGGL(classify_mfma8s_kernel<3>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+                MPX_MFMA8S(3);
             else
-                hipLaunchKernelGGL(classify_mfma8s_kernel<4>, dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb);
+                MPX_MFMA8S(4);
+#undef MPX_MFMA8S
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             done = nvec * 4;
         }

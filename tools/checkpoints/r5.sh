@@ -152,3 +152,28 @@ ckpt_r5_scale() {
             --warmup 5 || return 1
     done
 }
+
+# M: frames in flight — the driver's bench command with 2 / 3 / 6 streams,
+# alternated twice (is 2 still the best overlap?)
+ckpt_r5_streams() {
+    export O=${O:-gpurun_out/r5/streams}
+    mkdir -p "$O"
+    for r in 1 2; do
+        for s in 2 3 6; do
+            bash tools/gpu.sh run bench_s${s}_$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 --streams $s \
+                --no-cpu-baseline --no-stream --no-warm || return 1
+        done
+    done
+}
+
+# N: mfma8s loads in flight: one vs two trips ahead (MPX_CLS_MFMA8S_PF), nc 2-8
+ckpt_r5_pf() {
+    export O=${O:-gpurun_out/r5/pf}
+    mkdir -p "$O"
+    for r in 1 2; do
+        for pf in 1 2; do
+            MPX_CLS_MFMA8S_PF=$pf LAB3_NCS=2,3,4,6,8 LAB3_PATHS=mfma8 LAB3_TAG=pf${pf}_$r \
+                bash tools/gpu.sh run lab3_pf${pf}_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+        done
+    done
+}
