@@ -60,6 +60,33 @@ for d in sorted(glob.glob(os.path.join(root, "*", "lab*"))):
             rows.append({"lab": lab, "size": size, "timing": timing, "device": dev, "geometry": ks,
                          "median_ms": g["time_kernel_exe_ms"].median(), "runs": len(g)})
 out = pd.DataFrame(rows)
+# published GPU/CPU speedups (BASELINE.md derived rows: CPU median / best GPU median)
+PUBLISHED_SPEEDUP = {("lab2", "large"): 212.0, ("lab2", "medium"): 101.0, ("lab2", "small"): 0.006,
+                     ("lab1", "1000000"): 62.0}
+if "--speedups" in sys.argv:
+    print("| lab | bucket / n | CPU median ms (serial -O0, this host) | best MI355X median ms cold / warm (geometry) "
+          "| speedup cold / warm | published (RTX A6000 vs Xeon, cold) |")
+    print("|---|---|---|---|---|---|")
+    for (lab, size), g in out.groupby(["lab", "size"], sort=False):
+        cpu = g[g.device.str.startswith("CPU")]
+        gpu = g[~g.device.str.startswith("CPU")]
+        if cpu.empty or gpu.empty:
+            continue
+        cells = []
+        for timing in ("cold", "warm"):
+            c = cpu[cpu.timing == timing].median_ms
+            gg = gpu[gpu.timing == timing]
+            if c.empty or gg.empty:
+                cells.append(None)
+                continue
+            best = gg.loc[gg.median_ms.idxmin()]
+            cells.append((float(c.iloc[0]), float(best.median_ms), best.geometry))
+        cpu_ms = "/".join(f"{x[0]:.4g}" for x in cells if x)
+        gpu_ms = " / ".join(f"{x[1]:.5f} ({x[2]})" for x in cells if x)
+        sp = " / ".join(f"**{x[0] / x[1]:.1f}x**" for x in cells if x)
+        pub = PUBLISHED_SPEEDUP.get((lab, size))
+        print(f"| {lab} | {size} | {cpu_ms} | {gpu_ms} | {sp} | {str(pub) + 'x' if pub else '—'} |")
+    sys.exit(0)
 if "--vs-baseline" in sys.argv:
     out["geometry"] = [("CPU" if d.startswith("CPU") else g) for d, g in zip(out.device, out.geometry)]
     vs_baseline(out)
