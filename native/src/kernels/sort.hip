@@ -41,6 +41,7 @@
 //     never share scratch.
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 
 #include "internal.hpp"
 #include "mpx/tuning.h"
@@ -279,6 +280,8 @@ constexpr int kRWaves = kRThreads / 64;
 constexpr int kRPer = 16;                      // keys per thread
 constexpr int kRTile = kRThreads * kRPer;      // 8192 keys per tile
 constexpr int kRWaveKeys = kRTile / kRWaves;   // 1024 contiguous keys per wave
+constexpr int kHotMax = 4;                     // RANK 3: hot digits ranked by ballot (RANK 4: 2)
+constexpr int kHotShare = 16;                  // hot: at least 1 / kHotShare of the keys
 constexpr uint32_t kFlagA = 1u << 30;          // tile aggregate published
 constexpr uint32_t kFlagP = 2u << 30;          // inclusive prefix published
 constexpr uint32_t kCountMask = (1u << 30) - 1;
@@ -747,6 +750,20 @@ __device__ __forceinline__ uint32_t from_key_t(uint32_t k) { return from_key(k, 
 // that order would scramble keys equal in this digit and already ordered by
 // the lower ones, which the GPU sort suite's uniform, few-distinct, sorted and
 // reversed inputs (every variant, 4097 .. 2^26 keys) would catch.
+// RANK 3 / 4 (variants 18 / 19 and 20 / 21, AUTO): RANK 1 plus hot digits
+// ranked without LDS. A digit holding at least 1/kHotShare of the pass's keys
+// (tot[], known before the pass) puts many lanes of one returning add on one
+// counter, and those lanes serialise (the float32 top byte: 28.1M conflict
+// cycles against 15.2M for uniform digits, 136 vs 120 us; small-range ints:
+// every lane on one counter). The largest kHotMax (RANK 3) or 2 (RANK 4) such
+// digits keep a wave-uniform count in scalar registers instead: one compare
+// mask per hot digit per slice, rank = count + lanes below in the mask; the
+// remaining lanes take the returning add as before. The order is the same
+// (slice-major, lane-minor), so the pass stays stable. A pass without hot
+// digits (uniform data) runs the RANK 1 loop: the tile loop is instantiated
+// twice and the block picks one. Per 2^26-key float32 last pass
+// (profiles/lab5_sort.md): RANK 1 135.9 us, RANK 3 118.6 (8.3M conflicts,
+// 35.8M VALU), RANK 4 114.2 (16.0M, 25.2M VALU).
 // KNOCK (tuning probe, mpx_sort_scatter_probe; output NOT sorted): bit 1 stages
 // at lane-linear positions, 2 skips the counter read, 4 the leaders' add, 8 the
 // peer-mask table (own-lane masks), 16 the write-out's digit lookup — same
@@ -796,7 +813,44 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t *tbl = s_tbl + w * 512;
     uint32_t *const myword = tbl + (lane >> 5);
     const uint32_t mybit = 1u << (lane & 31);
-    const uint32_t dbase = scan256_excl_lds(t < 256 ? tot[t] : 0u, s_wsum);  // + the barrier after the zeroing
+    const uint32_t mytot = t < 256 ? tot[t] : 0u;
+    const uint32_t dbase = scan256_excl_lds(mytot, s_wsum);  // + the barrier after the zeroing
+    // RANK 3 / 4: the pass's hot digits, the HN largest (ties: lower digit
+    // first) of those with at least 1/kHotShare of the keys — at most
+    // kHotShare candidates; once per block
+    constexpr bool HOT = RANK == 3 || RANK == 4;
+    constexpr int HN = RANK == 4 ? 2 : kHotMax;  // hot-digit slots
+    int nh = 0;
+    uint32_t hd[HN] = {};
+    if constexpr (HOT) {
+        __shared__ uint32_t s_hotc[4], s_cd[kHotShare], s_cc[kHotShare], s_hd[HN];
+        const bool hot = t < 256 && (uint64_t)mytot * kHotShare >= (uint64_t)n;
+        const uint64_t hm = __builtin_amdgcn_ballot_w64(hot);
+        if (t < 256 && lane == 0) s_hotc[w] = (uint32_t)__popcll(hm);
+        lds_barrier();
+        uint32_t pos = lanes_below(hm), all = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const uint32_t c = s_hotc[ww];
+            pos += ww < w ? c : 0u;
+            all += c;
+        }
+        if (hot) {  // pos < kHotShare: the candidates hold more than all keys otherwise
+            s_cd[pos] = (uint32_t)t;
+            s_cc[pos] = mytot;
+        }
+        lds_barrier();
+        if (hot) {
+            uint32_t order = 0;
+            for (uint32_t c = 0; c < all; ++c)
+                order += s_cc[c] > mytot || (s_cc[c] == mytot && s_cd[c] < (uint32_t)t);
+            if (order < (uint32_t)HN) s_hd[order] = (uint32_t)t;
+        }
+        lds_barrier();
+        nh = (int)__builtin_amdgcn_readfirstlane(all < (uint32_t)HN ? all : (uint32_t)HN);
+#pragma unroll
+        for (int j = 0; j < HN; ++j) hd[j] = j < nh ? __builtin_amdgcn_readfirstlane(s_hd[j]) : 256u;
+    }
 
     // whole tiles: one offset register (tile base + lane), slices in the
     // immediate field; the partial last tile (block-uniform) loads and stores
@@ -822,7 +876,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
             }
         }
     };
-    auto do_tile = [&](uint32_t (&key)[kRPer], int ptile) {
+    // HOTP (RANK 3 / 4 with hot digits in this pass): a separate instance of the
+    // tile loop, so a pass without hot digits runs RANK 1's code unchanged
+    auto do_tile = [&](uint32_t (&key)[kRPer], int ptile, auto hotp) {
+        constexpr bool HOTP = decltype(hotp)::value;
         // s_cnt and the tables are zero here (kernel start / previous write-out)
         const uint32_t excl = t < 256 ? offs[(size_t)t * ntiles + ptile] : 0u;
         const int64_t tile0 = (int64_t)ptile * TILE;
@@ -836,7 +893,37 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 if (i0 + e * kSlice >= n32) key[e] = 0xffffffffu;
         }
         uint32_t rank[kRPer];
-        if constexpr (RANK >= 1) {
+        if constexpr (HOTP) {
+            // every slot is compared (unused slots hold 256, which no digit
+            // matches): straight-line code keeps the counts in scalar registers
+            uint32_t hc[HN] = {};  // wave-uniform counts of the hot digits
+#pragma unroll
+            for (int e = 0; e < kRPer; ++e) {
+                const uint32_t d = (key[e] >> shift) & 255u;
+                uint32_t r = 0;
+                bool hit = false;
+#pragma unroll
+                for (int j = 0; j < HN; ++j) {
+                    const bool is = d == hd[j];
+                    const uint64_t m = __builtin_amdgcn_uicmp(d, hd[j], 32);  // ICMP_EQ: the compare's lane mask
+                    // hc[j] + the lanes below in m: mbcnt accumulates onto its operand
+                    const uint32_t rj =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, hc[j]));
+                    r = is ? rj : r;
+                    hc[j] += (uint32_t)__popcll(m);
+                    hit = hit || is;
+                }
+                if (!hit) r = atomicAdd(&s_cnt[crow][d], 1u);
+                rank[e] = r;
+            }
+            // no returning add touched a hot digit's counter
+            if (lane == 0) {
+                const int wrow = __builtin_amdgcn_readfirstlane(crow);  // scalar addresses: no VGPRs held for them
+#pragma unroll
+                for (int j = 0; j < HN; ++j)
+                    if (j < nh) s_cnt[wrow][hd[j]] = hc[j];
+            }
+        } else if constexpr (RANK >= 1) {
 #pragma unroll
             for (int e = 0; e < kRPer; ++e) rank[e] = atomicAdd(&s_cnt[crow][(key[e] >> shift) & 255u], 1u);
         } else {
@@ -920,33 +1007,43 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
     };
 
-    if constexpr (PF == 2) {
-        // two tiles in flight: three register sets in fixed roles (an
-        // unrolled rotation — a copy between sets would wait for the copied
-        // loads and shorten the prefetch back to one tile)
-        uint32_t a[kRPer], b[kRPer], c[kRPer];
-        load_tile(a, tile);
-        if (tile + per < t1) load_tile(b, tile + per);
-        for (;;) {
-            if (tile + 2 * per < t1) load_tile(c, tile + 2 * per);
-            do_tile(a, tile);
-            if ((tile += per) >= t1) break;
-            if (tile + 2 * per < t1) load_tile(a, tile + 2 * per);
-            do_tile(b, tile);
-            if ((tile += per) >= t1) break;
-            if (tile + 2 * per < t1) load_tile(b, tile + 2 * per);
-            do_tile(c, tile);
-            if ((tile += per) >= t1) break;
-        }
-    } else {
-        uint32_t a[kRPer], b[kRPer];
-        load_tile(a, tile);
-        for (; tile < t1; tile += per) {
-            if (tile + per < t1) load_tile(b, tile + per);  // in flight under this tile's work
-            do_tile(a, tile);
+    auto run_tiles = [&](auto hotp) {
+        if constexpr (PF == 2) {
+            // two tiles in flight: three register sets in fixed roles (an
+            // unrolled rotation — a copy between sets would wait for the copied
+            // loads and shorten the prefetch back to one tile)
+            uint32_t a[kRPer], b[kRPer], c[kRPer];
+            load_tile(a, tile);
+            if (tile + per < t1) load_tile(b, tile + per);
+            for (;;) {
+                if (tile + 2 * per < t1) load_tile(c, tile + 2 * per);
+                do_tile(a, tile, hotp);
+                if ((tile += per) >= t1) break;
+                if (tile + 2 * per < t1) load_tile(a, tile + 2 * per);
+                do_tile(b, tile, hotp);
+                if ((tile += per) >= t1) break;
+                if (tile + 2 * per < t1) load_tile(b, tile + 2 * per);
+                do_tile(c, tile, hotp);
+                if ((tile += per) >= t1) break;
+            }
+        } else {
+            uint32_t a[kRPer], b[kRPer];
+            load_tile(a, tile);
+            for (; tile < t1; tile += per) {
+                if (tile + per < t1) load_tile(b, tile + per);  // in flight under this tile's work
+                do_tile(a, tile, hotp);
 #pragma unroll
-            for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+                for (int e = 0; e < kRPer; ++e) a[e] = b[e];
+            }
         }
+    };
+    if constexpr (HOT) {
+        if (nh > 0)  // block-uniform
+            run_tiles(std::true_type{});
+        else
+            run_tiles(std::false_type{});
+    } else {
+        run_tiles(std::false_type{});
     }
 }
 
@@ -1144,6 +1241,18 @@ constexpr int kCThreads = 256;
 // VEC (16-B aligned input, whole tile in range): counting ignores order, so
 // each lane reads 16-B pieces (8 loads of 1 KiB per wave instead of 32 of
 // 256 B); the partial last tile keeps the 4-B form.
+// One key per lane into the wave's histogram row. The lanes holding the first
+// active lane's digit add through that lane alone (one add of their count): a
+// pass whose digits are skewed (one value for small-range ints, a few for
+// floats' top byte) otherwise serialises up to 32 same-address lanes per add.
+__device__ __forceinline__ void count_add(uint32_t *hw, uint32_t d) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    const bool is = d == d0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(is);
+    const bool lead = (int)(threadIdx.x & 63) == __builtin_ctzll(m);  // the first active lane
+    if (!is || lead) atomicAdd(&hw[d], is ? (uint32_t)__popcll(m) : 1u);
+}
+
 template <bool VEC, int TILE>
 __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in, int64_t n, int shift, int mode,
                                                 int tile, uint32_t *hw) {
@@ -1157,10 +1266,10 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
         for (int e = 0; e < kCPer / 4; ++e) q[e] = src[e * 64];
 #pragma unroll
         for (int e = 0; e < kCPer / 4; ++e) {
-            atomicAdd(&hw[(to_key(q[e].x, mode) >> shift) & 255u], 1u);
-            atomicAdd(&hw[(to_key(q[e].y, mode) >> shift) & 255u], 1u);
-            atomicAdd(&hw[(to_key(q[e].z, mode) >> shift) & 255u], 1u);
-            atomicAdd(&hw[(to_key(q[e].w, mode) >> shift) & 255u], 1u);
+            count_add(hw, (to_key(q[e].x, mode) >> shift) & 255u);
+            count_add(hw, (to_key(q[e].y, mode) >> shift) & 255u);
+            count_add(hw, (to_key(q[e].z, mode) >> shift) & 255u);
+            count_add(hw, (to_key(q[e].w, mode) >> shift) & 255u);
         }
     } else {
         const int64_t base = (int64_t)tile * TILE + w * kWaveKeys + lane;
@@ -1172,7 +1281,7 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
         }
 #pragma unroll
         for (int e = 0; e < kCPer; ++e)
-            if (base + e * 64 < n) atomicAdd(&hw[(to_key(key[e], mode) >> shift) & 255u], 1u);
+            if (base + e * 64 < n) count_add(hw, (to_key(key[e], mode) >> shift) & 255u);
     }
 }
 
@@ -1325,7 +1434,9 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // onesweep (one histogram read, then decoupled look-back per digit pass):
 // correct, and 1.2 ms at 2^26 against 0.70 (profiles/lab5_sort.md); 15 / 16 its
 // one-block-per-CU and static-order experiments; 17 = 12 with one counter row
-// per half-wave (RANK 2: skewed digits contend half as much). Retired after round-3
+// per half-wave (RANK 2: skewed digits contend half as much); 18 / 19 = 12 / 13
+// with up to four hot digits ranked by ballot (RANK 3), 20 / 21 the same with
+// two (RANK 4). Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1359,7 +1470,7 @@ void launch_lean(int p, int mode, int blocks, hipStream_t s, const uint32_t *src
 }
 
 // Lane order of same-address returning LDS adds. The RANK >= 1
-// scatters (variants 9-17, AUTO above 2^18 keys) are stable only because one
+// scatters (variants 9-21, AUTO above 2^18 keys) are stable only because one
 // ds_add_rtn_u32 applies its same-address lanes in ascending lane order —
 // observed on gfx950, not promised by the ISA. This probe checks it once per
 // device before the first such sort: four waves, three address patterns
@@ -1424,18 +1535,19 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // vs 0.229) and lose at 2^26 (0.987 vs 0.828; not yet explained — a
     // candidate: with 16 tiles per block the 64-B digit runs of neighbouring
     // tiles stop meeting in L2; profiles/lab5_sort.md)
-    // AUTO (round 4, profiles/lab5_sort.md): the returning-add ranking with
-    // two tiles of keys in flight, on 4096-key tiles up to 2^23 keys (13),
-    // on 8192-key tiles above (12)
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 13 : 12;
+    // AUTO (round 5, profiles/lab5_sort.md): the returning-add ranking with
+    // two tiles of keys in flight and the two hottest digits of a skewed pass
+    // ranked by ballot (RANK 4), on 4096-key tiles up to 2^23 keys (21), on
+    // 8192-key tiles above (20); uniform passes run the round-4 code (12 / 13)
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 21 : 20;
     // the returning-add ranking needs ascending lane order (probe above)
-    const bool rtn_rank = (variant >= 9 && variant <= 17);
+    const bool rtn_rank = (variant >= 9 && variant <= 21);
     if (rtn_rank && lds_rtn_order_ok(s) != 1) {
         if (!auto_variant) return MPX_ERR_UNSUPPORTED;
         variant = n <= kTile4kMaxN ? 8 : 7;
     }
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
-    const bool small_tiles = variant == 8 || variant == 10 || variant == 13;
+    const bool small_tiles = variant == 8 || variant == 10 || variant == 13 || variant == 19 || variant == 21;
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
     const bool onesweep = variant >= 14 && variant <= 16;
     if (variant == 1 || onesweep) {
@@ -1526,6 +1638,18 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                                                     r.status, ntiles);
                 else if (variant == 13)  // 10 with two tiles of keys in flight
                     launch_lean<kRThreads / 2, 1, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
+                                                        r.hist, r.status, ntiles);
+                else if (variant == 18)  // 12 with hot digits ranked by ballot (RANK 3)
+                    launch_lean<kRThreads, 3, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
+                                                    r.status, ntiles);
+                else if (variant == 19)  // 13 with hot digits ranked by ballot
+                    launch_lean<kRThreads / 2, 3, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
+                                                        r.hist, r.status, ntiles);
+                else if (variant == 20)  // 18 with two hot-digit slots (RANK 4)
+                    launch_lean<kRThreads, 4, 4, 2>(p, mode, std::min(kNumCUs * 2, rounded), s, src, dst, n, r.hist,
+                                                    r.status, ntiles);
+                else if (variant == 21)  // 19 with two hot-digit slots
+                    launch_lean<kRThreads / 2, 4, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
                                                         r.hist, r.status, ntiles);
                 else
                     launch_lean<kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
@@ -1724,8 +1848,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 17 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 17", variant);
+    if (variant < 0 || variant > 21 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 21", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);

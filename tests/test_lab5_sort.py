@@ -260,7 +260,7 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 @pytest.mark.parametrize("kind", ["int", "float"])
 @pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
@@ -280,6 +280,47 @@ def test_gpu_radix_variants(gpu, variant, kind, n):
     _native.check(L.mpx_sort_variant(d.data_ptr(), n, dt, ws.data_ptr(), nb, variant, _native.stream_of(d)))
     assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
     _native.check(L.mpx_sort_ws_status(ws.data_ptr(), n, dt))  # no look-back wait gave up
+
+
+def skewed_array(kind, n, seed):
+    """Digit distributions with hot digits (at least 1/32 of the keys on one
+    digit value in some pass): what RANK 3 ranks by ballot."""
+    rng = np.random.default_rng(seed)
+    if kind == "float_normal":  # top byte: a handful of sign / exponent values
+        return rng.standard_normal(n).astype(np.float32)
+    if kind == "float_unit":  # [0, 1): top byte 0x3f / 0x3e / ... (few), the rest uniform
+        return rng.random(n, dtype=np.float32)
+    if kind == "int_range":  # passes 2 and 3: one digit; pass 1: four
+        return rng.integers(0, 1000, n, dtype=np.int64).astype(np.int32)
+    if kind == "int_mix":  # 60 % one value, the rest uniform: one hot digit in every pass
+        a = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+        a[rng.random(n) < 0.6] = 0x12345678
+        return a
+    # "int_many_hot": eight top bytes of 1/8 each — more hot digits than
+    # kHotMax, so four take ballots and four the returning add in one pass
+    hi = rng.integers(0, 8, n, dtype=np.int64) * 29 + 3
+    return ((hi << 24) | rng.integers(0, 1 << 24, n, dtype=np.int64)).astype(np.uint32).view(np.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [12, 13, 18, 19, 20, 21])
+@pytest.mark.parametrize("kind", ["float_normal", "float_unit", "int_range", "int_mix", "int_many_hot"])
+@pytest.mark.parametrize("n", [8193, (1 << 20) + 7, (1 << 23) + 5])
+def test_gpu_radix_variants_skewed_digits(gpu, variant, kind, n):
+    """Hot digits: the returning-add ranking (12 / 13) serialises same-address
+    lanes, RANK 3 (18 / 19) ranks up to four hot digits per pass by ballot and
+    the rest by returning adds. Both must stay stable (the lower passes' order
+    survives every later pass) — checked against the total order."""
+    from cuda_mpi_openmp_amd import _native
+
+    L = _native.lib()
+    a = skewed_array(kind, n, seed=n + variant)
+    dt = 1 if kind.startswith("float") else 0
+    d = torch.from_numpy(a.copy()).to(gpu)
+    nb = int(L.mpx_sort_workspace_bytes(n, dt))
+    ws = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    _native.check(L.mpx_sort_variant(d.data_ptr(), n, dt, ws.data_ptr(), nb, variant, _native.stream_of(d)))
+    assert d.cpu().numpy().tobytes() == total_order_sorted(a).tobytes()
 
 
 @pytest.mark.gpu
@@ -309,7 +350,7 @@ def test_retired_sort_variants_are_refused():
     from cuda_mpi_openmp_amd import _native
 
     L = _native.lib()
-    for v in (3, 5, 6, 18, -1):
+    for v in (3, 5, 6, 22, -1):
         assert L.mpx_sort_variant(None, 1 << 20, 0, None, 0, v, None) != 0
         assert b"sort variant" in L.mpx_last_error()
 

@@ -177,3 +177,26 @@ ckpt_r5_pf() {
         done
     done
 }
+
+# O: sort hot digits (VERDICT r4 Next #6): RANK 3 / 4 rank up to four / two
+# hot digits per pass by ballot. Sort GPU tests, variants 12 / 18 / 20 and
+# 13 / 19 / 21 (SORT_AB) in one process on uniform and skewed data, twice, then
+# one kernel trace and one LDS counter pass (SORT_PROF) on 2^26 uniform int32
+# and normal floats (the skewed last pass).
+ckpt_r5_sort() {
+    export O=${O:-gpurun_out/r5/sort}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_lab5_sort.py &&
+    for r in 1 2; do
+        SORT_PROBE_PARTS=variants SORT_PROBE_VARIANTS=${SORT_AB:-12,18,20,13,19,21} SORT_PROBE_LOGN=24,26 \
+            bash tools/gpu.sh run probe$r 400 python -u tools/experiments/sort_probe.py || return 1
+    done &&
+    export SORT_PROBE_PARTS=variants SORT_PROBE_VARIANTS=${SORT_PROF:-12,18,20} SORT_PROBE_LOGN=26 SORT_PROBE_SMALL=0 \
+        SORT_PROBE_CASES=float32_normal,int32_uniform SORT_PROBE_ITERS=3 &&
+    bash tools/gpu.sh prof sort_trace -- python tools/experiments/sort_probe.py &&
+    bash tools/gpu.sh pmc sort_lds "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES" -- \
+        python tools/experiments/sort_probe.py &&
+    python tools/experiments/kprof_table.py "$O" --grep radix > "$O/kernels_table.md" &&
+    python tools/pmc_median.py "$O"/sort_lds > "$O/medians.md" &&
+    find "$O" -name "*.db" -delete
+}

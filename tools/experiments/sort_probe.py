@@ -10,7 +10,8 @@
    compared with torch.sort, plus the distributions that stress stability
    (few distinct values, all equal, sorted, reversed, normal floats).
 One JSON line per measurement. SORT_PROBE_ITERS (default 7) timed runs each,
-SORT_PROBE_PARTS=knock,variants, SORT_PROBE_VARIANTS=7,9, SORT_PROBE_LOGN=24,26 and
+SORT_PROBE_PARTS=knock,variants, SORT_PROBE_VARIANTS=7,9, SORT_PROBE_LOGN=24,26,
+SORT_PROBE_CASES=float32_normal,... (default: every case) and
 SORT_PROBE_SMALL=0|1 narrow a run."""
 import json
 import os
@@ -70,6 +71,9 @@ def main():
             n = 1 << lg
             cases.append(("int32_uniform", torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev)))
             cases.append(("float32_normal", torch.randn(n, device=dev)))
+            # skewed digits (RANK 3's hot-digit ballots): passes 2 / 3 one digit, pass 1 four
+            cases.append(("int32_range1000", torch.randint(0, 1000, (n,), dtype=torch.int32, device=dev)))
+            cases.append(("float32_uniform01", torch.rand(n, device=dev)))
         n = (1 << 22) + 37
         cases += [] if not SMALL else [("int32_few", torch.randint(0, 4, (n,), dtype=torch.int32, device=dev)),
                   ("int32_equal", torch.full((n,), 7, dtype=torch.int32, device=dev)),
@@ -78,7 +82,10 @@ def main():
                   ("float32_few", (torch.randint(0, 3, (n,), device=dev) - 1).float() * 0.5),
                   ("int32_bytes_skewed", (torch.randint(0, 2, (n,), dtype=torch.int32, device=dev) << 24)
                    | torch.randint(0, 1 << 8, (n,), dtype=torch.int32, device=dev))]
+        want = [c for c in os.environ.get("SORT_PROBE_CASES", "").split(",") if c]
         for name, src in cases:
+            if want and name not in want:
+                continue
             ref = torch.sort(src).values
             n = src.numel()
             dt = DTYPES[src.dtype]
