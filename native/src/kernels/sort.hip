@@ -786,7 +786,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __shared__ uint32_t s_wsum[4];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int crow = RANK == 2 ? 2 * w + (lane >> 5) : w;  // this lane's counter row
-    for (int i = t; i < NW * 512; i += TPB) s_tbl[i] = 0;
+    if constexpr (RANK == 0)  // the returning-add rankings never touch the tables (no LDS kept for them)
+        for (int i = t; i < NW * 512; i += TPB) s_tbl[i] = 0;
     for (int i = t; i < NR * CW; i += TPB) (&s_cnt[0][0])[i] = 0;
     const int xcd = blockIdx.x % kNumXCDs, per = gridDim.x / kNumXCDs;  // gridDim.x: a multiple of 8
     const int t1 = (int)((int64_t)ntiles * (xcd + 1) / kNumXCDs);
@@ -1404,6 +1405,7 @@ struct RadixWs {
 
 int64_t radix_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
 constexpr int kRTileSmall = kRTile / 2;  // the 256-thread lean scatter's tile (variant 8)
+constexpr int kRTileBig = kRTile * 2;    // the 1024-thread lean scatter's tile (variant 22)
 
 size_t radix_ws_bytes(int64_t n) {  // status sized for the smaller tile (twice the tiles)
     const size_t keys = ((size_t)n * 4 + 255) / 256 * 256;
@@ -1436,7 +1438,8 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // one-block-per-CU and static-order experiments; 17 = 12 with one counter row
 // per half-wave (RANK 2: skewed digits contend half as much); 18 / 19 = 12 / 13
 // with up to four hot digits ranked by ballot (RANK 3), 20 / 21 the same with
-// two (RANK 4). Retired after round-3
+// two (RANK 4); 22 = 20 on 16384-key tiles (1024 threads, one block per CU).
+// Retired after round-3
 // measurements (profiles/lab5_sort.md): 3 (ballot peer masks), 5 (reverse
 // tile walk), 6 (lean with six barriers per tile).
 // Look-back resolves one predecessor tile per memory round trip and the
@@ -1541,14 +1544,17 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // 8192-key tiles above (20); uniform passes run the round-4 code (12 / 13)
     if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 21 : 20;
     // the returning-add ranking needs ascending lane order (probe above)
-    const bool rtn_rank = (variant >= 9 && variant <= 21);
+    const bool rtn_rank = (variant >= 9 && variant <= 22);
     if (rtn_rank && lds_rtn_order_ok(s) != 1) {
         if (!auto_variant) return MPX_ERR_UNSUPPORTED;
         variant = n <= kTile4kMaxN ? 8 : 7;
     }
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13 || variant == 19 || variant == 21;
-    const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall) : (int)r.tiles;
+    const bool big_tiles = variant == 22;  // 16384-key tiles (1024-thread lean scatter, 1 block per CU)
+    const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall)
+                       : big_tiles ? (int)((n + kRTileBig - 1) / kRTileBig)
+                                   : (int)r.tiles;
     const bool onesweep = variant >= 14 && variant <= 16;
     if (variant == 1 || onesweep) {
         MPX_RETURN_IF_HIP_ERROR(hipMemsetAsync(r.hist, 0, r.zero_bytes, s));
@@ -1607,6 +1613,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             if (small_tiles)
                 hipLaunchKernelGGL(radix_count_kernel<kRTileSmall>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
                                    n, 8 * p, in_mode, r.status, ntiles);
+            else if (big_tiles)
+                hipLaunchKernelGGL(radix_count_kernel<kRTileBig>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
+                                   n, 8 * p, in_mode, r.status, ntiles);
             else
                 hipLaunchKernelGGL(radix_count_kernel<kRTile>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src, n,
                                    8 * p, in_mode, r.status, ntiles);
@@ -1651,6 +1660,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
                 else if (variant == 21)  // 19 with two hot-digit slots
                     launch_lean<kRThreads / 2, 4, 4, 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n,
                                                         r.hist, r.status, ntiles);
+                else if (variant == 22)  // 20 on 16384-key tiles: longer digit runs, fewer partial output lines
+                    launch_lean<kRThreads * 2, 4, 4, 2>(p, mode, std::min(kNumCUs, rounded), s, src, dst, n, r.hist,
+                                                        r.status, ntiles);
                 else
                     launch_lean<kRThreads / 2>(p, mode, std::min(kNumCUs * 4, rounded), s, src, dst, n, r.hist,
                                                r.status, ntiles);
@@ -1848,8 +1860,8 @@ extern "C" int mpx_sort_ws(void *data, int64_t n, int dtype, void *workspace, in
 // with a persistent scatter (see radix_sort32).
 extern "C" int mpx_sort_variant(void *data, int64_t n, int dtype, void *workspace, int64_t workspace_bytes, int variant,
                                 void *stream) {
-    if (variant < 0 || variant > 21 || variant == 3 || variant == 5 || variant == 6) {
-        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 21", variant);
+    if (variant < 0 || variant > 22 || variant == 3 || variant == 5 || variant == 6) {
+        mpx::set_error("sort variant %d: 0 (auto), 1, 2, 4, 7 .. 22", variant);
         return MPX_ERR_ARG;
     }
     return mpx::sort_impl(data, n, dtype, workspace, workspace_bytes, stream, variant);

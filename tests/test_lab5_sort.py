@@ -260,7 +260,7 @@ def test_gpu_sort_workspace_contract(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [1, 2, 4, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("kind", ["int", "float"])
 @pytest.mark.parametrize("n", [4097, 8193, 100_003, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants(gpu, variant, kind, n):
@@ -303,7 +303,7 @@ def skewed_array(kind, n, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [12, 13, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [12, 13, 18, 19, 20, 21, 22])
 @pytest.mark.parametrize("kind", ["float_normal", "float_unit", "int_range", "int_mix", "int_many_hot"])
 @pytest.mark.parametrize("n", [8193, (1 << 20) + 7, (1 << 23) + 5])
 def test_gpu_radix_variants_skewed_digits(gpu, variant, kind, n):
@@ -350,7 +350,7 @@ def test_retired_sort_variants_are_refused():
     from cuda_mpi_openmp_amd import _native
 
     L = _native.lib()
-    for v in (3, 5, 6, 22, -1):
+    for v in (3, 5, 6, 23, -1):
         assert L.mpx_sort_variant(None, 1 << 20, 0, None, 0, v, None) != 0
         assert b"sort variant" in L.mpx_last_error()
 
