@@ -1448,6 +1448,7 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // reduce-then-scan re-reads each tile once more but never waits.
 constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
 constexpr int64_t kTile4kMaxN = (int64_t)1 << 23;    // 4096-key tiles up to here (2^24: 0.187 ms both ways)
+constexpr int64_t kTile16kMinN = (int64_t)1 << 26;   // 16384-key tiles from here (variant 22)
 
 // pass p of the lean scatter: the first pass reads raw int32 / float32, the
 // last writes them back, the middle passes move keys
@@ -1540,9 +1541,12 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // tiles stop meeting in L2; profiles/lab5_sort.md)
     // AUTO (round 5, profiles/lab5_sort.md): the returning-add ranking with
     // two tiles of keys in flight and the two hottest digits of a skewed pass
-    // ranked by ballot (RANK 4), on 4096-key tiles up to 2^23 keys (21), on
-    // 8192-key tiles above (20); uniform passes run the round-4 code (12 / 13)
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 21 : 20;
+    // ranked by compare masks (RANK 4), on 4096-key tiles up to 2^23 keys
+    // (21), on 8192-key tiles below 2^26 (20), on 16384-key tiles from 2^26
+    // (22: longer digit runs, fewer partial output lines; 2^26 int32 0.689-0.697
+    // vs 0.706 ms, but 10 % slower at 2^24 with one block per CU); uniform
+    // passes run the round-4 code (12 / 13)
+    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 21 : n < kTile16kMinN ? 20 : 22;
     // the returning-add ranking needs ascending lane order (probe above)
     const bool rtn_rank = (variant >= 9 && variant <= 22);
     if (rtn_rank && lds_rtn_order_ok(s) != 1) {

@@ -200,3 +200,14 @@ ckpt_r5_sort() {
     python tools/pmc_median.py "$O"/sort_lds > "$O/medians.md" &&
     find "$O" -name "*.db" -delete
 }
+
+# P: mfma8s feature pairs by v_perm sign-extension (two VALU fewer per pixel):
+# classifier GPU tests, then the new library against the previous classify
+# kernel (abl/libmpx_old.so, built from HEAD's classify.hip) alternated 3x.
+ckpt_r5_lab3c() {
+    export O=${O:-gpurun_out/r5/lab3c}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=2,3,4,6,8 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
+        python -u tools/experiments/lab3_ab.py
+}
