@@ -945,11 +945,16 @@ __device__ __forceinline__ uint32_t s16x2_bits(s16x2 v) { return __builtin_bit_c
 // the four feature dwords of pixel p (build_i8's slot order)
 __device__ __forceinline__ void mfma8s_features(uint32_t p, int (&F)[4]) {
     const uint32_t x = p ^ 0x80808080u;  // centred channels as signed bytes
-    const int xi = (int)x;
-    const short r = (short)__builtin_amdgcn_sbfe(xi, 0, 8), g = (short)__builtin_amdgcn_sbfe(xi, 8, 8),
-                b = (short)__builtin_amdgcn_sbfe(xi, 16, 8);
+    // sign-extended 16-bit pairs in one v_perm each: with {x << 8 : x} as the
+    // perm's 64-bit source, selectors 8 / 10 / 11 replicate the top bits of
+    // bytes 1 / 5 / 7 = the signs of g / r / b (one shift instead of three
+    // bit-field extracts)
+    const uint32_t y = x << 8;
+    auto pair = [&](uint32_t sel) { return __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(y, x, sel)); };
     const s16x2 c128 = {128, 128};
-    const s16x2 U = {r, g}, V = {b, r}, W = {b, g}, Z = {b, b};
+    const s16x2 U = pair(0x08010A00u), V = pair(0x0A000B02u), W = pair(0x08010B02u);
+    const s16x2 Z = {V.x, V.x};  // op_sel of V's low half in the packed multiply, no instruction
+    // U = {r, g}, V = {b, r}, W = {b, g}, Z = {b, b}
     const uint32_t P01 = s16x2_bits(U * U + c128);  // [rr | gg] + 128
     const uint32_t P23 = s16x2_bits(V * W + c128);  // [bb | rg] + 128
     const uint32_t P45 = s16x2_bits(U * Z + c128);  // [rb | gb] + 128
