@@ -1007,7 +1007,10 @@ constexpr int kAmb8sCap = 1024;
 // PF: trips of loads in flight (1: the next trip's 16 B under this trip's
 // ranking; 2: two register sets in fixed roles, the trip after next issued
 // before this one is ranked — twice the bytes in flight per lane)
-template <int NS, int PF = 1>
+// MEM (tuning, MPX_CLS_MFMA8S_MEM): bit 1 non-temporal loads, bit 2
+// non-temporal stores of the image vectors (cls_load / cls_store); 4 = probe:
+// the same loop without the ranking (alpha cleared; output NOT classified)
+template <int NS, int PF = 1, int MEM = 0>
 __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, I8Params ip, FastParams fp,
                                                               uint32_t *amb) {
@@ -1021,6 +1024,10 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     auto trip = [&](const uint4 q, int64_t vi) {
+        if constexpr ((MEM & 4) != 0) {  // memory-only probe
+            cls_store<MEM>(&v[vi], make_uint4(q.x & 0xffffffu, q.y & 0xffffffu, q.z & 0xffffffu, q.w & 0xffffffu));
+            return;
+        }
         const uint32_t px[4] = {q.x, q.y, q.z, q.w};
         uint32_t o[4];
         bool u[4];
@@ -1039,30 +1046,30 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
                     if ((mask >> m) & 1u) o[m] = classify_direct(px[m], nc, cp);
             }
         }
-        v[vi] = make_uint4(o[0], o[1], o[2], o[3]);
+        cls_store<MEM>(&v[vi], make_uint4(o[0], o[1], o[2], o[3]));
     };
     if constexpr (PF == 2) {
-        uint4 qa = i < nvec ? v[i] : uint4{};
-        uint4 qb = i + stride < nvec ? v[i + stride] : uint4{};
+        uint4 qa = i < nvec ? cls_load<MEM>(&v[i]) : uint4{};
+        uint4 qb = i + stride < nvec ? cls_load<MEM>(&v[i + stride]) : uint4{};
         while (i < nvec) {
             {
                 const uint4 q = qa;
-                if (i + 2 * stride < nvec) qa = v[i + 2 * stride];
+                if (i + 2 * stride < nvec) qa = cls_load<MEM>(&v[i + 2 * stride]);
                 trip(q, i);
             }
             if ((i += stride) >= nvec) break;
             {
                 const uint4 q = qb;
-                if (i + 2 * stride < nvec) qb = v[i + 2 * stride];
+                if (i + 2 * stride < nvec) qb = cls_load<MEM>(&v[i + 2 * stride]);
                 trip(q, i);
             }
             i += stride;
         }
     } else {
-        uint4 qn = i < nvec ? v[i] : uint4{};
+        uint4 qn = i < nvec ? cls_load<MEM>(&v[i]) : uint4{};
         for (; i < nvec; i += stride) {
             const uint4 q = qn;
-            if (i + stride < nvec) qn = v[i + stride];
+            if (i + stride < nvec) qn = cls_load<MEM>(&v[i + stride]);
             trip(q, i);
         }
     }
@@ -1484,20 +1491,48 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         const int64_t nvec = npix / 4;
         if (nvec > 0) {
             const int64_t blocks = (nvec + 255) / 256;
+            // at most 16 blocks per CU (two resident rounds at 8 waves per SIMD,
+            // 16 trips per thread at 8192^2): more, shorter-lived workgroups
+            // balance the load across CUs, and fewer trips per thread keep less
+            // store latency on each wave's critical path (gfx950 stores count
+            // in vmcnt with the loads). 8192^2, µs, 8 -> 16 blocks per CU:
+            // nc = 2 126-129 -> 118, nc = 4 133-135 -> 128-130, nc = 8 same
+            // (profiles/lab3_classify.md). MPX_CLS_MFMA8S_GRID=k overrides
+            // (tuning).
+            static const int gcap = [] {
+                const char *e = std::getenv("MPX_CLS_MFMA8S_GRID");
+                const int k = e ? std::atoi(e) : 0;
+                return k > 0 ? k : 16;
+            }();
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256)
-                                   : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+                                   : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * gcap);
             const int ns = (nc + 1) / 2;
-            // MPX_CLS_MFMA8S_PF=2: two trips of loads in flight (A/B; read once)
+            // MPX_CLS_MFMA8S_PF=2: two trips of loads in flight; MPX_CLS_MFMA8S_MEM=1..3:
+            // non-temporal loads (1) / stores (2) / both (3) (A/B; read once)
             static const int pf = [] {
                 const char *e = std::getenv("MPX_CLS_MFMA8S_PF");
                 return (e && e[0] == '2') ? 2 : 1;
             }();
-#define MPX_MFMA8S(NS)                                                                                             \
-    do {                                                                                                           \
-        if (pf == 2)                                                                                               \
-            hipLaunchKernelGGL((classify_mfma8s_kernel<NS, 2>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb); \
-        else                                                                                                       \
-            hipLaunchKernelGGL((classify_mfma8s_kernel<NS, 1>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb); \
+            static const int mem = [] {
+                const char *e = std::getenv("MPX_CLS_MFMA8S_MEM");
+                return (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
+            }();
+#define MPX_MFMA8S_L(NS, PF, MEM) \
+    hipLaunchKernelGGL((classify_mfma8s_kernel<NS, PF, MEM>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb)
+#define MPX_MFMA8S(NS)                    \
+    do {                                  \
+        if (pf == 2)                      \
+            MPX_MFMA8S_L(NS, 2, 0);       \
+        else if (mem == 1)                \
+            MPX_MFMA8S_L(NS, 1, 1);       \
+        else if (mem == 2)                \
+            MPX_MFMA8S_L(NS, 1, 2);       \
+        else if (mem == 3)                \
+            MPX_MFMA8S_L(NS, 1, 3);       \
+        else if (mem == 4)                \
+            MPX_MFMA8S_L(NS, 1, 4);       \
+        else                              \
+            MPX_MFMA8S_L(NS, 1, 0);       \
     } while (0)
             if (ns == 1)
                 MPX_MFMA8S(1);
@@ -1508,6 +1543,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             else
                 MPX_MFMA8S(4);
 #undef MPX_MFMA8S
+#undef MPX_MFMA8S_L
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             done = nvec * 4;
         }

@@ -211,3 +211,70 @@ ckpt_r5_lab3c() {
     LAB3_NCS=2,3,4,6,8 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
         python -u tools/experiments/lab3_ab.py
 }
+
+# Q: the lab3 in-place floor on the same box: the linear 16-B copy with source
+# == destination (plain / non-temporal) beside mfma8 / fast32 at nc = 2 / 4
+ckpt_r5_floor() {
+    export O=${O:-gpurun_out/r5/floor}
+    mkdir -p "$O"
+    for r in 1 2; do
+        LAB3_FLOOR=1 LAB3_NCS=2,4 LAB3_PATHS=mfma8,fast LAB3_TAG=r$r \
+            bash tools/gpu.sh run lab3_floor$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done
+}
+
+# R: mfma8s memory policy (MPX_CLS_MFMA8S_MEM: 1 NT loads, 2 NT stores, 3 both)
+# against the in-place copy floor, alternated twice
+ckpt_r5_mem() {
+    export O=${O:-gpurun_out/r5/mem}
+    mkdir -p "$O"
+    for r in 1 2; do
+        for m in 0 1 2 3; do
+            MPX_CLS_MFMA8S_MEM=$m LAB3_FLOOR=$([ $m = 0 ] && echo 1 || echo 0) LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 \
+                LAB3_TAG=m${m}_$r bash tools/gpu.sh run lab3_m${m}_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+        done
+    done
+}
+
+# S: where the mfma8s time goes: the same loop without the ranking (MEM=4),
+# the default, and larger grids (MPX_CLS_MFMA8S_GRID blocks per CU), twice
+ckpt_r5_grid() {
+    export O=${O:-gpurun_out/r5/grid}
+    mkdir -p "$O"
+    for r in 1 2; do
+        for k in 8 32 256; do
+            for m in 0 4; do
+                MPX_CLS_MFMA8S_GRID=$k MPX_CLS_MFMA8S_MEM=$m LAB3_FLOOR=$([ $k$m = 80 ] && echo 1 || echo 0) \
+                    LAB3_NCS=2,4 LAB3_PATHS=mfma8 LAB3_TAG=g${k}m${m}_$r \
+                    bash tools/gpu.sh run lab3_g${k}m${m}_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+            done
+        done
+    done
+}
+
+# T: mfma8s grid sweep (blocks per CU: trips per thread = 256 / k) with one or
+# two trips of loads in flight, nc = 2 / 4 / 8, twice
+ckpt_r5_grid2() {
+    export O=${O:-gpurun_out/r5/grid2}
+    mkdir -p "$O"
+    for r in 1 2; do
+        for k in 16 32 64; do
+            for pf in 1 2; do
+                MPX_CLS_MFMA8S_GRID=$k MPX_CLS_MFMA8S_PF=$pf LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 LAB3_TAG=g${k}pf${pf}_$r \
+                    bash tools/gpu.sh run lab3_g${k}pf${pf}_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+            done
+        done
+    done
+}
+
+# U: launch grids of the other classify paths (explicit grids through the
+# public API: 2048 = the default 8 blocks per CU, up to 16384), nc = 12 (fast32
+# in AUTO), 16 and 32 (mfma8), plus the new mfma8s default at nc = 2 / 4 / 8
+ckpt_r5_grid3() {
+    export O=${O:-gpurun_out/r5/grid3}
+    mkdir -p "$O"
+    LAB3_NCS=12,16,32 LAB3_GRIDS=2048,4096,8192,16384 \
+        bash tools/gpu.sh run grid_sweep 600 python -u tools/experiments/lab3_grid_sweep.py &&
+    LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 LAB3_TAG=g16 \
+        bash tools/gpu.sh run lab3_g16 300 python -u tools/experiments/lab3_ab.py
+}

@@ -41,6 +41,23 @@ def main():
     ncs = [int(v) for v in os.environ.get("LAB3_NCS", "2,4,8,32").split(",")]
     paths = os.environ.get("LAB3_PATHS", "fast,mfma8").split(",")
     tag = os.environ.get("LAB3_TAG", "")
+    if os.environ.get("LAB3_FLOOR", "0") == "1":
+        # the in-place read-modify-write floor of the same bytes: the tune
+        # library's linear 16-B copy with source == destination (d = 0 plain,
+        # 1 non-temporal), same rotation, same timing
+        from cuda_mpi_openmp_amd import _native
+        T = _native.tune_lib()
+        for d in (0, 1):
+            cyc = [0]
+
+            def run_copy(d=d):
+                x = imgs[cyc[0] % 3]
+                _native.check(T.mpx_strip_copy_probe(x.data_ptr(), x.data_ptr(), size, size, 0, d, 0,
+                                                     _native.stream_of(x)))
+                cyc[0] += 1
+            med, mn = time_us(run_copy)
+            print(json.dumps({"tag": tag, "path": f"inplace_copy_d{d}", "us": round(med, 1), "us_min": round(mn, 1),
+                              "tbps": round(2 * size * size * 4 / (med * 1e-6) / 1e12, 2)}), flush=True)
     for nc in ncs:
         pts = class_points_for(size, size, nc, 64, seed=nc)
         mu, inv = ops.class_stats(host, pts)
