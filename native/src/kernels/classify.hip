@@ -674,11 +674,15 @@ __device__ __forceinline__ void rank_regs(const i32x16 &da, const i32x16 &db, in
 
 // Per-wave constants of the mfma8 GEMM (weights, accumulator init, byte
 // selectors of the feature packing).
+// packed 16-bit channel products (the int8 feature builders)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t s16x2_bits(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
 struct Mfma8Lane {
     long wa, wb;
     i32x16 cinit;
     int add, h;
-    uint32_t selA, selB, selD;
+    uint32_t sel0, sel1;  // feature dwords from the packed products (mfma8_chunk)
 };
 
 __device__ __forceinline__ Mfma8Lane mfma8_lane(const I8Params &ip, int lane) {
@@ -692,9 +696,10 @@ __device__ __forceinline__ Mfma8Lane mfma8_lane(const I8Params &ip, int lane) {
     // half 0 packs byte 1 of P + 128 (the h limbs), half 1 byte 0 of P (the l limbs)
     L.add = L.h ? 0 : 128;
     const uint32_t sel = L.h ? 0u : 1u;
-    L.selA = sel | ((4u + sel) << 8) | (0x0Cu << 16) | (0x0Cu << 24);  // [x.s, y.s, 0, 0]
-    L.selB = 0x0Cu | (0x0Cu << 8) | (sel << 16) | ((4u + sel) << 24);   // [0, 0, x.s, y.s]
-    L.selD = 0x0Cu | (0x0Cu << 8) | (0u << 16) | ((L.h ? 0x0Cu : 4u) << 24);  // [0, 0, x6, g | 0]
+    // d0 = byte s of each 16-bit product [rr gg | bb rg]: perm(PB, PA)
+    L.sel0 = sel | ((2u + sel) << 8) | ((4u + sel) << 16) | ((6u + sel) << 24);
+    // d1 = [rb.s, gb.s, b or r, 0 or g]: perm(PC, centred pixel)
+    L.sel1 = (4u + sel) | ((6u + sel) << 8) | ((L.h ? 2u : 0u) << 16) | ((L.h ? 0x0Cu : 1u) << 24);
     return L;
 }
 
@@ -707,14 +712,18 @@ __device__ __forceinline__ uint32_t mfma8_chunk(const uint4 &q, const Mfma8Lane 
     int32_t rb[4], rs[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        const int p = (int)(px[m] ^ 0x80808080u);  // bytes - 128, sign-extended below
-        const int r = __builtin_amdgcn_sbfe(p, 0, 8), g = __builtin_amdgcn_sbfe(p, 8, 8),
-                  b = __builtin_amdgcn_sbfe(p, 16, 8);
-        const uint32_t P0 = (uint32_t)(r * r + L.add), P1 = (uint32_t)(g * g + L.add), P2 = (uint32_t)(b * b + L.add);
-        const uint32_t P3 = (uint32_t)(r * g + L.add), P4 = (uint32_t)(r * b + L.add), P5 = (uint32_t)(g * b + L.add);
-        const uint32_t x6 = (uint32_t)(L.h ? b : r);
-        const uint32_t d0 = __builtin_amdgcn_perm(P1, P0, L.selA) | __builtin_amdgcn_perm(P3, P2, L.selB);
-        const uint32_t d1 = __builtin_amdgcn_perm(P5, P4, L.selA) | __builtin_amdgcn_perm((uint32_t)g, x6, L.selD);
+        // the six products as three packed 16-bit multiply-adds of sign-extended
+        // channel pairs (mfma8s_features: one v_perm per pair), then one v_perm
+        // per feature dword
+        const uint32_t x = px[m] ^ 0x80808080u;  // bytes - 128
+        const uint32_t y = x << 8;
+        auto pair = [&](uint32_t sl) { return __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(y, x, sl)); };
+        const s16x2 U = pair(0x08010A00u), V = pair(0x0A000B02u), W = pair(0x08010B02u);  // {r,g} {b,r} {b,g}
+        const s16x2 Z = {V.x, V.x};
+        const s16x2 ad = {(short)L.add, (short)L.add};
+        const uint32_t PA = s16x2_bits(U * U + ad), PB = s16x2_bits(V * W + ad), PC = s16x2_bits(U * Z + ad);
+        const uint32_t d0 = __builtin_amdgcn_perm(PB, PA, L.sel0);
+        const uint32_t d1 = __builtin_amdgcn_perm(PC, x, L.sel1);
         const long feat = (long)(((uint64_t)d1 << 32) | d0);
         const i32x16 da = __builtin_amdgcn_mfma_i32_32x32x16_i8(L.wa, feat, i32x16{}, 0, 0, 0);
         const i32x16 db = __builtin_amdgcn_mfma_i32_32x32x16_i8(L.wb, feat, L.cinit, 0, 0, 0);
@@ -919,7 +928,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
 //   NS = row sets (2 classes each) with real classes: 1, 2, 3 or 4.
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 struct Mfma8sLane {
     int w[4][4];     // [row set][step]: 4 int8 weights of this lane's row
@@ -940,7 +948,6 @@ __device__ __forceinline__ Mfma8sLane mfma8s_lane(const I8Params &ip, int lane) 
     return L;
 }
 
-__device__ __forceinline__ uint32_t s16x2_bits(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
 // the four feature dwords of pixel p (build_i8's slot order)
 __device__ __forceinline__ void mfma8s_features(uint32_t p, int (&F)[4]) {
@@ -1558,7 +1565,10 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         }();
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;
-            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            // 16 blocks per CU (round-5 sweep at 8192^2, 2048 -> 4096 blocks:
+            // nc = 12 269.5 -> 261.1 µs, 16 269.7 -> 262.7, 32 391.1 -> 375.2;
+            // 8192 and 16384 slower again; profiles/lab3_classify.md)
+            const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
 #define MPX_MFMA8_LAUNCH(NREG)                                                                                       \
     do {                                                                                                             \
         if (win)                                                                                                     \
@@ -1630,7 +1640,10 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             // ("unspecified launch failure"), so it is capped
             const int blk = block > 0 ? std::min(block, 256) : 256;
             const int64_t blocks = (nvec + blk - 1) / blk;
-            const int g = grid > 0 ? (int)useful_grid(grid, nvec, blk) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 8);
+            // 32 blocks per CU (round-5 sweep at 8192^2, 2048 -> 8192 blocks:
+            // nc = 12 285.6 -> 247.4 µs, 16 297.9 -> 288.2, 32 524.4 -> 504.9;
+            // profiles/lab3_classify.md)
+            const int g = grid > 0 ? (int)useful_grid(grid, nvec, blk) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 32);
             // wave-contiguous vectors need waves that start at multiples of 64 threads
             const int o = (opt & 4) && blk % 64 != 0 ? opt & 3 : opt;
             if (nq == 2 && o != 0) {

@@ -278,3 +278,14 @@ ckpt_r5_grid3() {
     LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 LAB3_TAG=g16 \
         bash tools/gpu.sh run lab3_g16 300 python -u tools/experiments/lab3_ab.py
 }
+
+# V: mfma8 (32x32) feature bytes from packed 16-bit products: classifier GPU
+# tests, then new vs previous classify kernel (abl/libmpx_old.so) alternated
+# 3x at nc = 16 / 32 (mfma8) and 4 (mfma8s)
+ckpt_r5_lab3d() {
+    export O=${O:-gpurun_out/r5/lab3d}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=4,16,32 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
+        python -u tools/experiments/lab3_ab.py
+}
