@@ -289,3 +289,25 @@ ckpt_r5_lab3d() {
     LAB3_NCS=4,16,32 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
         python -u tools/experiments/lab3_ab.py
 }
+
+# W (final tree, after the late lab3 / sort changes): smoke, the driver's
+# bench, the per-kernel profile, and AUTO at nc = 2 .. 32 over three rotated
+# images; the full GPU suite runs in its own call (checkpoint r5_tests)
+ckpt_r5_final2() {
+    export O=${O:-gpurun_out/r5/final2}
+    mkdir -p "$O"
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    LAB3_NCS=2,3,4,6,8,12,16,20,24,32 LAB3_PATHS=auto LAB3_TAG=auto \
+        bash tools/gpu.sh run lab3_auto 400 python -u tools/experiments/lab3_ab.py &&
+    bash tools/gpu.sh profile kfinal -- python3 tools/prof_all.py &&
+    python tools/experiments/kprof_table.py "$O" > "$O/kernels_table.md" &&
+    python tools/pmc_median.py "$O"/kfinal.pmc* > "$O/medians.md" &&
+    python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
+    du -sh "$O" && find "$O" -name "*.db" -delete && du -sh "$O"
+}
+ckpt_r5_tests() {
+    export O=${O:-gpurun_out/r5/tests2}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests
+}
