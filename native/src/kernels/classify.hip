@@ -1009,7 +1009,12 @@ __device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane &L
 // one append per trip instead of one per pixel (with ~0.4% of the pixels
 // undecided at nc = 4, a quarter of the trips have one). The pixels are
 // re-read from the image after the loop: their RGB bytes are untouched.
-constexpr int kAmb8sCap = 1024;
+// Every list is private to one wave (its own LDS rows and counters): a wave
+// appends, then ranks its own deferred pixels, in program order — LDS
+// operations of one wave execute in order — so the kernel has no block
+// barrier, and short-lived workgroups cost no more than long ones.
+constexpr int kAmb8sCapW = 256;   // deferred (vector, mask) entries per wave
+constexpr int kAmb8sCap2W = 64;   // pixels the fp32 stage leaves to the fp64 chain, per wave
 
 // PF: trips of loads in flight (1: the next trip's 16 B under this trip's
 // ranking; 2: two register sets in fixed roles, the trip after next issued
@@ -1021,12 +1026,16 @@ template <int NS, int PF = 1, int MEM = 0>
 __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, I8Params ip, FastParams fp,
                                                               uint32_t *amb) {
-    const Mfma8sLane L = mfma8s_lane(ip, threadIdx.x & 63);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const Mfma8sLane L = mfma8s_lane(ip, lane);
     const int32_t T2k = ip.T2 * 32 + 31;
-    __shared__ int64_t s_amb[kAmb8sCap];  // vector index << 4 | undecided-pixel mask
-    __shared__ uint32_t s_namb, s_npx;
-    if (threadIdx.x == 0) s_namb = s_npx = 0;
-    __syncthreads();
+    __shared__ int64_t s_amb[4][kAmb8sCapW];  // vector index << 4 | undecided-pixel mask
+    __shared__ uint32_t s_namb[4], s_npx[4];
+    __shared__ int64_t s_amb2[4][kAmb8sCap2W];
+    __shared__ uint32_t s_ambpx2[4][kAmb8sCap2W];
+    __shared__ uint32_t s_namb2[4];
+    if (lane == 0) s_namb[w] = s_npx[w] = s_namb2[w] = 0;
+    __builtin_amdgcn_wave_barrier();
     uint4 *v = reinterpret_cast<uint4 *>(img);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1044,9 +1053,9 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
         // is built only inside the rare branch
         if (__builtin_expect(u[0] | u[1] | u[2] | u[3], 0)) {
             const uint32_t mask = (uint32_t)u[0] | ((uint32_t)u[1] << 1) | ((uint32_t)u[2] << 2) | ((uint32_t)u[3] << 3);
-            const uint32_t slot = atomicAdd(&s_namb, 1u);
-            if (slot < (uint32_t)kAmb8sCap) {
-                s_amb[slot] = (vi << 4) | mask;
+            const uint32_t slot = atomicAdd(&s_namb[w], 1u);
+            if (slot < (uint32_t)kAmb8sCapW) {
+                s_amb[w][slot] = (vi << 4) | mask;
             } else {  // list full: the exact chain inline (never at the benchmark's rates)
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
@@ -1080,20 +1089,17 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
             trip(q, i);
         }
     }
-    // the deferred pixels: the fp32 proven-margin ranking first, the exact fp64
-    // chain for what it leaves (as in MFMA8, every lane busy in each stage)
-    __shared__ int64_t s_amb2[kAmb8Cap2];
-    __shared__ uint32_t s_ambpx2[kAmb8Cap2];
-    __shared__ uint32_t s_namb2;
-    if (threadIdx.x == 0) s_namb2 = 0;
-    __syncthreads();
-    const uint32_t nd = min(s_namb, (uint32_t)kAmb8sCap);
-    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
-        const int64_t e = s_amb[j];
+    // this wave's deferred pixels: the fp32 proven-margin ranking first, the
+    // exact fp64 chain for what it leaves (every lane of the wave busy in each
+    // stage); the wave's appends above precede these reads in program order
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nd = min(s_namb[w], (uint32_t)kAmb8sCapW);
+    for (uint32_t j = lane; j < nd; j += 64) {
+        const int64_t e = s_amb[w][j];
         const int64_t vi = e >> 4;
         const uint32_t mask = (uint32_t)e & 15u;
-        atomicAdd(&s_npx, (uint32_t)__popc(mask));
-        const uint4 q = v[vi];  // this thread's own vector: written above in program order
+        atomicAdd(&s_npx[w], (uint32_t)__popc(mask));
+        const uint4 q = v[vi];  // a vector this wave wrote above, in program order
         const uint32_t px[4] = {q.x, q.y, q.z, q.w};
         for (int m = 0; m < 4; ++m) {
             if (!((mask >> m) & 1u)) continue;
@@ -1101,20 +1107,20 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
             if (classify_fp32_one(px[m], nc, fp, o)) {
                 img[vi * 4 + m] = o;
             } else {
-                const uint32_t slot = atomicAdd(&s_namb2, 1u);
-                if (slot < (uint32_t)kAmb8Cap2) {
-                    s_amb2[slot] = vi * 4 + m;
-                    s_ambpx2[slot] = px[m];
+                const uint32_t slot = atomicAdd(&s_namb2[w], 1u);
+                if (slot < (uint32_t)kAmb8sCap2W) {
+                    s_amb2[w][slot] = vi * 4 + m;
+                    s_ambpx2[w][slot] = px[m];
                 } else {
                     img[vi * 4 + m] = classify_direct(px[m], nc, cp);
                 }
             }
         }
     }
-    __syncthreads();
-    if (amb && threadIdx.x == 0 && s_npx) atomicAdd(amb, s_npx);  // one global add per block
-    const uint32_t nd2 = min(s_namb2, (uint32_t)kAmb8Cap2);
-    for (uint32_t j = threadIdx.x; j < nd2; j += blockDim.x) img[s_amb2[j]] = classify_direct(s_ambpx2[j], nc, cp);
+    __builtin_amdgcn_wave_barrier();
+    if (amb && lane == 0 && s_npx[w]) atomicAdd(amb, s_npx[w]);  // one global add per wave with any
+    const uint32_t nd2 = min(s_namb2[w], (uint32_t)kAmb8sCap2W);
+    for (uint32_t j = lane; j < nd2; j += 64) img[s_amb2[w][j]] = classify_direct(s_ambpx2[w][j], nc, cp);
 }
 
 // ---------------------------------------------------------------------------

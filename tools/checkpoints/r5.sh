@@ -311,3 +311,20 @@ ckpt_r5_tests() {
     mkdir -p "$O"
     bash tools/gpu.sh tests
 }
+
+# X: mfma8s with per-wave deferral lists (no block barriers): classifier GPU
+# tests; new vs previous kernel (abl/libmpx_old.so) at the default grid, then
+# the new kernel at 16 / 32 / 64 / 128 blocks per CU, nc = 2 / 4 / 8, twice
+ckpt_r5_lab3e() {
+    export O=${O:-gpurun_out/r5/lab3e}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 2 -- \
+        python -u tools/experiments/lab3_ab.py &&
+    for r in 1 2; do
+        for k in 16 32 64 128; do
+            MPX_CLS_MFMA8S_GRID=$k LAB3_NCS=2,4,8 LAB3_PATHS=mfma8 LAB3_TAG=g${k}_$r \
+                bash tools/gpu.sh run lab3_g${k}_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+        done
+    done
+}
