@@ -1254,7 +1254,11 @@ __device__ __forceinline__ void count_add(uint32_t *hw, uint32_t d) {
     if (!is || lead) atomicAdd(&hw[d], is ? (uint32_t)__popcll(m) : 1u);
 }
 
-template <bool VEC, int TILE>
+typedef uint32_t sort_u32x4 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take clang vectors
+
+// NT: non-temporal key loads (the count pass reads every key once; tuning
+// A/B, MPX_SORT_COUNT_NT)
+template <bool VEC, int TILE, bool NT = false>
 __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in, int64_t n, int shift, int mode,
                                                 int tile, uint32_t *hw) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1264,7 +1268,14 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
         const uint4 *src = reinterpret_cast<const uint4 *>(in + (int64_t)tile * TILE + w * kWaveKeys) + lane;
         uint4 q[kCPer / 4];
 #pragma unroll
-        for (int e = 0; e < kCPer / 4; ++e) q[e] = src[e * 64];
+        for (int e = 0; e < kCPer / 4; ++e) {
+            if constexpr (NT) {
+                const sort_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const sort_u32x4 *>(src + e * 64));
+                q[e] = make_uint4(x[0], x[1], x[2], x[3]);
+            } else {
+                q[e] = src[e * 64];
+            }
+        }
 #pragma unroll
         for (int e = 0; e < kCPer / 4; ++e) {
             count_add(hw, (to_key(q[e].x, mode) >> shift) & 255u);
@@ -1286,7 +1297,7 @@ __device__ __forceinline__ void count_tile_keys(const uint32_t *__restrict__ in,
     }
 }
 
-template <int TILE = kRTile>
+template <int TILE = kRTile, bool NT = false>
 __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *__restrict__ in, int64_t n, int shift,
                                                                 int mode, uint32_t *__restrict__ cnt, int ntiles) {
     __shared__ uint32_t h[kCThreads / 64][256];
@@ -1296,7 +1307,7 @@ __global__ __launch_bounds__(kCThreads) void radix_count_kernel(const uint32_t *
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     // block-uniform: whole tile in range and the input 16-B aligned
     if (((int64_t)tile + 1) * TILE <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0)
-        count_tile_keys<true, TILE>(in, n, shift, mode, tile, h[w]);
+        count_tile_keys<true, TILE, NT>(in, n, shift, mode, tile, h[w]);
     else
         count_tile_keys<false, TILE>(in, n, shift, mode, tile, h[w]);
     __syncthreads();
@@ -1556,6 +1567,10 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // variant 8: 4096-key tiles (256-thread lean scatter, 4 blocks per CU)
     const bool small_tiles = variant == 8 || variant == 10 || variant == 13 || variant == 19 || variant == 21;
     const bool big_tiles = variant == 22;  // 16384-key tiles (1024-thread lean scatter, 1 block per CU)
+    static const bool count_nt = [] {  // MPX_SORT_COUNT_NT=1: non-temporal count-pass loads (A/B, read once)
+        const char *e = std::getenv("MPX_SORT_COUNT_NT");
+        return e && e[0] == '1';
+    }();
     const int ntiles = small_tiles ? (int)((n + kRTileSmall - 1) / kRTileSmall)
                        : big_tiles ? (int)((n + kRTileBig - 1) / kRTileBig)
                                    : (int)r.tiles;
@@ -1617,6 +1632,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
             if (small_tiles)
                 hipLaunchKernelGGL(radix_count_kernel<kRTileSmall>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
                                    n, 8 * p, in_mode, r.status, ntiles);
+            else if (big_tiles && count_nt)
+                hipLaunchKernelGGL((radix_count_kernel<kRTileBig, true>), dim3((unsigned)ntiles), dim3(kCThreads), 0, s,
+                                   src, n, 8 * p, in_mode, r.status, ntiles);
             else if (big_tiles)
                 hipLaunchKernelGGL(radix_count_kernel<kRTileBig>, dim3((unsigned)ntiles), dim3(kCThreads), 0, s, src,
                                    n, 8 * p, in_mode, r.status, ntiles);

@@ -328,3 +328,17 @@ ckpt_r5_lab3e() {
         done
     done
 }
+
+# Y: non-temporal count-pass loads (MPX_SORT_COUNT_NT) for the 16384-key
+# tiles, alternated three times at 2^26 (variant 22 = AUTO there)
+ckpt_r5_cnt() {
+    export O=${O:-gpurun_out/r5/cnt}
+    mkdir -p "$O"
+    for r in 1 2 3; do
+        for nt in 0 1; do
+            MPX_SORT_COUNT_NT=$nt SORT_PROBE_PARTS=variants SORT_PROBE_VARIANTS=22 SORT_PROBE_LOGN=26 \
+                SORT_PROBE_SMALL=0 bash tools/gpu.sh run probe_nt${nt}_$r 300 python -u tools/experiments/sort_probe.py \
+                || return 1
+        done
+    done
+}
