@@ -342,3 +342,13 @@ ckpt_r5_cnt() {
         done
     done
 }
+
+# Z: the final tree as the driver will see it: smoke, the driver's bench
+# command, the full GPU suite
+ckpt_r5_last() {
+    export O=${O:-gpurun_out/r5/last}
+    mkdir -p "$O"
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh tests
+}
