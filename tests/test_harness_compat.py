@@ -125,3 +125,25 @@ def test_compat_lab2_outputs_gt_and_sidecars(tmp_path):
     for f in before:
         with open(lab / "data" / f, "rb") as a, open(os.path.join(ROOT, "labs", "lab2", "data", f), "rb") as b:
             assert a.read() == b.read(), f
+
+
+def test_harness_summary_renders_the_tracked_comparison():
+    """profiles/harness_vs_baseline.md is rendered from the tracked r5 CSVs by
+    tools/harness_summary.py: the speedup table carries every lab2 bucket and
+    lab1 size with the published figure beside it, and the per-geometry
+    tables every published configuration (VERDICT r4 Next #3)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    raw = os.path.join(root, "profiles", "raw", "r5", "harness_cmp")
+    tool = os.path.join(root, "tools", "harness_summary.py")
+    sp = subprocess.run([sys.executable, tool, raw, "--speedups"], capture_output=True, text=True, check=True).stdout
+    rows = {tuple(c.strip() for c in line.split("|")[1:3]): line for line in sp.splitlines() if line.startswith("| lab")}
+    for key, pub in ((("lab2", "large"), "212.0x"), (("lab2", "medium"), "101.0x"), (("lab1", "1000000"), "62.0x")):
+        assert key in rows and rows[key].rstrip().endswith(f"| {pub} |"), (key, sp)
+    assert ("lab2", "xl4096") in rows and ("lab1", "1000") in rows
+    vb = subprocess.run([sys.executable, tool, raw, "--vs-baseline"], capture_output=True, text=True, check=True).stdout
+    for head in ("### lab1 n = 1000000", "### lab2 large bucket", "### lab2 small bucket"):
+        assert head in vb
+    assert "[[16, 16], [1024, 1024]]" in vb and "auto (tuned)" in vb
