@@ -77,19 +77,23 @@ class _AmdSmi:
 
         self.a = amdsmi
         amdsmi.amdsmi_init()
-        hs = amdsmi.amdsmi_get_processor_handles()
-        if not hs:
-            raise RuntimeError("amdsmi: no GPU handles")
-        self.h = hs[0]
-        if bdf:
-            for h in hs:
-                try:
-                    if amdsmi.amdsmi_get_gpu_device_bdf(h).lower().endswith(bdf.lower()):
-                        self.h = h
-                        break
-                except Exception:  # noqa: BLE001
-                    continue
-        self.read()  # fail here, not in the thread
+        try:
+            hs = amdsmi.amdsmi_get_processor_handles()
+            if not hs:
+                raise RuntimeError("amdsmi: no GPU handles")
+            self.h = hs[0]
+            if bdf:
+                for h in hs:
+                    try:
+                        if amdsmi.amdsmi_get_gpu_device_bdf(h).lower().endswith(bdf.lower()):
+                            self.h = h
+                            break
+                    except Exception:  # noqa: BLE001
+                        continue
+            self.read()  # fail here, not in the thread
+        except Exception:
+            self.close()  # the library was initialised: shut it down before falling back
+            raise
 
     def read(self) -> Dict[str, float]:
         return _flatten(self.a.amdsmi_get_gpu_metrics_info(self.h))
