@@ -352,3 +352,23 @@ ckpt_r5_last() {
     bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
     bash tools/gpu.sh tests
 }
+
+# AA: fast32 with per-wave deferral lists: classifier GPU tests, then new vs
+# previous kernel (abl/libmpx_old.so) alternated 3x at nc = 12 / 16 / 32
+ckpt_r5_fast() {
+    export O=${O:-gpurun_out/r5/fast}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=12,16,32 LAB3_PATHS=fast bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
+        python -u tools/experiments/lab3_ab.py
+}
+
+# AB: mfma8 (32x32) with per-wave deferral lists: classifier GPU tests, then
+# new vs previous kernel (abl/libmpx_old.so) alternated 3x at nc = 16 / 24 / 32
+ckpt_r5_m8w() {
+    export O=${O:-gpurun_out/r5/m8w}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=16,24,32 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
+        python -u tools/experiments/lab3_ab.py
+}
