@@ -925,20 +925,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
 //   of P = byte 0 of (P + 128) ^ 0x80.
 //   Keys as in MFMA8: ((D_a << 8) + D_b) << 5 | class — two v_lshl_add per
 //   class — then the running top-2 in the lane; no cross-lane merge.
-//   NS = row sets (2 classes each) with real classes: 1, 2, 3 or 4.
+//   NS = row sets (2 classes each) with real classes: 1 .. 7 up to
+//   kMfma8sMaxClasses = 14 classes (8 for MPX_CLS_MFMA8S_MAX=16, A/B).
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+template <int NS>
 struct Mfma8sLane {
-    int w[4][4];     // [row set][step]: 4 int8 weights of this lane's row
-    i32x4 cinit[4];  // [row set]: {0, c(2s), 0, c(2s + 1)}
+    int w[NS][4];     // [row set][step]: 4 int8 weights of this lane's row
+    i32x4 cinit[NS];  // [row set]: {0, c(2s), 0, c(2s + 1)}
 };
 
-__device__ __forceinline__ Mfma8sLane mfma8s_lane(const I8Params &ip, int lane) {
-    Mfma8sLane L;
+template <int NS>
+__device__ __forceinline__ Mfma8sLane<NS> mfma8s_lane(const I8Params &ip, int lane) {
+    Mfma8sLane<NS> L;
     const int r = lane & 3;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const int c = 2 * s + (r >> 1);
         const uint64_t *limb = (r & 1) ? ip.b[c] : ip.a[c];
 #pragma unroll
@@ -973,7 +976,7 @@ __device__ __forceinline__ void mfma8s_features(uint32_t p, int (&F)[4]) {
 
 // rank one pixel: provisional output and whether its top-2 margin is within T2
 template <int NS>
-__device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane &L, int32_t T2k, bool &undecided) {
+__device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane<NS> &L, int32_t T2k, bool &undecided) {
     int F[4];
     mfma8s_features(p, F);
     i32x4 D[NS];
@@ -1027,7 +1030,7 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
                                                               ClassParams cp, I8Params ip, FastParams fp,
                                                               uint32_t *amb) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const Mfma8sLane L = mfma8s_lane(ip, lane);
+    const Mfma8sLane<NS> L = mfma8s_lane<NS>(ip, lane);
     const int32_t T2k = ip.T2 * 32 + 31;
     __shared__ int64_t s_amb[4][kAmb8sCapW];  // vector index << 4 | undecided-pixel mask
     __shared__ uint32_t s_namb[4], s_npx[4];
@@ -1389,10 +1392,22 @@ int classify_choose(int nc, int path, bool fast_ok) {
 //   mfma8 123-128  126      128-129  149-153  176      277-281  280-283  341-342  340-341  407-413
 // The 4x4x4 form's cost grows with its row sets (two classes each), the
 // 32x32 form's with its ranked accumulator registers (8 for <= 16 classes,
-// 12 for <= 24, 16 for <= 32) and FAST32's linearly: MFMA8 below 9 classes,
-// at exactly 16 and from 20 (nc = 12 and, round 4, 17-19 stay on FAST32).
+// 12 for <= 24, 16 for <= 32) and FAST32's linearly. Late round 5, the
+// 4x4x4 form at 5-8 row sets (4 waves per SIMD; 3 at 8 sets) against both,
+// with 16 / 32 blocks per CU, two runs (profiles/raw/r5/small16/):
+//   nc        10         12         14         16
+//   fast    218-226    245-247    262-267    297
+//   4x4x4   229-232    238-240    253-254    286-287
+//   32x32   291-292    259-271    264        262-264
+// So the 4x4x4 form up to 14 classes (kMfma8sMaxClasses), the 32x32 form
+// above. AUTO over nc = 2 .. 32 with that rule (raw/r5/auto14/, µs): 9 201.6,
+// 10 208.2 (fast32), 11 225.0, 12 235.1, 13 250.9, 14 249.6 (4x4x4), 15
+// 284.0 (fast32 — the 32x32 form ranks the same 8 registers at 15 as at 16,
+// 262.5), 20 319.6, 32 377.0: MFMA8 below 9 classes, at 11-16 and from 20
+// (9-10 and 17-19 stay on FAST32).
 constexpr int kAutoMfma8MinClasses = 20;
-inline bool auto_mfma8(int nc) { return nc <= 8 || nc == 16 || nc >= kAutoMfma8MinClasses; }
+constexpr int kMfma8sMaxClasses = 14;
+inline bool auto_mfma8(int nc) { return nc <= 8 || (nc >= 11 && nc <= 16) || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.
@@ -1500,7 +1515,14 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
         const char *e = std::getenv("MPX_CLS_MFMA8_SMALL");
         return !(e && e[0] == '0');
     }();
-    if (chosen == MPX_CLS_MFMA8 && nc <= 8 && small8) {
+    // the small form up to kMfma8sMaxClasses; MPX_CLS_MFMA8S_MAX=k (8..16)
+    // moves the boundary (A/B; read once)
+    static const int small_max = [] {
+        const char *e = std::getenv("MPX_CLS_MFMA8S_MAX");
+        const int k = e ? std::atoi(e) : 0;
+        return k >= 8 && k <= 16 ? k : kMfma8sMaxClasses;
+    }();
+    if (chosen == MPX_CLS_MFMA8 && nc <= small_max && small8) {
         const int64_t nvec = npix / 4;
         if (nvec > 0) {
             const int64_t blocks = (nvec + 255) / 256;
@@ -1553,8 +1575,16 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
                 MPX_MFMA8S(2);
             else if (ns == 3)
                 MPX_MFMA8S(3);
-            else
+            else if (ns == 4)
                 MPX_MFMA8S(4);
+            else if (ns == 5)
+                MPX_MFMA8S_L(5, 1, 0);
+            else if (ns == 6)
+                MPX_MFMA8S_L(6, 1, 0);
+            else if (ns == 7)
+                MPX_MFMA8S_L(7, 1, 0);
+            else
+                MPX_MFMA8S_L(8, 1, 0);
 #undef MPX_MFMA8S
 #undef MPX_MFMA8S_L
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());

@@ -372,3 +372,36 @@ ckpt_r5_m8w() {
     LAB3_NCS=16,24,32 LAB3_PATHS=mfma8 bash tools/gpu.sh ab lab3 abl/libmpx_old.so 3 -- \
         python -u tools/experiments/lab3_ab.py
 }
+
+# AC: the 4x4x4 one-pixel-per-lane form at 9-16 classes (MPX_CLS_MFMA8S_MAX=16,
+# row sets 5-8) against the 32x32 form and fast32, nc = 10 / 12 / 14 / 16, twice
+ckpt_r5_small16() {
+    export O=${O:-gpurun_out/r5/small16}
+    mkdir -p "$O"
+    for r in 1 2; do
+        MPX_CLS_MFMA8S_MAX=16 LAB3_NCS=10,12,14,16 LAB3_PATHS=mfma8 LAB3_TAG=small_$r \
+            bash tools/gpu.sh run small_$r 300 python -u tools/experiments/lab3_ab.py &&
+        LAB3_NCS=10,12,14,16 LAB3_PATHS=mfma8,fast LAB3_TAG=base_$r \
+            bash tools/gpu.sh run base_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done
+}
+
+# AD: AUTO with the 4x4x4 form up to 14 classes: classifier GPU tests (nc 1-14
+# on the small form), then AUTO over nc = 2 .. 32 on three rotated images
+ckpt_r5_auto14() {
+    export O=${O:-gpurun_out/r5/auto14}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=2,4,8,9,10,11,12,13,14,15,16,20,32 LAB3_PATHS=auto LAB3_TAG=auto \
+        bash tools/gpu.sh run lab3_auto 400 python -u tools/experiments/lab3_ab.py
+}
+
+# AE: AUTO at nc = 15 (now the 32x32 form) and its neighbours, twice
+ckpt_r5_auto15() {
+    export O=${O:-gpurun_out/r5/auto15}
+    mkdir -p "$O"
+    for r in 1 2; do
+        LAB3_NCS=14,15,16,17 LAB3_PATHS=auto,fast LAB3_TAG=r$r \
+            bash tools/gpu.sh run lab3_auto_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done
+}
