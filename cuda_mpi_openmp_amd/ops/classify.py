@@ -49,15 +49,14 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``mfma64`` — fp64 MFMA distance GEMM (v_mfma_f64_16x16x4_f64);
       * ``mfma8``  — exact int8 MFMA distance GEMM (16-bit fixed-point weights
         in two int8 limbs, int32 keys): one pixel per lane on
-        v_mfma_i32_4x4x4_16b_i8 up to 14 classes, v_mfma_i32_32x32x16_i8
+        v_mfma_i32_4x4x4_16b_i8 up to 13 classes, v_mfma_i32_32x32x16_i8
         above;
-      * ``auto``   — ``mfma8`` below 9 classes, at 11-16 and from 20 (where
-        it measured faster on MI355X, round-5 sweeps at 8192^2, µs: nc = 4 123
-        vs 134, 8 172 vs 188, 12 235-240 vs 245-247, 14 250-254 vs 262-267,
-        15 ~262 vs 284, 16 262-267 vs 288-297, 32 376-381 vs 505-524; the
-        one-pixel-per-lane 4x4x4 form up to 14 classes, the 32x32 form above),
-        else ``fast`` (the f32 MFMA shares the VALU's fp32 datapath on gfx950;
-        fast32 wins at 9-10 and 17-19).
+      * ``auto``   — ``mfma8`` below 9 classes, at 15-16 and from 20 (where it
+        measured faster on MI355X, round-5 sweeps at 8192^2, µs: nc = 4 123
+        vs 134, 8 172 vs 188, 15 262 vs 279, 16 260-267 vs 288-297, 32
+        376-381 vs 505-524), else ``fast`` (the f32 MFMA shares the VALU's
+        fp32 datapath on gfx950; at 9-14 the int8 forms' lead over fast32 is
+        within the box-to-box spread or negative, and fast32 wins at 17-19).
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes

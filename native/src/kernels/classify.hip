@@ -926,7 +926,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
 //   Keys as in MFMA8: ((D_a << 8) + D_b) << 5 | class — two v_lshl_add per
 //   class — then the running top-2 in the lane; no cross-lane merge.
 //   NS = row sets (2 classes each) with real classes: 1 .. 7 up to
-//   kMfma8sMaxClasses = 14 classes (8 for MPX_CLS_MFMA8S_MAX=16, A/B).
+//   kMfma8sMaxClasses = 13 classes (8 for MPX_CLS_MFMA8S_MAX=16, A/B).
 // ---------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
@@ -1394,20 +1394,20 @@ int classify_choose(int nc, int path, bool fast_ok) {
 // 32x32 form's with its ranked accumulator registers (8 for <= 16 classes,
 // 12 for <= 24, 16 for <= 32) and FAST32's linearly. Late round 5, the
 // 4x4x4 form at 5-8 row sets (4 waves per SIMD; 3 at 8 sets) against both,
-// with 16 / 32 blocks per CU, two runs (profiles/raw/r5/small16/):
-//   nc        10         12         14         16
-//   fast    218-226    245-247    262-267    297
-//   4x4x4   229-232    238-240    253-254    286-287
-//   32x32   291-292    259-271    264        262-264
-// So the 4x4x4 form up to 14 classes (kMfma8sMaxClasses), the 32x32 form
-// above. AUTO over nc = 2 .. 32 with that rule (raw/r5/auto14/, µs): 9 201.6,
-// 10 208.2 (fast32), 11 225.0, 12 235.1, 13 250.9, 14 249.6 (4x4x4), 15
-// 284.0 (fast32 — the 32x32 form ranks the same 8 registers at 15 as at 16,
-// 262.5), 20 319.6, 32 377.0: MFMA8 below 9 classes, at 11-16 and from 20
-// (9-10 and 17-19 stay on FAST32).
+// with 16 / 32 blocks per CU, on four boxes (profiles/raw/r5/{small16,
+// auto14,auto15,mid}/), µs:
+//   nc        10        11        12        13        14        15       16
+//   fast    218-226   238-242   235-247   251-252   262-276   279      288-297
+//   4x4x4   229-232   262-263   223-240   246-251   245-290    —       286-287
+//   32x32   291-292   293-297   259-271   260-264   260-264   262      260-264
+// The 4x4x4 form beats the 32x32 form up to 13 classes on every box
+// (kMfma8sMaxClasses: explicit mfma8 runs it there); against FAST32 its lead
+// at 12-14 is within the box-to-box spread and it loses at 11, so AUTO keeps
+// FAST32 at 9-14 and 17-19 and takes MFMA8 below 9 classes, at 15-16 (the
+// 32x32 form ranks the same 8 registers at 15 as at 16) and from 20.
 constexpr int kAutoMfma8MinClasses = 20;
-constexpr int kMfma8sMaxClasses = 14;
-inline bool auto_mfma8(int nc) { return nc <= 8 || (nc >= 11 && nc <= 16) || nc >= kAutoMfma8MinClasses; }
+constexpr int kMfma8sMaxClasses = 13;
+inline bool auto_mfma8(int nc) { return nc <= 8 || nc == 15 || nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.

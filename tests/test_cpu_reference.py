@@ -150,12 +150,11 @@ def test_classify_plan_routes():
     assert ops.classify_plan(mu20, inv20, "auto")[0] == "mfma8"
     mu19, inv19 = stats(19)
     assert ops.classify_plan(mu19, inv19, "auto")[0] == "fast"
-    # 11-14 classes: the 4x4x4 form at 6-7 row sets, 15: the 32x32 form (late
-    # round 5); 9-10 stay on the packed-VALU path
-    for k in (11, 14, 15):
-        muk, invk = stats(k)
-        assert ops.classify_plan(muk, invk, "auto")[0] == "mfma8", k
-    for k in (9, 10):
+    # 15 classes: the 32x32 int8 form (late round 5); 9-14 stay on the
+    # packed-VALU path
+    mu15, inv15 = stats(15)
+    assert ops.classify_plan(mu15, inv15, "auto")[0] == "mfma8"
+    for k in (9, 11, 12, 14):
         muk, invk = stats(k)
         assert ops.classify_plan(muk, invk, "auto")[0] == "fast", k
     # at exactly 16 and from 20 classes AUTO runs the exact int8-MFMA distance

@@ -405,3 +405,16 @@ ckpt_r5_auto15() {
             bash tools/gpu.sh run lab3_auto_$r 300 python -u tools/experiments/lab3_ab.py || return 1
     done
 }
+
+# AF: 11-14 classes, the three forms side by side on one box, alternated
+# twice: 4x4x4 (mfma8 path, default), 32x32 (MPX_CLS_MFMA8S_MAX=8), fast32
+ckpt_r5_mid() {
+    export O=${O:-gpurun_out/r5/mid}
+    mkdir -p "$O"
+    for r in 1 2; do
+        LAB3_NCS=11,12,13,14 LAB3_PATHS=mfma8,fast LAB3_TAG=small_$r \
+            bash tools/gpu.sh run small_$r 300 python -u tools/experiments/lab3_ab.py &&
+        MPX_CLS_MFMA8S_MAX=8 LAB3_NCS=11,12,13,14 LAB3_PATHS=mfma8 LAB3_TAG=big_$r \
+            bash tools/gpu.sh run big_$r 300 python -u tools/experiments/lab3_ab.py || return 1
+    done
+}
