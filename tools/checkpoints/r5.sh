@@ -418,3 +418,12 @@ ckpt_r5_mid() {
             bash tools/gpu.sh run big_$r 300 python -u tools/experiments/lab3_ab.py || return 1
     done
 }
+
+# AG: the final AUTO rule: classifier GPU tests, AUTO at nc = 2 .. 32 once
+ckpt_r5_autofinal() {
+    export O=${O:-gpurun_out/r5/autofinal}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py tests/test_cpu_reference.py -k "classify" &&
+    LAB3_NCS=2,4,8,9,12,14,15,16,20,32 LAB3_PATHS=auto LAB3_TAG=auto \
+        bash tools/gpu.sh run lab3_auto 400 python -u tools/experiments/lab3_ab.py
+}
