@@ -121,6 +121,27 @@ def test_gpu_sort_matches_cpu(gpu, kind, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int_uniform", "int_range", "float_normal"])
+def test_gpu_sort_auto_at_2_26(gpu, kind):
+    """AUTO at 2^26 + 5 keys: 16384-key tiles (variant 22, one 1024-thread
+    block per CU), a partial last tile, hot-digit ranking on the skewed
+    passes — equal to torch.sort (no NaN / signed zeros in these inputs, where
+    torch's order and the IEEE total order agree)."""
+    n = (1 << 26) + 5
+    g = torch.Generator(device=gpu)
+    g.manual_seed(26)
+    if kind == "int_uniform":
+        x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=gpu, generator=g)
+    elif kind == "int_range":
+        x = torch.randint(0, 1000, (n,), dtype=torch.int32, device=gpu, generator=g)
+    else:
+        x = torch.randn(n, device=gpu, generator=g)
+    ref = torch.sort(x).values
+    ops.sort_(x)
+    assert torch.equal(x.view(torch.int32), ref.view(torch.int32))
+
+
+@pytest.mark.gpu
 def test_gpu_sort_lane_order_probe(gpu):
     """the production ranking's stability premise (same-address
     returning LDS adds in ascending lane order) is probed once per device;

@@ -427,3 +427,10 @@ ckpt_r5_autofinal() {
     LAB3_NCS=2,4,8,9,12,14,15,16,20,32 LAB3_PATHS=auto LAB3_TAG=auto \
         bash tools/gpu.sh run lab3_auto 400 python -u tools/experiments/lab3_ab.py
 }
+
+# AH: the 2^26-key AUTO sort tests
+ckpt_r5_sort26() {
+    export O=${O:-gpurun_out/r5/sort26}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_lab5_sort.py -k "auto_at_2_26 or lane_order"
+}
