@@ -32,9 +32,9 @@
 //     (stages > kTile as fused global half-cleaner passes, up to 3 per pass).
 //   * uint8 uses a counting sort: a per-block LDS histogram folded into 256
 //     global bin counts by one atomic per bin and block (hist_u8_kernel), then
-//     every block scans the 256 counts itself and writes its 16-B pieces of
-//     the output, each piece's value found by binary search over the bucket
-//     starts in LDS (fill_u8_kernel).
+//     every block scans the 256 counts itself and writes one contiguous run of
+//     16-B pieces of the output, a piece's value searched only among the
+//     buckets its run overlaps (fill_u8_kernel).
 //   * Scratch comes from a caller-provided workspace (mpx_sort_workspace_bytes
 //     / mpx_sort_ws): the Python op takes it from torch's caching allocator on
 //     the tensor's stream, so concurrent sorts on different streams or devices
@@ -182,12 +182,16 @@ __device__ inline int64_t u8_scalar_pos(int64_t i, int64_t head, int64_t tail0) 
 
 // Counting sort, step 1: per-block LDS histogram of the bytes, then one
 // global atomic per non-empty bin (ghist zeroed beforehand). Each thread keeps
-// two 16-B loads in flight.
+// four 16-B loads in flight. The histogram has 32 copies of every bin, copy
+// lane % 32 at word bin * 32 + lane % 32: each 32-lane half of an atomic then
+// touches 32 distinct banks. (One shared 256-word histogram put random bytes
+// ~3.5 deep on the busiest bank: 22.9 us at 2^26, LDS-bound.)
 __global__ __launch_bounds__(1024) void hist_u8_kernel(const uint8_t *__restrict__ x, int64_t n, int64_t head,
                                                        int64_t nvec, uint32_t *__restrict__ ghist) {
-    __shared__ uint32_t h[256];
-    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __shared__ uint32_t h[256 * 32];
+    for (int k = threadIdx.x; k < 256 * 32; k += 1024) h[k] = 0;
     __syncthreads();
+    const uint32_t lane32 = threadIdx.x & 31u;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint4 *v = reinterpret_cast<const uint4 *>(x + head);
@@ -196,23 +200,32 @@ __global__ __launch_bounds__(1024) void hist_u8_kernel(const uint8_t *__restrict
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) atomicAdd(&h[(w[k] >> (8 * b)) & 255u], 1u);
+            for (int b = 0; b < 4; ++b) atomicAdd(&h[(((w[k] >> (8 * b)) & 255u) << 5) | lane32], 1u);
     };
     int64_t i = gid;
-    for (; i + stride < nvec; i += 2 * stride) {
-        const uint4 q0 = v[i], q1 = v[i + stride];
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        const uint4 q0 = v[i], q1 = v[i + stride], q2 = v[i + 2 * stride], q3 = v[i + 3 * stride];
         count(q0);
         count(q1);
+        count(q2);
+        count(q3);
     }
-    if (i < nvec) count(v[i]);
+    for (; i < nvec; i += stride) count(v[i]);
     const int64_t tail0 = head + 16 * nvec;
-    for (int64_t j = gid; j < head + (n - tail0); j += stride) atomicAdd(&h[x[u8_scalar_pos(j, head, tail0)]], 1u);
+    for (int64_t j = gid; j < head + (n - tail0); j += stride)
+        atomicAdd(&h[((uint32_t)x[u8_scalar_pos(j, head, tail0)] << 5) | lane32], 1u);
     __syncthreads();
-    if (threadIdx.x < 256 && h[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], h[threadIdx.x]);
+    if (threadIdx.x < 256) {
+        const int t = threadIdx.x;
+        uint32_t c = 0;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) c += h[(t << 5) | ((j + t) & 31)];  // rotated: 32 banks per half
+        if (c) atomicAdd(&ghist[t], c);
+    }
 }
 
-__device__ inline int u8_value_at(const int64_t *start, int64_t o) {
-    int lo = 0, hi = 255;  // largest v with start[v] <= o
+__device__ inline int u8_value_at(const int64_t *start, int64_t o, int lo = 0, int hi = 255) {
+    // largest v in [lo, hi] with start[v] <= o (start[lo] <= o given)
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (start[mid] <= o) lo = mid;
@@ -222,8 +235,11 @@ __device__ inline int u8_value_at(const int64_t *start, int64_t o) {
 }
 
 // step 2: every block scans the 256 global bin counts itself (exclusive
-// prefix in LDS: no separate scan launch), then writes its 16-B pieces of the
-// sorted output
+// prefix in LDS: no separate scan launch), then writes one contiguous run of
+// 16-B pieces of the sorted output, 4 KiB per block-wide store. A piece's
+// value is searched only between the buckets of the run's first and last
+// byte: no search at all when one bucket covers the run (a bucket spans
+// n / 256 bytes of uniform input, a run nvec / grid pieces).
 __global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, int64_t n, int64_t head,
                                                       int64_t nvec, const uint32_t *__restrict__ ghist) {
     __shared__ int64_t start[257];
@@ -248,9 +264,13 @@ __global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, i
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint4 *v = reinterpret_cast<uint4 *>(x + head);
-    for (int64_t i = gid; i < nvec; i += stride) {
+    const int64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const int64_t c0 = (int64_t)blockIdx.x * per, c1 = min(c0 + per, nvec);
+    const int b0 = c0 < c1 ? u8_value_at(start, head + 16 * c0) : 0;
+    const int b1 = c0 < c1 ? u8_value_at(start, head + 16 * c1 - 1, b0) : 0;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
         const int64_t o = head + 16 * i;
-        int val = u8_value_at(start, o);
+        int val = u8_value_at(start, o, b0, b1);
         if (start[val + 1] > o + 15) {  // the whole 16-B piece lies in one bucket (all but ~256 pieces)
             const uint32_t r = (uint32_t)val * 0x01010101u;
             v[i] = make_uint4(r, r, r, r);

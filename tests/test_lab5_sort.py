@@ -208,6 +208,20 @@ def test_gpu_sort_u8_unaligned(gpu, offset, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [33, 1_000, 65_537, 1 << 22, 50_000_017])
+def test_gpu_sort_u8_skewed(gpu, n):
+    """uint8 counting sort on skewed bytes: most bins empty, one bin holding
+    most keys, single-key bins, bucket edges inside a 16-B piece and across
+    the per-wave runs of the fill."""
+    rng = np.random.default_rng(n)
+    a = rng.choice(np.array([0, 1, 7, 128, 200, 255], dtype=np.uint8), n, p=[0.02, 0.6, 0.1, 0.25, 0.02, 0.01])
+    a[rng.integers(0, n, 3)] = [3, 99, 254]
+    d = torch.from_numpy(a.copy()).to(gpu)
+    ops.sort_(d)
+    assert d.cpu().numpy().tobytes() == np.sort(a).tobytes()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pattern", ["equal", "sorted", "reversed", "two_values", "high_byte_only"])
 def test_gpu_radix_sort_patterns(gpu, pattern):
     """Radix-specific digit distributions: a single digit value in every pass

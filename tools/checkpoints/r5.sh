@@ -434,3 +434,19 @@ ckpt_r5_sort26() {
     mkdir -p "$O"
     bash tools/gpu.sh tests tests/test_lab5_sort.py -k "auto_at_2_26 or lane_order"
 }
+
+# AI: uint8 counting sort at 2^26: kernel trace (hist vs fill split)
+ckpt_r5_u8() {
+    export O=${O:-gpurun_out/r5/u8}
+    mkdir -p "$O"
+    LAB5_DTYPES=uint8 LAB5_LOGN=26 LAB5_VARIANTS=0 bash tools/gpu.sh prof u8_trace -- python tools/experiments/lab5_bench.py &&
+    python tools/experiments/kprof_table.py "$O" --grep u8 > "$O/kernels_table.md" && find "$O" -name "*.db" -delete
+}
+
+ckpt_r5_u8b() {
+    export O=${O:-gpurun_out/r5/u8b}
+    mkdir -p "$O"
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lab5_sort.py -m gpu -k "u8 or uchar" > "$O/tests.log" 2>&1 &&
+    LAB5_DTYPES=uint8 LAB5_LOGN=26 LAB5_VARIANTS=0 bash tools/gpu.sh prof u8_trace -- python tools/experiments/lab5_bench.py &&
+    python tools/experiments/kprof_table.py "$O" --grep u8 > "$O/kernels_table.md" && find "$O" -name "*.db" -delete
+}
