@@ -450,3 +450,11 @@ ckpt_r5_u8b() {
     LAB5_DTYPES=uint8 LAB5_LOGN=26 LAB5_VARIANTS=0 bash tools/gpu.sh prof u8_trace -- python tools/experiments/lab5_bench.py &&
     python tools/experiments/kprof_table.py "$O" --grep u8 > "$O/kernels_table.md" && find "$O" -name "*.db" -delete
 }
+
+# AJ: uint8 counting sort at 2^26 after the bank-spread histogram: trace + counters
+ckpt_r5_u8p() {
+    export O=${O:-gpurun_out/r5/u8p}
+    mkdir -p "$O"
+    LAB5_DTYPES=uint8 LAB5_LOGN=26 LAB5_VARIANTS=0 bash tools/gpu.sh profile u8 -- python tools/experiments/lab5_bench.py &&
+    python tools/experiments/kprof_table.py "$O" --grep u8 > "$O/kernels_table.md" && find "$O" -name "*.db" -delete
+}
