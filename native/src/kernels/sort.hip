@@ -9,7 +9,7 @@
 //     bit patterns: -NaN < -inf < ... < -0 < +0 < ... < +inf < +NaN.
 //   * n > kTile: LSD radix sort, 8-bit digits, 4 passes (radix_sort32), in
 //     one of two forms chosen by n:
-//       - n <= kOnesweepMaxN (2^18), onesweep: one histogram pass builds all
+//       - onesweep (variant 1; AUTO up to 2^18 keys before round 5): one histogram pass builds all
 //         four 256-bin digit histograms at once; each digit pass is ONE kernel
 //         in which a block takes the next 8192-key tile from an atomic tile
 //         counter, ranks its keys stably in LDS (per-wave peer masks of equal
@@ -17,7 +17,7 @@
 //         per-wave digit counters), resolves its global digit offsets by
 //         decoupled look-back (flag + count in one 32-bit word), then stages
 //         the tile in LDS in digit order and writes it out in runs per digit;
-//       - larger n, reduce-then-scan: per pass a count kernel (per-tile digit
+//       - AUTO, reduce-then-scan: per pass a count kernel (per-tile digit
 //         counts), a scan kernel (per-tile offsets and digit totals) and a
 //         persistent scatter kernel (radix_scatter_lean_kernel: 2 blocks per
 //         CU walking XCD-local tiles, next tile prefetched while this one is
@@ -1477,7 +1477,7 @@ RadixWs radix_layout(void *ws, int64_t n) {
 // cross-XCD round trip on MI355X is long (agent-scope loads miss the per-XCD
 // L2), so once many tiles are in flight the chain, not HBM, bounds onesweep;
 // reduce-then-scan re-reads each tile once more but never waits.
-constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // measured crossover (profiles/lab5_sort.md)
+constexpr int64_t kOnesweepMaxN = (int64_t)1 << 18;  // onesweep's AUTO range before round 5; the probe's lower bound
 constexpr int64_t kTile4kMaxN = (int64_t)1 << 23;    // 4096-key tiles up to here (2^24: 0.187 ms both ways)
 constexpr int64_t kTile16kMinN = (int64_t)1 << 26;   // 16384-key tiles from here (variant 22)
 
@@ -1577,7 +1577,9 @@ int radix_sort32(uint32_t *x, int64_t n, int mode, void *ws, int variant, hipStr
     // (22: longer digit runs, fewer partial output lines; 2^26 int32 0.689-0.697
     // vs 0.706 ms, but 10 % slower at 2^24 with one block per CU); uniform
     // passes run the round-4 code (12 / 13)
-    if (variant == 0) variant = n <= kOnesweepMaxN ? 1 : n <= kTile4kMaxN ? 21 : n < kTile16kMinN ? 20 : 22;
+    // (21 also below 2^18 since round 5: 0.059-0.062 vs onesweep's 0.068-0.082 ms
+    // from 2^14 to 2^18 keys, profiles/raw/r5/l5small/)
+    if (variant == 0) variant = n <= kTile4kMaxN ? 21 : n < kTile16kMinN ? 20 : 22;
     // the returning-add ranking needs ascending lane order (probe above)
     const bool rtn_rank = (variant >= 9 && variant <= 22);
     if (rtn_rank && lds_rtn_order_ok(s) != 1) {
@@ -1815,7 +1817,7 @@ int sort_impl(void *data, int64_t n, int dtype, void *ws, int64_t ws_bytes, void
 // Convenience form without a caller workspace (tools, one-off sorts): the
 // scratch is allocated for this call and freed after the stream drains.
 // Did a look-back wait of the last sort in `ws` give up (kSpinLimit)? Only
-// the onesweep schedule (n <= kOnesweepMaxN) waits; its predecessors are
+// the onesweep schedule (variant 1, on request) waits; its predecessors are
 // always resident (tile ids in launch order), so this is a hardware-fault
 // detector. Synchronous: call after the sort's stream has drained.
 int sort_ws_status(const void *ws, int64_t n, int dtype) {

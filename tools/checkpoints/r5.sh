@@ -458,3 +458,11 @@ ckpt_r5_u8p() {
     LAB5_DTYPES=uint8 LAB5_LOGN=26 LAB5_VARIANTS=0 bash tools/gpu.sh profile u8 -- python tools/experiments/lab5_bench.py &&
     python tools/experiments/kprof_table.py "$O" --grep u8 > "$O/kernels_table.md" && find "$O" -name "*.db" -delete
 }
+
+# AK: AUTO without onesweep (21 from 2^14 keys): lab5 GPU tests + small-n bench
+ckpt_r5_small() {
+    export O=${O:-gpurun_out/r5/small}
+    mkdir -p "$O"
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lab5_sort.py tests/test_gpu_kernels.py -m gpu > "$O/tests.log" 2>&1 &&
+    LAB5_DTYPES=int32,float32 LAB5_LOGN=12,14,16,17,18,19,20 LAB5_VARIANTS=1,21 LAB5_ITERS=30 timeout -k 10 300 python tools/experiments/lab5_bench.py > "$O/bench.log" 2>&1
+}

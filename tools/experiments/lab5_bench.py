@@ -64,7 +64,8 @@ def main():
             if dt != torch.uint8:
                 for v, nm in ((1, "onesweep"), (2, "reduce_scan"), (4, "reduce_scan_persistent_r2"),
                               (7, "lean_scatter"), (8, "lean_scatter_tile4096"), (9, "lean_rtn_rank"),
-                              (10, "lean_rtn_rank_tile4096")):
+                              (10, "lean_rtn_rank_tile4096"), (20, "hot_rank"), (21, "hot_rank_tile4096"),
+                              (22, "hot_rank_tile16384")):
                     if v not in only:
                         continue
                     try:
