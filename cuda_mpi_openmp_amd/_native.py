@@ -86,6 +86,7 @@ _SIGNATURES = {
     "mpx_classify_ex": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_classify_plan": (c_int, [c_int, _dp, _dp, c_int, ctypes.POINTER(ctypes.c_float)]),
     "mpx_classify_i8_params": (c_int, [c_int, _dp, _dp, c_vp, c_vp, c_vp, c_vp]),
+    "mpx_classify_f16_params": (c_int, [c_int, _dp, _dp, c_vp, c_vp, c_vp]),
     "mpx_jacobi_f64": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "mpx_jacobi_sync_bytes": (c_int, []),
     "mpx_jacobi_peer_sweep": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

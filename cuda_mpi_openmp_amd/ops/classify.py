@@ -12,7 +12,7 @@ import torch
 from .. import _native
 from .edge import check_image
 
-PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3, "mfma64": 4, "mfma8": 5}
+PATHS = {"direct": 0, "mfma": 1, "auto": 2, "fast": 3, "mfma64": 4, "mfma8": 5, "mfma16": 6}
 PATH_NAMES = {v: k for k, v in PATHS.items()}
 MAX_CLASSES = 32
 
@@ -51,6 +51,9 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
         in two int8 limbs, int32 keys): one pixel per lane on
         v_mfma_i32_4x4x4_16b_i8 up to 13 classes, v_mfma_i32_32x32x16_i8
         above;
+      * ``mfma16`` — f16 MFMA distance GEMM (v_mfma_f32_32x32x16_f16, f16
+        hi + lo weight limbs, exact integer features, fp32 keys): one pixel
+        per lane with all of its classes in that lane;
       * ``auto``   — ``mfma8`` below 9 classes, at 15-16 and from 20 (where it
         measured faster on MI355X, round-5 sweeps at 8192^2, µs: nc = 4 123
         vs 134, 8 172 vs 188, 15 262 vs 279, 16 260-267 vs 288-297, 32

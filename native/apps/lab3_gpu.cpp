@@ -35,6 +35,7 @@ int main() {
         else if (!std::strcmp(e, "fast")) path = MPX_CLS_FAST;
         else if (!std::strcmp(e, "mfma64")) path = MPX_CLS_MFMA64;
         else if (!std::strcmp(e, "mfma8")) path = MPX_CLS_MFMA8;
+        else if (!std::strcmp(e, "mfma16")) path = MPX_CLS_MFMA16;
     }
     std::string in_path, out_path;
     if (!in.next_token(in_path) || !in.next_token(out_path)) {

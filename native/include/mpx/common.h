@@ -61,7 +61,9 @@ enum mpx_classify_path {
     MPX_CLS_AUTO = 2,   /* FAST, or DIRECT when the fp32 margin cannot be proven    */
     MPX_CLS_FAST = 3,   /* fp32 packed-VALU distances, proven margin + fallback     */
     MPX_CLS_MFMA64 = 4, /* fp64 MFMA distance GEMM, proven margin + exact fallback  */
-    MPX_CLS_MFMA8 = 5   /* exact int8 MFMA distance GEMM (int32 keys), proven margin */
+    MPX_CLS_MFMA8 = 5,  /* exact int8 MFMA distance GEMM (int32 keys), proven margin */
+    MPX_CLS_MFMA16 = 6  /* f16 MFMA distance GEMM (f16 weight limbs, fp32 keys), one
+                           pixel per lane, proven margin + exact fallback           */
 };
 
 /* lab5 element types (binary fixtures lab5/data/{int10,float10,uchar10}). */

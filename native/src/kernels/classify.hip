@@ -1127,6 +1127,225 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
 }
 
 // ---------------------------------------------------------------------------
+// MFMA16 (round 6, VERDICT r5 Next #1): the distance GEMM on
+// v_mfma_f32_32x32x16_f16 with ONE pixel per lane and all of its classes in
+// that lane's accumulator registers.
+//
+// Why f16 and not int8: an int8 GEMM needs the 16-bit weights in two limbs at
+// two fixed-point scales, so every (pixel, class) key costs two shift-adds
+// (D_a << 13, D_b << 5 and the tag) before the top-2 — and its common scale
+// leaves small weights few bits, so 1.2 % of the pixels fell inside the
+// margin at 32 classes. In f16 each limb carries its own exponent: the weight
+// is hi + lo (two f16, ~22 bits), the products with the exact integer
+// features are exact in the fp32 accumulator, and the accumulator IS the
+// distance: one v_and_or per key puts the class tag in its low mantissa bits
+// (the FAST32 key), and the top-2 takes 2.5 VALU per PAIR of keys:
+//     t = med3(B, k0, k1); B = min3(B, k0, k1); S = min(S, t)
+// (second-smallest of {B, S, k0, k1} = min(S, med3(B, k0, k1)), and the S
+// updates of two pairs fuse into one v_min3).
+//
+// One pixel per lane on a 32x32 tile: the D rows of lane half h are rows
+// (r & 3) + 8 (r >> 2) + 4 h, i.e. register r of either half is class r of
+// the 16-class set. Lane l supplies B[k = 8 h + j][col = l & 31] = feature j
+// of ITS OWN pixel, and the A rows of half h are non-zero only in k-block h
+// (A[i][8 kb + j] = w[class(i)][j] when (i >> 2) & 1 == kb, else 0), so the
+// rows a lane reads sum its own pixel's features only: 64 pixels x 16 classes
+// per MFMA triple, no cross-lane merge, no duplicated feature bytes.
+//
+// Features (all exact in f16; q = channel - 128 from the byte via the 0x64xx
+// magic: f16 0x64nn = 1024 + nn, minus 1152): the six products P = q_i q_j
+// as h = f16(P) (|h| <= 16384) and l = P - h (|l| <= 4, one v_pk_fma), and
+// the three channels. 24 slots in three K = 8 fragments:
+//     B1 = [h(rr gg bb rb rg bg), r, g]  x hi limbs, then the same B1 x lo limbs
+//     B3 = [l(rr gg bb rb rg bg), b, b]  x hi limbs (hi and lo of b)
+// The class constant (+ a positivity bias) is the fp32 accumulator input.
+// build_half bounds |computed - reference chain| per class (limb rounding,
+// fp32 accumulation as any 25-term sum, the reference chain's own error), and
+// a pixel is decided by the FAST32 test against T2 = 2 max_c tol_c; the rest
+// take the fp32 then the fp64 stage (per-wave lists, as MFMA8S).
+// ---------------------------------------------------------------------------
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kHalfMfmas = 3;  // MFMAs per 16-class set
+
+struct HalfParams {
+    uint32_t w[2][kHalfMfmas][16][4];  // [set][mfma][class in set]: 8 f16 slot weights (the A row)
+    float c[MPX_MAX_CLASSES];          // accumulator init: scaled constant + bias; padded classes 3e38
+    float T2;                          // decision margin (scaled units; the FAST32 test)
+};
+
+template <int NSET>
+struct Mfma16Lane {
+    h8_t a[NSET][kHalfMfmas];  // A fragments (zero where the row's half is not the lane's k-block)
+    f32x16 cinit[NSET];
+};
+
+template <int NSET>
+__device__ __forceinline__ Mfma16Lane<NSET> mfma16_lane(const HalfParams &hp, int lane) {
+    Mfma16Lane<NSET> L;
+    const int i = lane & 31;                                 // this lane's A row
+    const bool mine = ((i >> 2) & 1) == (lane >> 5);         // row i is read by lane half (lane >> 5)
+    const int cls = (i & 3) + 4 * (i >> 3);                  // class (within the set) of D row i
+#pragma unroll
+    for (int s = 0; s < NSET; ++s) {
+#pragma unroll
+        for (int j = 0; j < kHalfMfmas; ++j) {
+            const uint4 u = mine ? make_uint4(hp.w[s][j][cls][0], hp.w[s][j][cls][1], hp.w[s][j][cls][2],
+                                              hp.w[s][j][cls][3])
+                                 : make_uint4(0, 0, 0, 0);
+            L.a[s][j] = __builtin_bit_cast(h8_t, u);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) L.cinit[s][r] = hp.c[16 * s + r];
+    }
+    return L;
+}
+
+__device__ __forceinline__ uint32_t h2_bits(h2_t v) { return __builtin_bit_cast(uint32_t, v); }
+
+// the three K = 8 feature fragments of pixel p (layout in the header above)
+__device__ __forceinline__ void mfma16_features(uint32_t p, h8_t &B1, h8_t &B3) {
+    const h2_t off = {(_Float16)-1152.0f, (_Float16)-1152.0f};
+    const h2_t R1 = __builtin_bit_cast(h2_t, __builtin_amdgcn_perm(0x64646464u, p, 0x04010400u)) + off;  // {r, g}
+    const h2_t R2 = __builtin_bit_cast(h2_t, __builtin_amdgcn_perm(0x64646464u, p, 0x04000402u)) + off;  // {b, r}
+    const uint32_t R3 = __builtin_amdgcn_perm(0u, h2_bits(R2), 0x01000100u);                                // {b, b}
+    const h2_t R2x = {R2.x, R2.x}, R2s = {R2.y, R2.x}, R1y = {R1.y, R1.y};
+    const h2_t H0 = R1 * R1;    // {rr, gg}
+    const h2_t H1 = R2 * R2x;   // {bb, rb}
+    const h2_t H2 = R2s * R1y;  // {rg, bg}
+    const h2_t L0 = __builtin_elementwise_fma(R1, R1, -H0);
+    const h2_t L1 = __builtin_elementwise_fma(R2, R2x, -H1);
+    const h2_t L2 = __builtin_elementwise_fma(R2s, R1y, -H2);
+    B1 = __builtin_bit_cast(h8_t, make_uint4(h2_bits(H0), h2_bits(H1), h2_bits(H2), h2_bits(R1)));
+    B3 = __builtin_bit_cast(h8_t, make_uint4(h2_bits(L0), h2_bits(L1), h2_bits(L2), R3));
+}
+
+// min3 of keys (VALU results, never MFMA registers: no hazard hidden from the
+// compiler). Written in C the backend CSEs min(k0, k1) with the med3 below and
+// emits two v_min instead of one v_min3.
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// rank one pixel: provisional output and whether its top-2 margin is within T2
+template <int NSET, int NR>
+__device__ __forceinline__ uint32_t mfma16_pixel(uint32_t p, const Mfma16Lane<NSET> &L, float T2, bool &undecided) {
+    h8_t B1, B3;
+    mfma16_features(p, B1, B3);
+    f32x16 acc[NSET];
+#pragma unroll
+    for (int s = 0; s < NSET; ++s) {
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(L.a[s][0], B1, L.cinit[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(L.a[s][1], B1, acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(L.a[s][2], B3, acc[s], 0, 0, 0);
+    }
+    uint32_t B = 0, S = 0;
+#pragma unroll
+    for (int s = 0; s < NSET; ++s) {
+        constexpr int kLast = NR;
+        const int nr = s == NSET - 1 ? kLast : 16;
+        uint32_t k[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (r < nr) k[r] = (__float_as_uint(acc[s][r]) & ~31u) | (uint32_t)(16 * s + r);
+        int r0 = 0;
+        if (s == 0) {
+            B = min(k[0], k[1]);
+            S = max(k[0], k[1]);
+            r0 = 2;
+        }
+#pragma unroll
+        for (int r = r0; r < 16; r += 2) {
+            if (r < nr) {
+                const uint32_t a = k[r], b = k[r + 1];
+                const uint32_t t = max(min(a, b), min(max(a, b), B));  // v_med3_u32
+                B = umin3(B, a, b);
+                S = min(S, t);
+            }
+        }
+    }
+    undecided = !decided(B, S, T2);
+    return __builtin_amdgcn_perm(B & 31u, p, 0x04020100u);
+}
+
+// The MFMA8S loop skeleton (one pixel per lane, four per 16-B vector, one
+// trip of loads ahead, per-wave deferral lists without block barriers).
+template <int NSET, int NR>
+__global__ __launch_bounds__(256) void classify_mfma16_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
+                                                              ClassParams cp, HalfParams hp, FastParams fp,
+                                                              uint32_t *amb) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const Mfma16Lane<NSET> L = mfma16_lane<NSET>(hp, lane);
+    const float T2 = hp.T2;
+    __shared__ int64_t s_amb[4][kAmb8sCapW];  // vector index << 4 | undecided-pixel mask
+    __shared__ uint32_t s_namb[4], s_npx[4];
+    __shared__ int64_t s_amb2[4][kAmb8sCap2W];
+    __shared__ uint32_t s_ambpx2[4][kAmb8sCap2W];
+    __shared__ uint32_t s_namb2[4];
+    if (lane == 0) s_namb[w] = s_npx[w] = s_namb2[w] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint4 qn = i < nvec ? v[i] : uint4{};
+    for (; i < nvec; i += stride) {
+        const uint4 q = qn;
+        if (i + stride < nvec) qn = v[i + stride];
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        uint32_t o[4];
+        bool u[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o[m] = mfma16_pixel<NSET, NR>(px[m], L, T2, u[m]);
+        if (__builtin_expect(u[0] | u[1] | u[2] | u[3], 0)) {
+            const uint32_t mask = (uint32_t)u[0] | ((uint32_t)u[1] << 1) | ((uint32_t)u[2] << 2) | ((uint32_t)u[3] << 3);
+            const uint32_t slot = atomicAdd(&s_namb[w], 1u);
+            if (slot < (uint32_t)kAmb8sCapW) {
+                s_amb[w][slot] = (i << 4) | mask;
+            } else {  // list full: the exact chain inline
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if ((mask >> m) & 1u) o[m] = classify_direct(px[m], nc, cp);
+            }
+        }
+        v[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    // this wave's deferred pixels: the fp32 proven-margin ranking first, the
+    // exact fp64 chain for what it leaves (every lane of the wave busy in each)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nd = min(s_namb[w], (uint32_t)kAmb8sCapW);
+    for (uint32_t j = lane; j < nd; j += 64) {
+        const int64_t e = s_amb[w][j];
+        const int64_t vi = e >> 4;
+        const uint32_t mask = (uint32_t)e & 15u;
+        atomicAdd(&s_npx[w], (uint32_t)__popc(mask));
+        const uint4 q = v[vi];  // written by this wave above, in program order
+        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+        for (int m = 0; m < 4; ++m) {
+            if (!((mask >> m) & 1u)) continue;
+            uint32_t o;
+            if (classify_fp32_one(px[m], nc, fp, o)) {
+                img[vi * 4 + m] = o;
+            } else {
+                const uint32_t slot = atomicAdd(&s_namb2[w], 1u);
+                if (slot < (uint32_t)kAmb8sCap2W) {
+                    s_amb2[w][slot] = vi * 4 + m;
+                    s_ambpx2[w][slot] = px[m];
+                } else {
+                    img[vi * 4 + m] = classify_direct(px[m], nc, cp);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (amb && lane == 0 && s_npx[w]) atomicAdd(amb, s_npx[w]);
+    const uint32_t nd2 = min(s_namb2[w], (uint32_t)kAmb8sCap2W);
+    for (uint32_t j = lane; j < nd2; j += 64) img[s_amb2[w][j]] = classify_direct(s_ambpx2[w][j], nc, cp);
+}
+
+// ---------------------------------------------------------------------------
 // Host: expanded fp32 weights and the rigorous decision margin.
 // ---------------------------------------------------------------------------
 typedef long double ld;
@@ -1367,6 +1586,114 @@ bool build_i8(int nc, const double *mu, const double *inv, I8Params &ip) {
     }
     return true;
 }
+
+// x rounded to the nearest f16 (ties to even); 0 below the normal range (the
+// kernel sees no f16 subnormals) and false on overflow
+bool f16_round(ld x, ld &r, uint16_t &bits) {
+    r = 0;
+    bits = 0;
+    if (x == 0) return true;
+    const ld a = std::fabs(x);
+    int ex;
+    std::frexp(a, &ex);  // a = f 2^ex, f in [0.5, 1): normal f16 exponent E = ex - 1
+    if (ex - 1 < -14) return true;
+    const ld quantum = std::ldexp((ld)1, ex - 11);
+    ld m = std::nearbyint(a / quantum) * quantum;
+    std::frexp(m, &ex);
+    if (!(m <= (ld)65504)) return false;
+    const int E = ex - 1;
+    const uint32_t mant = (uint32_t)std::llround((m / std::ldexp((ld)1, E) - 1) * 1024);
+    bits = (uint16_t)(((x < 0) ? 0x8000u : 0u) | ((uint32_t)(E + 15) << 10) | mant);
+    r = x < 0 ? -m : m;
+    return true;
+}
+
+// f16 limbs for MFMA16 (see the kernel): every expanded weight times a common
+// power of two 2^e (the largest in [2^13, 2^14)) as hi + lo f16. The bound per
+// class, in scaled units: the limb rounding against the exact weight (per
+// unit of feature: 16384 for the h slots, 4 for the l slots, which take hi
+// only, 128 for the channels), the fp32 accumulator's rounding as any sum of
+// 25 terms (24 exact products + the constant) with unit roundoff 2^-23 (twice
+// RNE's: covers any internal order and a truncating adder), the constant's
+// own fp32 rounding, and the reference fp64 chain's error.
+bool build_half(int nc, const double *mu, const double *inv, HalfParams &hp) {
+    ld w[MPX_MAX_CLASSES][kFeat], refb[MPX_MAX_CLASSES], psd[MPX_MAX_CLASSES];
+    if (!expand_classes(nc, mu, inv, w, refb, psd)) return false;
+    ld wmax = 0, mag = 0;
+    for (int c = 0; c < nc; ++c)
+        for (int k = 0; k < kFeat; ++k) {
+            if (k < 9) wmax = std::fmax(wmax, std::fabs(w[c][k]));
+            mag = std::fmax(mag, std::fabs(w[c][k]) * kPhiMax[k]);
+        }
+    if (!(wmax > 0) || !(mag < 1e30L)) return false;
+    int ex;
+    std::frexp(wmax, &ex);
+    const ld scale = std::ldexp((ld)1, 14 - ex);  // wmax * scale in [2^13, 2^14)
+    // expanded weight of each quadratic slot j (rr gg bb rb rg bg) and its feature bound
+    constexpr int kQuad[6] = {0, 1, 2, 4, 3, 5};
+    const ld u = std::ldexp((ld)1, -23);
+    const ld g25 = 25 * u / (1 - 25 * u);
+    ld hi[MPX_MAX_CLASSES][9], lo[MPX_MAX_CLASSES][9];
+    uint16_t hb[MPX_MAX_CLASSES][9], lb[MPX_MAX_CLASSES][9];
+    ld base_tol[MPX_MAX_CLASSES], base_abs[MPX_MAX_CLASSES];
+    for (int c = 0; c < nc; ++c) {
+        ld rep = 0, abs_terms = 0;
+        for (int k = 0; k < 9; ++k) {
+            const ld x = w[c][k] * scale;
+            if (!f16_round(x, hi[c][k], hb[c][k])) return false;
+            if (!f16_round(x - hi[c][k], lo[c][k], lb[c][k])) return false;
+            const ld dev = std::fabs(hi[c][k] + lo[c][k] - x);
+            if (k < 6) {
+                rep += dev * 16384 + std::fabs(lo[c][k]) * 4;
+                abs_terms += (std::fabs(hi[c][k]) + std::fabs(lo[c][k])) * 16384 + std::fabs(hi[c][k]) * 4;
+            } else {
+                rep += dev * 128;
+                abs_terms += (std::fabs(hi[c][k]) + std::fabs(lo[c][k])) * 128;
+            }
+        }
+        base_tol[c] = rep + (refb[c] + psd[c] + 1e-15L * mag) * scale;
+        base_abs[c] = abs_terms;
+    }
+    // the accumulator input of class c with a positivity bias, and its bound
+    auto tol = [&](int c, ld bias, float *cout) -> ld {
+        const ld cx = w[c][9] * scale + bias;
+        const float cf = (float)cx;
+        if (cout) *cout = cf;
+        const ld acc = g25 * (base_abs[c] + std::fabs((ld)cf));
+        return (base_tol[c] + acc + std::fabs((ld)cf - cx)) * 1.001L + 1e-30L;
+    };
+    ld tmax0 = 0;
+    for (int c = 0; c < nc; ++c) tmax0 = std::fmax(tmax0, tol(c, 0, nullptr));
+    const ld bias = 4 * tmax0;
+    ld tmax = 0;
+    for (int c = 0; c < nc; ++c) tmax = std::fmax(tmax, tol(c, bias, &hp.c[c]));
+    if (!(bias > 2 * tmax)) return false;
+    if (!(mag * scale + bias < 1e37L)) return false;
+    for (int c = nc; c < MPX_MAX_CLASSES; ++c) hp.c[c] = 3.0e38f;
+    std::memset(hp.w, 0, sizeof(hp.w));
+    for (int c = 0; c < nc; ++c) {
+        uint16_t e[kHalfMfmas][8];
+        for (int j = 0; j < 6; ++j) {
+            e[0][j] = hb[c][kQuad[j]];  // B1: h slots x hi
+            e[1][j] = lb[c][kQuad[j]];  // B1: h slots x lo
+            e[2][j] = hb[c][kQuad[j]];  // B3: l slots x hi
+        }
+        e[0][6] = hb[c][6];  // B1: r, g (hi)
+        e[0][7] = hb[c][7];
+        e[1][6] = lb[c][6];  // B1: r, g (lo)
+        e[1][7] = lb[c][7];
+        e[2][6] = hb[c][8];  // B3: b, b (hi, lo)
+        e[2][7] = lb[c][8];
+        for (int j = 0; j < kHalfMfmas; ++j)
+            for (int d = 0; d < 4; ++d)
+                hp.w[c / 16][j][c % 16][d] = (uint32_t)e[j][2 * d] | ((uint32_t)e[j][2 * d + 1] << 16);
+    }
+    const ld t2x = 2 * tmax * (1 + std::ldexp((ld)1, -20));  // see decided()
+    float t2 = (float)t2x;
+    if ((ld)t2 < t2x) t2 = std::nextafter(t2, INFINITY);
+    hp.T2 = t2;
+    return true;
+}
 }  // namespace
 
 // Paths other than MFMA8 under AUTO: FAST32, or DIRECT when no decision bound
@@ -1412,7 +1739,7 @@ inline bool auto_mfma8(int nc) { return nc <= 8 || nc == 15 || nc == 16 || nc >=
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.
 int classify_resolve_uncached(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
-                              Fast64Params &fp64, I8Params &ip8);
+                              Fast64Params &fp64, I8Params &ip8, HalfParams &hp);
 
 // Resolved parameters of recent (statistics, path) pairs: a classifier is
 // typically run many times with one set of class statistics (the benchmark
@@ -1426,10 +1753,11 @@ struct ResolvedEntry {
     FastParams fp;
     Fast64Params fp64;
     I8Params ip8;
+    HalfParams hp;
 };
 
 int classify_resolve(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
-                     Fast64Params &fp64, I8Params &ip8) {
+                     Fast64Params &fp64, I8Params &ip8, HalfParams &hp) {
     static std::mutex mtx;
     static std::vector<std::unique_ptr<ResolvedEntry>> cache;  // most recent first
     constexpr size_t kCap = 16;
@@ -1443,6 +1771,7 @@ int classify_resolve(int nc, const double *mu, const double *inv, int path, bool
                 fp = e.fp;
                 fp64 = e.fp64;
                 ip8 = e.ip8;
+                hp = e.hp;
                 const int chosen = e.chosen;
                 std::rotate(cache.begin(), cache.begin() + (std::ptrdiff_t)i, cache.begin() + (std::ptrdiff_t)i + 1);
                 return chosen;
@@ -1450,7 +1779,7 @@ int classify_resolve(int nc, const double *mu, const double *inv, int path, bool
         }
     }
     auto e = std::make_unique<ResolvedEntry>();
-    const int chosen = classify_resolve_uncached(nc, mu, inv, path, aligned, e->fp, e->fp64, e->ip8);
+    const int chosen = classify_resolve_uncached(nc, mu, inv, path, aligned, e->fp, e->fp64, e->ip8, e->hp);
     e->nc = nc;
     e->path = path;
     e->aligned = aligned;
@@ -1460,6 +1789,7 @@ int classify_resolve(int nc, const double *mu, const double *inv, int path, bool
     fp = e->fp;
     fp64 = e->fp64;
     ip8 = e->ip8;
+    hp = e->hp;
     std::lock_guard<std::mutex> lk(mtx);
     cache.insert(cache.begin(), std::move(e));
     if (cache.size() > kCap) cache.pop_back();
@@ -1467,7 +1797,7 @@ int classify_resolve(int nc, const double *mu, const double *inv, int path, bool
 }
 
 int classify_resolve_uncached(int nc, const double *mu, const double *inv, int path, bool aligned, FastParams &fp,
-                              Fast64Params &fp64, I8Params &ip8) {
+                              Fast64Params &fp64, I8Params &ip8, HalfParams &hp) {
     if (path == MPX_CLS_DIRECT || !aligned) return MPX_CLS_DIRECT;
     // mfma8 re-ranks its undecided pixels in fp32 first: its FastParams too
     // (T2 = +inf when the fp32 bound cannot be proven: the fp64 chain then
@@ -1484,10 +1814,11 @@ int classify_resolve_uncached(int nc, const double *mu, const double *inv, int p
         fp_for_i8();
         return MPX_CLS_MFMA8;
     }
-    const bool ok = path == MPX_CLS_MFMA64  ? build_fast64(nc, mu, inv, fp64)
-                    : path == MPX_CLS_MFMA8 ? build_i8(nc, mu, inv, ip8)
-                                            : build_fast(nc, mu, inv, fp);
-    if (path == MPX_CLS_MFMA8 && ok) fp_for_i8();
+    const bool ok = path == MPX_CLS_MFMA64   ? build_fast64(nc, mu, inv, fp64)
+                    : path == MPX_CLS_MFMA8  ? build_i8(nc, mu, inv, ip8)
+                    : path == MPX_CLS_MFMA16 ? build_half(nc, mu, inv, hp)
+                                             : build_fast(nc, mu, inv, fp);
+    if ((path == MPX_CLS_MFMA8 || path == MPX_CLS_MFMA16) && ok) fp_for_i8();
     return classify_choose(nc, path, ok);
 }
 
@@ -1497,7 +1828,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
     MPX_CHECK_ARG(grid >= 0 && block >= 0 && block <= 1024, "bad launch geometry");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA8, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA16, "bad path");
     if (npix == 0) return MPX_OK;
     MPX_CHECK_ARG(img, "null image");
     ClassParams cp{};
@@ -1507,7 +1838,8 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     FastParams fp;
     Fast64Params fp64;
     I8Params ip8;
-    const int chosen = classify_resolve(nc, mu, inv, path, aligned16(img), fp, fp64, ip8);
+    HalfParams hp;
+    const int chosen = classify_resolve(nc, mu, inv, path, aligned16(img), fp, fp64, ip8, hp);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
     // MFMA8 below 9 classes: the one-pixel-per-lane 4x4x4 form (MFMA8S);
     // MPX_CLS_MFMA8_SMALL=0 keeps the 32x32 form there (A/B)
@@ -1587,6 +1919,39 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
                 MPX_MFMA8S_L(8, 1, 0);
 #undef MPX_MFMA8S
 #undef MPX_MFMA8S_L
+            MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            done = nvec * 4;
+        }
+    } else if (chosen == MPX_CLS_MFMA16) {
+        const int64_t nvec = npix / 4;
+        if (nvec > 0) {
+            const int64_t blocks = (nvec + 255) / 256;
+            const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
+            // registers ranked in the last 16-class set: an even count (padded classes never win)
+            const int last = nc > 16 ? nc - 16 : nc;
+#define MPX_MFMA16(NSET, NR) \
+    hipLaunchKernelGGL((classify_mfma16_kernel<NSET, NR>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, hp, fp, amb)
+            if (nc <= 16) {
+                switch ((last + 1) / 2) {
+                    case 1: MPX_MFMA16(1, 2); break;
+                    case 2: MPX_MFMA16(1, 4); break;
+                    case 3: MPX_MFMA16(1, 6); break;
+                    case 4: MPX_MFMA16(1, 8); break;
+                    case 5: MPX_MFMA16(1, 10); break;
+                    case 6: MPX_MFMA16(1, 12); break;
+                    case 7: MPX_MFMA16(1, 14); break;
+                    default: MPX_MFMA16(1, 16); break;
+                }
+            } else if (last <= 4) {
+                MPX_MFMA16(2, 4);
+            } else if (last <= 8) {
+                MPX_MFMA16(2, 8);
+            } else if (last <= 12) {
+                MPX_MFMA16(2, 12);
+            } else {
+                MPX_MFMA16(2, 16);
+            }
+#undef MPX_MFMA16
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             done = nvec * 4;
         }
@@ -1729,13 +2094,15 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 int classify_plan_impl(int nc, const double *mu, const double *inv, int path, float *margin) {
     MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES, "need 1 <= nc <= 32");
     MPX_CHECK_ARG(mu && inv, "null class parameters");
-    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA8, "bad path");
+    MPX_CHECK_ARG(path >= MPX_CLS_DIRECT && path <= MPX_CLS_MFMA16, "bad path");
     FastParams fp;
     Fast64Params fp64;
     I8Params ip8;
-    const int chosen = classify_resolve(nc, mu, inv, path, true, fp, fp64, ip8);
+    HalfParams hp;
+    const int chosen = classify_resolve(nc, mu, inv, path, true, fp, fp64, ip8, hp);
     if (margin)
         *margin = chosen == MPX_CLS_MFMA8    ? (float)ip8.T2  // in key units
+                  : chosen == MPX_CLS_MFMA16 ? hp.T2
                   : chosen == MPX_CLS_MFMA64 ? (float)fp64.T2
                   : chosen == MPX_CLS_DIRECT ? 0.0f
                                              : fp.T2;
@@ -1777,4 +2144,21 @@ extern "C" int mpx_classify_i8_params(int nc, const double *mu, const double *in
 
 extern "C" int mpx_classify_plan(int nc, const double *mu, const double *inv, int path, float *margin) {
     return mpx::classify_plan_impl(nc, mu, inv, path, margin);
+}
+
+// Host-side export of the MFMA16 f16 weights (tests emulate the kernel on the
+// CPU): w = [32 classes][3 MFMAs][8 slots] f16 bit patterns, c = [32] fp32
+// accumulator inputs, *t2 = decision margin (the FAST32 test, scaled units).
+extern "C" int mpx_classify_f16_params(int nc, const double *mu, const double *inv, uint16_t *w, float *c,
+                                       float *t2) {
+    MPX_CHECK_ARG(nc >= 1 && nc <= MPX_MAX_CLASSES && mu && inv && w && c && t2, "bad arguments");
+    mpx::HalfParams hp;
+    if (!mpx::build_half(nc, mu, inv, hp)) return MPX_ERR_UNSUPPORTED;
+    for (int k = 0; k < MPX_MAX_CLASSES; ++k) {
+        for (int j = 0; j < mpx::kHalfMfmas; ++j)
+            for (int s = 0; s < 8; ++s) w[(k * mpx::kHalfMfmas + j) * 8 + s] = (uint16_t)(hp.w[k / 16][j][k % 16][s / 2] >> (16 * (s % 2)));
+        c[k] = hp.c[k];
+    }
+    *t2 = hp.T2;
+    return MPX_OK;
 }
