@@ -66,9 +66,10 @@ def select_device(local_rank: int, local_world: Optional[int], ndev: int, env=No
     * the launcher isolated devices per rank (a visibility variable set and
       fewer devices than node-local ranks, e.g. HIP_VISIBLE_DEVICES=<rank>):
       every rank sees its own GPU(s) from index 0 — device local_rank % ndev
-      (0 for one GPU per rank). Ranks that were all handed the SAME GPU are
-      still caught later: RCCL refuses duplicate devices and bench.py checks
-      distinct PCI ids;
+      (0 for one GPU per rank). Ranks that were all handed the SAME GPU (a
+      job-level restriction such as ROCR_VISIBLE_DEVICES=0,1,2,3 under 8
+      local ranks) are caught by :func:`init` itself, which gathers every
+      rank's (host, PCI id) and refuses duplicates (ADVICE r5);
     * otherwise (not isolated, more node-local ranks than devices): None.
     """
     env = os.environ if env is None else env
@@ -139,6 +140,8 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
         if use_cuda and backend == "nccl" and not contract:
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+    if world > 1 and use_cuda and not rehearsal:
+        check_distinct_devices(ctx)
     if world > 1 and contract:
         _contract.install(dev)
         ctx.native = _contract.ContractNativeComm.create(ctx) if use_cuda else None
@@ -148,6 +151,42 @@ def init(device: str = "auto", backend: Optional[str] = None, timeout_s: float =
         ctx.native = NativeComm.create(ctx)
     _CTX = ctx
     return ctx
+
+
+def device_pci(dev: torch.device) -> str:
+    """PCI location of a GPU ("dddd:bb:dd"), or "cpu"."""
+    if dev.type != "cuda":
+        return "cpu"
+    p = torch.cuda.get_device_properties(dev)
+    bus = getattr(p, "pci_bus_id", None)
+    if bus is None:
+        return f"cuda:{dev.index}"
+    return f"{getattr(p, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(p, 'pci_device_id', 0):02x}"
+
+
+def check_distinct_devices(ctx: DistContext) -> None:
+    """Collective: every rank's (host, GPU PCI id); SystemExit(2) on every
+    rank when two ranks of one host drive the same GPU — whatever the backend
+    or caller (RCCL would refuse later, gloo never)."""
+    import socket
+    import sys
+
+    mine = (socket.gethostname(), device_pci(ctx.device))
+    every = [None] * ctx.world
+    dist.all_gather_object(every, mine)
+    seen: dict = {}
+    dups = []
+    for r, key in enumerate(every):
+        if key in seen:
+            dups.append((seen[key], r, key))
+        seen.setdefault(key, r)
+    if dups:
+        if ctx.rank == 0:
+            print(f"[dist] ranks share a GPU: {', '.join(f'{a} and {b} on {k[0]} {k[1]}' for a, b, k in dups)}; "
+                  f"refusing (MPX_DIST_BACKEND=gloo or MPX_DIST_CONTRACT=nccl rehearse several ranks per GPU)",
+                  file=sys.stderr)
+        dist.destroy_process_group()
+        raise SystemExit(2)
 
 
 def shutdown() -> None:

@@ -39,7 +39,8 @@ Set-up is collective and TIME-BOUNDED everywhere:
 
 Fault injection (tests): ``MPX_PEER_INJECT=open_stall@R`` (rank R's IPC open
 never returns), ``verify_corrupt@R`` (R reports a wrong checksum),
-``probe_corrupt@R`` (R writes a wrong probe pattern).
+``probe_corrupt@R`` (R writes a wrong probe pattern), ``map_fail@R`` (R's
+mapping of its neighbours' mailboxes fails: every rank must agree on RCCL).
 
 Limitation of the open deadline: ``open_stall`` sleeps on the
 helper thread BEFORE it calls into HIP, so the tests show the vote and the
@@ -523,6 +524,8 @@ def try_peer_halo(ctx: DistContext, slab: Slab, own: torch.Tensor) -> Optional[P
     ph = None
     if mine is not None:
         try:
+            if _injected("map_fail", ctx.rank):  # fault hook: this rank cannot map its neighbours
+                raise RuntimeError("injected mapping failure (MPX_PEER_INJECT map_fail)")
             ph = PeerHalo(ctx, slab, own, mb, every)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"

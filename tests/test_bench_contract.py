@@ -195,3 +195,29 @@ def test_scale_driver_job_is_the_driver_command():
         job = [j for j in scale.plan(n, a, 8) if j["name"] == "conv/driver"][0]
         assert job["cmd"][1:] == ["bench.py", "--gpus", str(n), "--steps", "20", "--warmup", "5"]
         assert job["skip"] is None
+
+
+def test_bench_streaming_timeout_on_one_rank_cpu():
+    """VERDICT r5 Next #7 / ADVICE r5: a device-side halo wait that gives up on
+    ONE rank during the timed streaming steps (MPX_BENCH_INJECT_STREAM_TIMEOUT)
+    makes every rank leave the streaming phase together (no hang): the static
+    headline stays measured and verified, value_streaming is null, and the
+    record's status says streaming_failed; --strict-streaming turns it into a
+    non-zero exit."""
+    args = ["--gpus", "2", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2",
+            "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"]
+    rec = _run(args, nproc=2, env={"MPX_BENCH_INJECT_STREAM_TIMEOUT": "1"})
+    assert rec["value"] > 0 and rec["verified_bit_exact"] is True and rec["verified_pixels"] == 2 * 2 * 64 * 64
+    assert rec["value_streaming"] is None and "timed out" in rec["streaming_error"]
+    assert rec["verified_bit_exact_streaming"] is None and rec["status"] == "streaming_failed"
+    ok = _run(args, nproc=2)
+    assert ok["status"] == "ok" and ok["value_streaming"] > 0
+    _run(args + ["--strict-streaming"], nproc=2, env={"MPX_BENCH_INJECT_STREAM_TIMEOUT": "0"}, rc=3)
+
+
+def test_bench_records_multi_node_clock_policy():
+    """the job span uses one shared clock only on one node; the
+    record says which clock it used (here: one host, shared)."""
+    rec = _run(["--gpus", "2", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2",
+                "--no-stream", "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"], nproc=2)
+    assert rec["clock"] == "shared-monotonic" and rec["start_skew_ms"] is not None

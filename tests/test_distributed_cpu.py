@@ -290,3 +290,15 @@ def test_select_device_uses_node_local_values():
     assert select_device(3, None, 2, env={}) is None
     assert select_device(0, None, 1, env={}) == 0
     assert select_device(0, 1, 0, env={}) is None
+
+
+def test_span_per_rank_clock_when_multi_node():
+    """ranks on different hosts read unrelated monotonic clocks —
+    the job time is then the slowest rank's own span, never max(t1) - min(t0)
+    across clocks, and the skews are not reported."""
+    from cuda_mpi_openmp_amd.parallel.timing import Span
+
+    s = Span([0.0, 5e17], [2e6, 5e17 + 3e6], shared=False)
+    assert s.job_s == 3e-3 and s.fields(1)["clock"] == "per-rank" and s.fields(1)["start_skew_ms"] is None
+    one = Span([0.0, 1e6], [2e6, 3e6])
+    assert one.job_s == 3e-3 and one.fields(1)["clock"] == "shared-monotonic"
