@@ -7,8 +7,13 @@ fp32 luminance) on the hand-written gfx950 wave-streaming kernel (register
 windows shifted across lanes with DPP, no LDS, no barriers), synthetic random
 RGBA8 data.
 
-Scaling is WEAK: every rank owns one 4096x4096 row slab of a global
-(4096*N) x 4096 image. One step = read the slab's 2+2 halo rows from the
+Scaling is WEAK by default: every rank owns one 4096x4096 row slab of a global
+(4096*N) x 4096 image. ``--layout strong`` keeps ONE global 4096x4096 image
+and splits it into N row slabs (4096/N rows per rank: 512 at N = 8), same
+rotation, verification and job-span timing, recorded as ``scaling: "strong"``;
+at N = 1 both layouts are the same run. The strong layout also gathers every
+rotated slab's N-rank output and compares it with a one-device convolution of
+the whole frame (``verified_one_device``). One step = read the slab's 2+2 halo rows from the
 neighbouring ranks over xGMI + convolve every owned row. Halo transport
 (``--halo``): ``peer`` maps the neighbours' slabs once (IPC) and the conv
 kernel loads their boundary rows over xGMI on every step — one launch per
@@ -90,7 +95,10 @@ def parse_args(argv=None):
     p.add_argument("--sustain-ms", type=float, default=50.0,
                    help="value_sustained: the same K rotated steps timed again after this much continuous load "
                         "(0 = skip)")
-    p.add_argument("--size", type=int, default=4096, help="image side per GPU slab")
+    p.add_argument("--size", type=int, default=4096,
+                   help="image side: per GPU slab (weak layout) or of the one global image (strong layout)")
+    p.add_argument("--layout", choices=["weak", "strong"], default="weak",
+                   help="weak: a size x size slab per rank; strong: one size x size image split over the ranks")
     p.add_argument("--filter", default="sobel5")
     p.add_argument("--rotate", type=int, default=6,
                    help="independent image/output slab pairs cycled by the timed steps (working set > MALL)")
@@ -165,9 +173,12 @@ def run(args) -> int:
             torch.cuda.synchronize(ctx.device)
 
     overlap = {"auto": "auto", "on": True, "off": False, "pipeline": "pipeline"}[args.overlap]
+    strong = args.layout == "strong"
+    global_rows = args.size if strong else args.size * n
+    args.global_rows = global_rows
     dets = []
     for r in range(max(1, args.rotate)):
-        d = SlabEdgeDetector(ctx, args.size * n, args.size, args.filter, overlap=overlap, halo=args.halo)
+        d = SlabEdgeDetector(ctx, global_rows, args.size, args.filter, overlap=overlap, halo=args.halo)
         d.fill_random(seed=1234 + 7919 * r + ctx.rank)
         dets.append(d)
     sync()
@@ -301,10 +312,10 @@ def run(args) -> int:
             warm, warm1 = warm1, None
 
     ms_per_step = elapsed * 1e3 / max(1, args.steps)
-    pixels = n * args.size * args.size * args.steps
+    pixels = global_rows * args.size * args.steps
     value = pixels / elapsed / 1e9
 
-    ok, checked = True, 0
+    ok, checked, one_device = True, 0, None
     if not args.no_verify:
         for d in dets:
             good, cnt = verify_full(d, ops)
@@ -312,6 +323,9 @@ def run(args) -> int:
             checked += cnt
         ok = parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
         checked = int(parallel.all_reduce_sum_host(float(checked), ctx))
+        if strong:
+            one_device = verify_one_device(dets, args, ctx, ops, parallel)
+            ok &= one_device
 
     # ---- streaming: the same K steps with a real inter-rank dependency ----
     stream_rec = None
@@ -378,38 +392,43 @@ def run(args) -> int:
             "warmup_steps_run": warm_info["steps"],
             "warmup_ms": warm_info["ms"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": round(value / BASELINE_GPIXEL_PER_S, 2),
             "vs_baseline_note": BASELINE_NOTE,
             "dtype": "fp32",
-            "data": f"synthetic (uniform random RGBA8, {len(dets)} independent {args.size}x{args.size} slabs per GPU "
-                    f"cycled by the timed steps)",
+            "data": (f"synthetic (uniform random RGBA8, {len(dets)} independent {args.size}x{args.size} images "
+                     f"cycled by the timed steps, each split into {n} row slab(s))" if strong else
+                     f"synthetic (uniform random RGBA8, {len(dets)} independent {args.size}x{args.size} slabs per GPU "
+                     f"cycled by the timed steps)"),
             "config": {
                 "model": f"lab2 2D convolution {args.size}x{args.size} image, "
                          f"{d0.filter.k}x{d0.filter.k} filter ({d0.filter.name}"
                          f"{', separable 1x5+5x1 passes' if d0.filter.separable else ''}, band-streaming HIP kernel)",
-                "global_batch": n,
+                "global_batch": 1 if strong else n,
+                "layout": args.layout,
+                "rows_per_rank": [d0.slab.rows_of(r) for r in range(n)],
                 "seq_len": args.size,
                 "parallelism": f"slab{n}" + (("+halo-peer-fused" if d0.peer is not None else "+halo-pipelined"
                                               if d0.pipeline else "+halo-overlap" if d0.overlap else "+halo-inorder")
                                              if n > 1 else ""),
                 "transport": d0.transport if n > 1 else None,
                 "peer_probe": (None if n == 1 or args.halo == "rccl" or ctx.device.type != "cuda" else "ok" if d0.peer is not None else "fallback"),
-                "image_hw": [args.size * n, args.size],
+                "image_hw": [global_rows, args.size],
                 "halo_rows": [d0.filter.halo_up, d0.filter.halo_down],
                 "graph_steps": args.graph if graph is not None else 0,
                 "streams": nstreams,
                 "host_wait": wait_policy_in_force(ctx.device) if ctx.device.type == "cuda" else None,
                 "rotate": len(dets),
-                "working_set_MiB_per_gpu": round(len(dets) * 2 * args.size * args.size * 4 / 2**20, 1),
+                "working_set_MiB_per_gpu": round(len(dets) * 2 * d0.slab.rows * args.size * 4 / 2**20, 1),
             },
             "world_size_seen": seen,
             "rank_devices": rank_devices,
             "distinct_devices": len(set(rank_devices)),
             "rehearsal": rehearsal,
             **span.fields(args.steps),
-            "verified_bit_exact": ok and (args.no_verify or checked == n * len(dets) * args.size * args.size),
+            "verified_bit_exact": ok and (args.no_verify or checked == len(dets) * global_rows * args.size),
             "verified_pixels": checked,
+            "verified_one_device": one_device,
             "device": str(torch.cuda.get_device_name(ctx.device)) if ctx.device.type == "cuda" else "cpu",
         }
         if clocks is not None:
@@ -482,7 +501,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
     seeds = [1234 + 7919 * r for r in range(max(1, args.rotate))]
     sdets = []
     for sd in seeds:
-        d = SlabEdgeDetector(ctx, args.size * n, args.size, args.filter, halo=args.halo, stream=True)
+        d = SlabEdgeDetector(ctx, args.global_rows, args.size, args.filter, halo=args.halo, stream=True)
         d.fill_random(seed=sd + ctx.rank)
         sdets.append(d)
     cyc = [0]
@@ -528,7 +547,7 @@ def run_streaming(args, ctx, n, timed, watchdog, sync, ops, parallel) -> dict:
             d.close()
         raise StreamingTimeout(f"rank {ctx.rank}: streaming halo wait timed out during the timed steps "
                            f"({'this rank' if any(bad) else 'on another rank'}; slabs {[i for i, b in enumerate(bad) if b]})")
-    rec = {"value_streaming": _sig(n * args.size * args.size * args.steps / elapsed / 1e9),
+    rec = {"value_streaming": _sig(args.global_rows * args.size * args.steps / elapsed / 1e9),
            "streams_streaming": ns,
            "ms_per_step_streaming": round(elapsed * 1e3 / max(1, args.steps), 5),
            "host_enqueue_ms_per_step_streaming": round(enqueue_ms, 5),
@@ -616,6 +635,9 @@ def cpu_baseline_ms(det, size: int, ops, runs: int = 5) -> dict:
     import torch
 
     img = det.own[:size].to("cpu").contiguous()
+    if img.shape[0] < size:  # strong layout: this rank owns a fraction of the image; time a whole frame
+        g = torch.Generator().manual_seed(99)
+        img = torch.randint(0, 256, (size, size, 4), dtype=torch.uint8, generator=g)
     out = torch.empty_like(img)
     ops.conv(img, det.filter, out)  # first touch of the output pages outside the timing
     ts = []
@@ -638,6 +660,23 @@ def cpu_baseline_ms(det, size: int, ops, runs: int = 5) -> dict:
             if r.returncode == 0:
                 res["serial_o0_ms"] = parse_timing(r.stdout.splitlines()[0] if r.stdout else "")
     return res
+
+
+def verify_one_device(dets, args, ctx, ops, parallel) -> bool:
+    """Strong layout: every rotated image's gathered N-rank output equals one
+    device convolving the whole frame (regenerated from the ranks' seeds)."""
+    import torch
+
+    ok = True
+    n = ctx.world
+    for r_i, d in enumerate(dets):
+        got = parallel.gather_slabs(d.out.contiguous(), d.slab, ctx)
+        if ctx.rank == 0:
+            seed = 1234 + 7919 * r_i
+            full = torch.cat([regen_slab(seed + r, d.slab.rows_of(r), args.size, ctx.device) for r in range(n)])
+            ref = ops.conv(full, d.filter)
+            ok &= bool(torch.equal(got.to(ref.device), ref))
+    return parallel.max_over_ranks(0.0 if ok else 1.0, ctx) == 0.0
 
 
 def verify_full(det, ops):

@@ -221,3 +221,40 @@ def test_bench_records_multi_node_clock_policy():
     rec = _run(["--gpus", "2", "--device", "cpu", "--size", "64", "--steps", "2", "--warmup", "1", "--rotate", "2",
                 "--no-stream", "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"], nproc=2)
     assert rec["clock"] == "shared-monotonic" and rec["start_skew_ms"] is not None
+
+
+def test_bench_strong_layout_equals_one_device_cpu():
+    """VERDICT r5 Next #2: --layout strong splits ONE global image over the
+    ranks (rows_per_rank = size / N, uneven at N = 3); the gathered N-rank
+    output of every rotated frame equals a one-device run on every pixel, and
+    the record says strong."""
+    for n in (2, 3):
+        rec = _run(["--gpus", str(n), "--device", "cpu", "--layout", "strong", "--size", "97", "--steps", "2",
+                    "--warmup", "1", "--rotate", "2", "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"], nproc=n)
+        assert rec["scaling"] == "strong" and rec["config"]["layout"] == "strong"
+        assert rec["config"]["image_hw"] == [97, 97] and sum(rec["config"]["rows_per_rank"]) == 97
+        assert rec["verified_one_device"] is True and rec["verified_bit_exact"] is True
+        assert rec["verified_pixels"] == 2 * 97 * 97 and rec["verified_bit_exact_streaming"] is True
+        # value: the ONE image's pixels per step over the job span
+        assert abs(rec["value"] - 97 * 97 / (rec["ms_per_step"] * 1e-3) / 1e9) < 1e-3 * max(1e-3, rec["value"])
+    one = _run(["--device", "cpu", "--layout", "strong", "--size", "64", "--steps", "2", "--warmup", "1",
+                "--rotate", "2", "--no-stream", "--no-warm", "--sustain-ms", "0", "--no-cpu-baseline"])
+    assert one["n_gpus"] == 1 and one["config"]["image_hw"] == [64, 64] and one["verified_one_device"] is True
+
+
+def test_scale_plans_strong_conv_job():
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("scale", os.path.join(ROOT, "tools", "scale.py"))
+    scale = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(scale)
+    a = argparse.Namespace(device="auto", rehearse=False, contract=False, quick=False, driver_steps=20,
+                           driver_warmup=5)
+    job = [j for j in scale.plan(8, a, 8) if j["name"] == "conv/strong"][0]
+    assert job["kind"] == "strong" and "--layout" in job["cmd"] and job["cmd"][job["cmd"].index("--layout") + 1] \
+        == "strong"
+    rows = [{"name": "conv/strong", "kind": "strong", "n": 1, "status": "ok", "ms": 0.024},
+            {"name": "conv/strong", "kind": "strong", "n": 8, "status": "ok", "ms": 0.004}]
+    scale.efficiencies(rows)
+    assert rows[1]["efficiency"] == round(0.024 / (8 * 0.004), 4) and rows[1]["speedup"] == 6.0

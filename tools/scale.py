@@ -8,6 +8,8 @@ same commands a user would type):
 
   * conv (weak scaling, the flagship): ``bench.py --gpus N`` with one-sided
     peer halos and with RCCL halos — every rank owns a 4096^2 slab;
+  * conv/strong: ``bench.py --gpus N --layout strong`` — one 4096^2 frame
+    split into N row slabs (strong scaling, t_1 / (N t_N));
   * Jacobi 16384^2 fp64 (strong scaling): ``tools/bench_jacobi.py --gpus N``
     with device-signalled peer halos and with RCCL halos;
   * the native one-process runtime: ``bin/mpx_mgpu conv|jacobi --gpus N``;
@@ -101,6 +103,13 @@ def plan(n: int, a, ndev: int) -> List[dict]:
         assert drv[1:] == driver_command(n, a.driver_steps, a.driver_warmup), drv
     jobs.append({"name": "conv/driver", "kind": "weak", "skip": lacks,
                  "cmd": drv + (dev + ["--size", "128", "--rotate", "2"] if cpu else [])})
+    # strong scaling of the flagship (VERDICT r5 Next #2): ONE 4096^2 frame split
+    # into N row slabs (512 rows per rank at N = 8), the driver's K / W, halos
+    # by the default transport; efficiency t_1 / (N t_N)
+    jobs.append({"name": "conv/strong", "kind": "strong", "skip": lacks,
+                 "cmd": [py, "bench.py", "--gpus", str(n), "--layout", "strong", "--steps", str(a.driver_steps),
+                         "--warmup", str(a.driver_warmup), "--no-cpu-baseline"]
+                 + (dev + ["--size", "128", "--rotate", "2"] if cpu else [])})
     for halo in ("peer", "rccl"):
         skip = lacks
         if n > 1 and halo == "rccl" and a.rehearse and not cpu and not a.contract:
@@ -264,7 +273,7 @@ def main(argv=None) -> int:
                 # output: halos with a real inter-rank dependency) as its own curve
                 rec = res["record"] if not job["skip"] and res["status"] == "ok" else {}
                 if job["name"].startswith("conv/") and (job["skip"] or rec.get("value_streaming") is not None):
-                    srow = {"name": job["name"].replace("conv/", "conv-stream/"), "kind": "weak", "n": n,
+                    srow = {"name": job["name"].replace("conv/", "conv-stream/"), "kind": job["kind"], "n": n,
                             "cmd": row["cmd"], "status": row["status"]}
                     if job["skip"]:
                         srow["reason"] = job["skip"]
