@@ -214,3 +214,30 @@ def test_roberts_rgb_pins_reference_sample():
 def test_roberts_rgb_cpu_matches_torch(hw):
     img = rand_img(*hw, seed=hw[0] * 100 + hw[1])
     assert torch.equal(ops.roberts_rgb(img), ref.roberts_rgb(img))
+
+
+@pytest.mark.parametrize("bucket", ["medium", "large"])
+def test_metric_calc_gt_matches_independent_torch_oracle(bucket):
+    """the medium/large metric_calc GT (written by
+    tools/make_metric_gt.py from this repository's own serial CPU program) is
+    pinned independently: plain-torch Roberts (ops/reference.py, no native
+    code) on every bucket image equals its *_out_gt PNG on every byte. The
+    harness loads PNG inputs with alpha forced to 255 (reference
+    utils/converter.py:111), as here."""
+    import glob
+
+    from PIL import Image
+
+    from cuda_mpi_openmp_amd.ops import reference as torch_ref
+
+    from .helpers import ROOT
+
+    root = os.path.join(ROOT, "labs", "lab2", "metric_calc")
+    files = sorted(glob.glob(os.path.join(root, bucket, "*.png")))
+    assert len(files) == 3
+    for f in files:
+        src = np.array(Image.open(f).convert("RGBA"))
+        src[..., 3] = 255
+        gt = np.array(Image.open(os.path.join(root, f"{bucket}_out_gt", os.path.basename(f))).convert("RGBA"))
+        got = torch_ref.roberts(torch.from_numpy(src)).numpy()
+        assert got.shape == gt.shape and np.array_equal(got, gt), (f, int((got != gt).sum()))
