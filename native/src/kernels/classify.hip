@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <memory>
 #include <mutex>
+#include <tuple>
 #include <utility>
 #include <vector>
 #include <cstdlib>
@@ -66,7 +67,7 @@ __device__ __forceinline__ uint32_t classify_direct(uint32_t p, int nc, const Cl
     const double pr = (double)mpx_px_r(p), pg = (double)mpx_px_g(p), pb = (double)mpx_px_b(p);
     double best = 1.7976931348623157e308;  // DBL_MAX
     int cls = -1;
-    for (int c = 0; c < nc; ++c) {
+    auto one = [&](int c) {
         const double d0 = pr - cp.mu[3 * c + 0];
         const double d1 = pg - cp.mu[3 * c + 1];
         const double d2 = pb - cp.mu[3 * c + 2];
@@ -85,7 +86,18 @@ __device__ __forceinline__ uint32_t classify_direct(uint32_t p, int nc, const Cl
             best = dist;
             cls = c;
         }
+    };
+    // four classes per trip: their parameters arrive in one batch of scalar
+    // loads (one s_load wait per class made the deferred stages
+    // latency-bound, round 6); the classes stay in order (strict '<')
+    int c = 0;
+    for (; c + 4 <= nc; c += 4) {
+        one(c);
+        one(c + 1);
+        one(c + 2);
+        one(c + 3);
     }
+    for (; c < nc; ++c) one(c);
     return (p & 0x00ffffffu) | ((uint32_t)(uint8_t)cls << 24);
 }
 
@@ -173,13 +185,21 @@ __device__ __forceinline__ bool classify_fp32_one(uint32_t p, int nc, const Fast
                 b = (float)((p >> 16) & 0xffu) - 128.0f;
     const float f[9] = {r * r, g * g, b * b, r * g, r * b, g * b, r, g, b};
     uint32_t B = kKeyInit, S = kKeyInit;
-    for (int c = 0; c < nc; ++c) {
+    auto one = [&](int c) {
         const float *w = fp.w[c];
         float d = w[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) d = fmaf(w[k], f[k], d);
         rank_key(make_key(d, (uint32_t)c), B, S);
+    };
+    int c = 0;
+    for (; c + 4 <= nc; c += 4) {  // one batch of scalar loads per four classes
+        one(c);
+        one(c + 1);
+        one(c + 2);
+        one(c + 3);
     }
+    for (; c < nc; ++c) one(c);
     out = (p & 0x00ffffffu) | ((B & 31u) << 24);
     return decided(B, S, fp.T2);
 }
@@ -1271,12 +1291,85 @@ __device__ __forceinline__ uint32_t mfma16_pixel(uint32_t p, const Mfma16Lane<NS
     return __builtin_amdgcn_perm(B & 31u, p, 0x04020100u);
 }
 
+// Undecided pixels of a whole launch: each wave appends its LDS list of
+// (vector << 4 | pixel mask) entries to one device list (one atomic per wave)
+// and classify_fixup_kernel re-ranks them all afterwards, every lane busy. At
+// 0.05-0.1 % undecided a wave holds ~1-4 entries, and re-ranking them inside
+// the wave ran the fp32 stage (~15 VALU x nc per pixel slot) once per wave for
+// a handful of lanes: ~25 % of the kernel's VALU at 32 classes (round-6
+// counters, profiles/lab3_classify.md).
+// The list is split into kDeferSubs sub-lists (sub-list = workgroup id mod
+// kDeferSubs, each with its own counter): one counter for the whole launch
+// serialised ~16K same-address atomics in the L2 (+30-50 µs at 4-16
+// classes, round 6). Fix-up block b owns sub-list b: it reads its count,
+// re-ranks the entries and zeroes the count for the next launch.
+constexpr uint32_t kDeferSubs = 256;
+constexpr uint32_t kFixupParts = 4;  // fix-up blocks per sub-list (4 waves per SIMD: the stages' dependent chains overlap)
+struct DeferList {
+    uint64_t *ent;  // kDeferSubs x cap entries; nullptr: re-rank inside each wave (no device list)
+    uint32_t *ctr;  // 2 x kDeferSubs counters, used by calls of alternating parity
+    uint32_t cap;   // entries per sub-list
+    uint32_t par;   // this call's parity: the fix-up zeroes the other parity's counters for the next call
+};
+
+// re-rank the undecided pixels of one entry: fp32 proven margin, else fp64
+__device__ __forceinline__ uint32_t fix_entry(uint32_t *img, uint64_t e, int nc, const ClassParams &cp,
+                                              const FastParams &fp) {
+    const int64_t vi = (int64_t)(e >> 4);
+    const uint32_t mask = (uint32_t)e & 15u;
+    const uint4 q = reinterpret_cast<const uint4 *>(img)[vi];
+    const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+    for (int m = 0; m < 4; ++m) {
+        if (!((mask >> m) & 1u)) continue;
+        uint32_t o;
+        if (!classify_fp32_one(px[m], nc, fp, o)) o = classify_direct(px[m], nc, cp);
+        img[vi * 4 + m] = o;
+    }
+    return (uint32_t)__popc(mask);
+}
+
+// grid = kDeferSubs x kFixupParts blocks; block b takes part b / kDeferSubs of
+// sub-list b % kDeferSubs, one (entry, pixel slot) pair per thread — a thread
+// re-ranks at most one pixel per pass, so a wave's dependent fp32 / fp64
+// chains are short and four waves per SIMD overlap them (one thread per
+// entry, one wave per SIMD, ran 25-47 µs on ~50K entries). It also zeroes the
+// counters of the other parity, which the next call appends to.
+__global__ __launch_bounds__(256) void classify_fixup_kernel(uint32_t *__restrict__ img, DeferList dl, int nc,
+                                                             ClassParams cp, FastParams fp, uint32_t *amb) {
+    const uint32_t sub = blockIdx.x % kDeferSubs, part = blockIdx.x / kDeferSubs;
+    const uint32_t n = min(dl.ctr[dl.par * kDeferSubs + sub], dl.cap);
+    const uint64_t *ent = dl.ent + (size_t)sub * dl.cap;
+    uint32_t px = 0;
+    for (uint32_t j = part * 256 + threadIdx.x; j < 4 * n; j += 256 * kFixupParts) {
+        const uint64_t e = ent[j >> 2];
+        const uint32_t m = j & 3;
+        if (!((e >> m) & 1u)) continue;
+        const int64_t vi = (int64_t)(e >> 4);
+        const uint32_t p = img[vi * 4 + m];  // RGB untouched by the provisional result
+        uint32_t o;
+        if (!classify_fp32_one(p, nc, fp, o)) o = classify_direct(p, nc, cp);
+        img[vi * 4 + m] = o;
+        ++px;
+    }
+    __shared__ uint32_t s_px;
+    if (threadIdx.x == 0) s_px = 0;
+    __syncthreads();
+    if (px) atomicAdd(&s_px, px);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (amb && s_px) atomicAdd(amb, s_px);
+        if (part == 0) dl.ctr[(dl.par ^ 1u) * kDeferSubs + sub] = 0;
+    }
+}
+
 // The MFMA8S loop skeleton (one pixel per lane, four per 16-B vector, one
-// trip of loads ahead, per-wave deferral lists without block barriers).
-template <int NSET, int NR>
-__global__ __launch_bounds__(256) void classify_mfma16_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
+// trip of loads ahead, per-wave deferral lists without block barriers): the
+// remainder of an image past classify_mfma16t_kernel's whole blocks, and the
+// whole image when no device deferral list could be allocated.
+template <int NSET, int NR, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void classify_mfma16_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, HalfParams hp, FastParams fp,
-                                                              uint32_t *amb) {
+                                                              DeferList dl, uint32_t *amb) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const Mfma16Lane<NSET> L = mfma16_lane<NSET>(hp, lane);
     const float T2 = hp.T2;
@@ -1312,10 +1405,28 @@ __global__ __launch_bounds__(256) void classify_mfma16_kernel(uint32_t *__restri
         }
         v[i] = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    // this wave's deferred pixels: the fp32 proven-margin ranking first, the
-    // exact fp64 chain for what it leaves (every lane of the wave busy in each)
     __builtin_amdgcn_wave_barrier();
     const uint32_t nd = min(s_namb[w], (uint32_t)kAmb8sCapW);
+    if (dl.ent != nullptr) {  // to the launch's device list (classify_fixup_kernel)
+        if (nd == 0) return;
+        const uint32_t sub = blockIdx.x % kDeferSubs;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&dl.ctr[dl.par * kDeferSubs + sub], nd);
+        base = __shfl(base, 0);
+        uint64_t *ent = dl.ent + (size_t)sub * dl.cap;
+        uint32_t over = 0;
+        for (uint32_t j = lane; j < nd; j += 64) {
+            const uint64_t e = (uint64_t)s_amb[w][j];
+            if (base + j < dl.cap)
+                ent[base + j] = e;
+            else
+                over += fix_entry(img, e, nc, cp, fp);  // list full: this lane re-ranks it (never at benchmark rates)
+        }
+        if (amb && over) atomicAdd(amb, over);
+        return;
+    }
+    // this wave's deferred pixels: the fp32 proven-margin ranking first, the
+    // exact fp64 chain for what it leaves (every lane of the wave busy in each)
     for (uint32_t j = lane; j < nd; j += 64) {
         const int64_t e = s_amb[w][j];
         const int64_t vi = e >> 4;
@@ -1343,6 +1454,67 @@ __global__ __launch_bounds__(256) void classify_mfma16_kernel(uint32_t *__restri
     if (amb && lane == 0 && s_npx[w]) atomicAdd(amb, s_npx[w]);
     const uint32_t nd2 = min(s_namb2[w], (uint32_t)kAmb8sCap2W);
     for (uint32_t j = lane; j < nd2; j += 64) img[s_amb2[w][j]] = classify_direct(s_ambpx2[w][j], nc, cp);
+}
+
+// The production form: every thread takes exactly T 16-B vectors (T x 256
+// per block, no loop, no bounds checks: the launch covers whole blocks and
+// the host sends the remainder to the looped kernel above), all T loads
+// issued before the first pixel is ranked. Straight-line code is the one
+// shape for which the compiler's s_waitcnt placement is exact: in a loop it
+// waited vmcnt(0) at the loop head (the previous trip's store) and before
+// every store (its own prefetch), whatever the buffering (round 6 probes).
+// A wave's undecided pixels (<= 64 T entries: its LDS list never fills) go
+// to the launch's device list and classify_fixup_kernel.
+constexpr int kM16Trips = 4;
+
+template <int NSET, int NR, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void classify_mfma16t_kernel(
+    uint32_t *__restrict__ img, int nc, ClassParams cp, HalfParams hp, FastParams fp, DeferList dl, uint32_t *amb) {
+    constexpr int T = kM16Trips;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ int64_t s_amb[4][64 * T];  // vector index << 4 | undecided-pixel mask
+    __shared__ uint32_t s_namb[4];
+    if (lane == 0) s_namb[w] = 0;
+    const Mfma16Lane<NSET> L = mfma16_lane<NSET>(hp, lane);  // its loads first: trip 0 waits for them alone
+    const float T2 = hp.T2;
+    uint4 *v = reinterpret_cast<uint4 *>(img);
+    const int64_t base = (int64_t)blockIdx.x * (256 * T) + threadIdx.x;
+    uint4 q[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) q[t] = v[base + 256 * t];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int64_t vi = base + 256 * t;
+        const uint32_t px[4] = {q[t].x, q[t].y, q[t].z, q[t].w};
+        uint32_t o[4];
+        bool u[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) o[m] = mfma16_pixel<NSET, NR>(px[m], L, T2, u[m]);
+        if (__builtin_expect(u[0] | u[1] | u[2] | u[3], 0)) {
+            const uint32_t mask = (uint32_t)u[0] | ((uint32_t)u[1] << 1) | ((uint32_t)u[2] << 2) | ((uint32_t)u[3] << 3);
+            s_amb[w][atomicAdd(&s_namb[w], 1u)] = (vi << 4) | mask;  // at most one entry per lane and trip
+        }
+        v[vi] = make_uint4(o[0], o[1], o[2], o[3]);
+        __builtin_amdgcn_sched_barrier(0);  // one trip's registers at a time
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nd = s_namb[w];
+    if (nd == 0) return;
+    const uint32_t sub = blockIdx.x % kDeferSubs;
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(&dl.ctr[dl.par * kDeferSubs + sub], nd);
+    b0 = __shfl(b0, 0);
+    uint64_t *ent = dl.ent + (size_t)sub * dl.cap;
+    uint32_t over = 0;
+    for (uint32_t j = lane; j < nd; j += 64) {
+        const uint64_t e = (uint64_t)s_amb[w][j];
+        if (b0 + j < dl.cap)
+            ent[b0 + j] = e;
+        else
+            over += fix_entry(img, e, nc, cp, fp);  // list full: this lane re-ranks it (never at benchmark rates)
+    }
+    if (amb && over) atomicAdd(amb, over);
 }
 
 // ---------------------------------------------------------------------------
@@ -1822,6 +1994,51 @@ int classify_resolve_uncached(int nc, const double *mu, const double *inv, int p
     return classify_choose(nc, path, ok);
 }
 
+// One device deferral list per (device, stream), allocated on first use and
+// reset by the fix-up kernel itself (no memset launch per call). nullptr
+// lists (allocation failed) fall back to the in-wave re-ranking.
+DeferList defer_list(hipStream_t s, bool take) {
+    static std::mutex mtx;
+    static std::vector<std::tuple<int, hipStream_t, DeferList>> lists;
+    constexpr uint32_t kCap = 4096;  // entries per sub-list (8 MiB in all); 4 pixels each
+    int dev = 0;  // the stream's device (the image's), not necessarily the current one
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return DeferList{nullptr, nullptr, 0, 0};
+    }
+    std::lock_guard<std::mutex> lk(mtx);
+    for (auto &t : lists)
+        if (std::get<0>(t) == dev && std::get<1>(t) == s) {
+            DeferList &d = std::get<2>(t);
+            // launches that use the list alternate counter sets: the fix-up of
+            // one zeroes the set of the next (launches of one stream run in order)
+            if (take) d.par ^= 1u;
+            return d;
+        }
+    DeferList d{nullptr, nullptr, kCap, 0};
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    struct Restore {
+        int cur, dev;
+        ~Restore() {
+            if (cur != dev) (void)hipSetDevice(cur);
+        }
+    } restore{cur, dev};
+    if (hipMalloc(&d.ent, sizeof(uint64_t) * kCap * kDeferSubs) != hipSuccess) {
+        (void)hipGetLastError();
+        return DeferList{nullptr, nullptr, 0, 0};
+    }
+    if (hipMalloc(&d.ctr, 2 * kDeferSubs * sizeof(uint32_t)) != hipSuccess ||
+        hipMemsetAsync(d.ctr, 0, 2 * kDeferSubs * sizeof(uint32_t), s) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(d.ent);
+        return DeferList{nullptr, nullptr, 0, 0};
+    }
+    lists.emplace_back(dev, s, d);
+    return d;
+}
+
 int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const double *inv, int grid, int block,
                   int path, uint32_t *amb, void *stream) {
     MPX_CHECK_ARG(npix >= 0, "npix must be >= 0");
@@ -1929,8 +2146,29 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
             // registers ranked in the last 16-class set: an even count (padded classes never win)
             const int last = nc > 16 ? nc - 16 : nc;
-#define MPX_MFMA16(NSET, NR) \
-    hipLaunchKernelGGL((classify_mfma16_kernel<NSET, NR>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, hp, fp, amb)
+            static const int m16var = [] {  // TEMPORARY A/B (round 6): bit 1 = no device list, bit 2 = looped kernel only
+                const char *e = std::getenv("MPX_CLS_M16_VAR");
+                return e ? std::atoi(e) : 0;
+            }();
+            // whole blocks of kM16Trips x 256 vectors to the one-shot kernel (with the
+            // device deferral list), the rest looped
+            const int64_t want = (m16var & 6) ? 0 : nvec / (256 * kM16Trips);
+            const DeferList dl = want > 0 ? defer_list(s, true) : DeferList{nullptr, nullptr, 0, 0};
+            const int64_t nblk = dl.ent != nullptr ? want : 0;
+            const int64_t vdone = nblk * 256 * kM16Trips;
+            uint32_t *rimg = img + 4 * vdone;
+            const int64_t rvec = nvec - vdone;
+            const int gr = (int)std::min<int64_t>((rvec + 255) / 256, g);
+            const DeferList none{nullptr, nullptr, 0, 0};
+#define MPX_MFMA16(NSET, NR)                                                                                          \
+    do {                                                                                                              \
+        if (nblk > 0)                                                                                                 \
+            hipLaunchKernelGGL((classify_mfma16t_kernel<NSET, NR, 1>), dim3((unsigned)nblk), dim3(256), 0, s, img, nc, cp, \
+                               hp, fp, dl, amb);                                                                      \
+        if (rvec > 0)                                                                                                 \
+            hipLaunchKernelGGL((classify_mfma16_kernel<NSET, NR, 1>), dim3(gr), dim3(256), 0, s, rimg, rvec, nc, cp, hp, \
+                               fp, none, amb);                                                                        \
+    } while (0)
             if (nc <= 16) {
                 switch ((last + 1) / 2) {
                     case 1: MPX_MFMA16(1, 2); break;
@@ -1953,6 +2191,11 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             }
 #undef MPX_MFMA16
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            if (nblk > 0) {
+                hipLaunchKernelGGL(classify_fixup_kernel, dim3(kDeferSubs * kFixupParts), dim3(256), 0, s, img, dl, nc, cp, fp,
+                                   amb);
+                MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
+            }
             done = nvec * 4;
         }
     } else if (chosen == MPX_CLS_MFMA8) {

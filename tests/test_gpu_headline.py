@@ -63,7 +63,7 @@ def lab3_8192():
 
 
 @pytest.mark.parametrize("nc", [4, 16, 32])
-@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8", "auto"])
+@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8", "mfma16", "auto"])
 def test_classify_8192_every_pixel(gpu, lab3_8192, nc, path):
     img, ref = lab3_8192
     mu, inv, cls = ref[nc]
@@ -163,7 +163,7 @@ def test_classify_8192_nc32_vs_torch_fp64_oracle(gpu, lab3_8192):
     best = torch.empty(n, dtype=torch.uint8)
     for s0 in range(0, n, chunk):  # torch ops on the GPU, no framework kernel
         best[s0:s0 + chunk] = torch.argmin(_ref.classify_dist(px[s0:s0 + chunk], mu, inv, device=gpu), dim=1)
-    for path in ("fast", "mfma", "mfma64", "mfma8", "auto"):
+    for path in ("fast", "mfma", "mfma64", "mfma8", "mfma16", "auto"):
         d = img.to(gpu)
         ops.classify_(d, mu, inv, path=path)
         got = d.cpu()[..., 3].reshape(-1)

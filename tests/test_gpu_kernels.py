@@ -200,7 +200,7 @@ def test_classify_ground_truth(gpu):
         assert img_to_bytes(d) == gt, path
 
 
-CLS_PATHS = ("direct", "fast", "mfma", "mfma64", "mfma8", "auto")
+CLS_PATHS = ("direct", "fast", "mfma", "mfma64", "mfma8", "mfma16", "auto")
 
 
 def _random_classes(img, nc, npts, seed):
@@ -309,7 +309,7 @@ def test_classify_mfma8_small_class_counts(gpu, nc):
     assert amb.item() < 0.04 * img.shape[0] * img.shape[1]
 
 
-@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8"])
+@pytest.mark.parametrize("path", ["fast", "mfma", "mfma64", "mfma8", "mfma16"])
 def test_classify_exact_ties_all_fall_back(gpu, path):
     """Duplicated classes tie exactly on every pixel: every pixel must take the
     fp64 chain and keep the lowest class index (reference strict '<')."""
@@ -324,6 +324,44 @@ def test_classify_exact_ties_all_fall_back(gpu, path):
     assert torch.equal(d.cpu(), cpu)
     assert (cpu[..., 3] != 2).all()
     assert amb.item() >= int((cpu[..., 3] == 0).sum())  # every class-0 pixel tied with class 2
+
+
+@pytest.mark.parametrize("nc", [1, 2, 3, 4, 5, 8, 11, 16, 17, 20, 23, 28, 32])
+def test_classify_mfma16_class_counts(gpu, nc):
+    """mfma16 (f16 MFMA, one pixel per lane): every ranked-register count on
+    both the one-shot kernel (whole 1024-vector blocks, device deferral list +
+    fix-up kernel) and the looped tail (the rest of the image): uniform random
+    pixels, classes identical to the CPU reference, the fallback rare."""
+    img = rand_img(517, 643, seed=nc)  # 332431 pixels: 81 one-shot blocks + a looped tail + 3 scalar pixels
+    mu, inv = ops.class_stats(img, _random_classes(img, nc, 64, 200 + nc))
+    cpu = img.clone()
+    ops.classify_(cpu, mu, inv)
+    assert ops.classify_plan(mu, inv, "mfma16")[0] == "mfma16"
+    d = img.to(gpu)
+    amb = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.classify_(d, mu, inv, path="mfma16", ambiguous=amb)
+    assert torch.equal(d.cpu(), cpu)
+    assert amb.item() < 0.01 * img.shape[0] * img.shape[1]
+
+
+def test_classify_mfma16_list_reuse_and_overflow(gpu):
+    """The device deferral list is reused across calls on one stream (counter
+    sets alternate; the fix-up zeroes the next call's set): a large image, a
+    small one (no list), an image whose every pixel ties (the list overflows
+    into the in-wave re-ranking), then large again — every result identical
+    to the CPU reference."""
+    big = rand_img(1024, 1536, seed=1)
+    small = rand_img(31, 29, seed=2)
+    mu, inv = ops.class_stats(big, _random_classes(big, 20, 64, 9))
+    pts = _random_classes(big, 2, 30, 5)
+    mu_t, inv_t = ops.class_stats(big, [pts[0], pts[1], pts[0]])
+    tied = rand_img(2048, 2560, seed=3)  # 5.2M tied pixels: more entries than a sub-list holds
+    for img, m, iv in ((big, mu, inv), (small, mu, inv), (tied, mu_t, inv_t), (big, mu, inv), (big, mu_t, inv_t)):
+        cpu = img.clone()
+        ops.classify_(cpu, m, iv)
+        d = img.to(gpu)
+        ops.classify_(d, m, iv, path="mfma16")
+        assert torch.equal(d.cpu(), cpu)
 
 
 def test_classify_unaligned_view(gpu):
