@@ -97,6 +97,10 @@ def parse_args(argv=None):
                         "(0 = skip)")
     p.add_argument("--size", type=int, default=4096,
                    help="image side: per GPU slab (weak layout) or of the one global image (strong layout)")
+    p.add_argument("--steady-ms", type=float, default=300.0,
+                   help="value_steady: after this much continuous load, --steady-windows windows of the same K "
+                        "rotated steps, with the board's clock / power sampled over them on every rank (0 = skip)")
+    p.add_argument("--steady-windows", type=int, default=5)
     p.add_argument("--layout", choices=["weak", "strong"], default="weak",
                    help="weak: a size x size slab per rank; strong: one size x size image split over the ranks")
     p.add_argument("--filter", default="sobel5")
@@ -281,6 +285,37 @@ def run(args) -> int:
         sustained = timed(rot_step, args.steps).job_s
         watchdog.beat()
 
+    # steady state (VERDICT r5 Next #4): the same K rotated steps in several
+    # windows after >= steady_ms of load, with the board's clocks and power
+    # sampled over exactly those windows (a sampler of their own, started
+    # after the headline phase so it cannot disturb it)
+    steady = None
+    if args.steady_ms > 0 and graph is None:
+        ssam = None
+        if ctx.device.type == "cuda":
+            from cuda_mpi_openmp_amd.utils.clocks import ClockSampler
+
+            ssam = ClockSampler(hz=100, bdf=device_id(ctx.device)).start()
+        settle(rot_step, len(dets), args.steady_ms, ctx, sync, watchdog, parallel, lambda: [d.finish() for d in dets])
+        wins = []
+        for wi in range(max(1, args.steady_windows)):
+            cyc[0] = 0
+            timed.phase = f"steady{wi}"
+            wins.append(timed(rot_step, args.steps).job_s)
+            watchdog.beat()
+        t_lo = min(phases[f"steady{wi}"][0] for wi in range(len(wins)))
+        t_hi = max(phases[f"steady{wi}"][1] for wi in range(len(wins)))
+        for wi in range(len(wins)):
+            phases.pop(f"steady{wi}", None)
+        mine = None
+        if ssam is not None:
+            from cuda_mpi_openmp_amd.utils.clocks import key_fields
+
+            ssam.stop()
+            mine = key_fields(ssam.summary(t_lo, t_hi, pad_ns=3_000_000))
+            mine.update(source=ssam.source, error=ssam.error)
+        steady = {"wins": wins, "clocks": parallel.all_gather_object(mine, ctx)}
+
     warm = warm1 = None
     if not args.no_warm:
         # one input re-convolved: cache-resident, so it gets the resident-input
@@ -437,6 +472,12 @@ def run(args) -> int:
             rec["value_sustained"] = _sig(pixels / sustained / 1e9)
             rec["ms_per_step_sustained"] = round(sustained * 1e3 / max(1, args.steps), 5)
             rec["sustain_ms"] = args.sustain_ms
+        if steady is not None:
+            w = steady["wins"]
+            rec["value_steady"] = _sig(pixels * len(w) / sum(w) / 1e9)
+            rec["value_steady_windows"] = [_sig(pixels / x / 1e9) for x in w]
+            rec["steady_ms"] = args.steady_ms
+            rec["steady_clocks"] = steady["clocks"]  # per rank: gfxclk / power medians over the windows
         if warm is not None:
             rec["value_warm_cache"] = _sig(pixels / warm / 1e9)
             rec["ms_per_step_warm_cache"] = round(warm * 1e3 / max(1, args.steps), 5)

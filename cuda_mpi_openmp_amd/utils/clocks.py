@@ -71,6 +71,21 @@ def _flatten(m: dict) -> Dict[str, float]:
     return out
 
 
+def _try(fn):
+    try:
+        return fn()
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def _bdf_match(full: Optional[str], bdf: str) -> bool:
+    """``full`` ("0000:03:00.0") names the device ``bdf`` ("0000:03:00")?"""
+    if not full:
+        return False
+    f, b = full.lower().strip(), bdf.lower().strip()
+    return f == b or f.startswith(b + ".")
+
+
 class _AmdSmi:
     def __init__(self, bdf: Optional[str]):
         import amdsmi
@@ -83,13 +98,13 @@ class _AmdSmi:
                 raise RuntimeError("amdsmi: no GPU handles")
             self.h = hs[0]
             if bdf:
-                for h in hs:
-                    try:
-                        if amdsmi.amdsmi_get_gpu_device_bdf(h).lower().endswith(bdf.lower()):
-                            self.h = h
-                            break
-                    except Exception:  # noqa: BLE001
-                        continue
+                # the rank's own GPU or nothing (never another GPU's
+                # clocks under this rank's name); amdsmi BDFs carry the PCI
+                # function ("0000:03:00.0"), ours stop at the device
+                mine = [h for h in hs if _bdf_match(_try(lambda h=h: amdsmi.amdsmi_get_gpu_device_bdf(h)), bdf)]
+                if not mine:
+                    raise RuntimeError(f"amdsmi: no GPU with BDF {bdf}")
+                self.h = mine[0]
             self.read()  # fail here, not in the thread
         except Exception:
             self.close()  # the library was initialised: shut it down before falling back
@@ -106,10 +121,12 @@ class _AmdSmi:
 
 
 class _Hwmon:
-    def __init__(self, card: Optional[str] = None):
+    def __init__(self, bdf: Optional[str] = None):
         cands = sorted(glob.glob("/sys/class/drm/card*/device/hwmon/hwmon*"))
-        if card:
-            cands = [c for c in cands if f"/{card}/" in c] or cands
+        if bdf:  # the card whose PCI device is this rank's GPU, or nothing
+            cands = [c for c in cands if _bdf_match(os.path.basename(os.path.realpath(c.split("/hwmon/")[0])), bdf)]
+            if not cands:
+                raise RuntimeError(f"hwmon: no card with BDF {bdf}")
         if not cands:
             raise RuntimeError("no hwmon directory for a GPU")
         self.d = cands[0]
@@ -152,7 +169,7 @@ class ClockSampler:
         self.error: Optional[str] = None
         self._src = None
         errs = []
-        for name, mk in (("amdsmi", lambda: _AmdSmi(bdf)), ("hwmon", _Hwmon)):
+        for name, mk in (("amdsmi", lambda: _AmdSmi(bdf)), ("hwmon", lambda: _Hwmon(bdf))):
             try:
                 self._src = mk()
                 self.source = name
@@ -193,8 +210,12 @@ class ClockSampler:
         self._stop.set()
         if self._t is not None:
             self._t.join(timeout=2.0)
+            if self._t.is_alive():  # still inside a read: never close the source under it
+                self.error = (self.error or "") + "sampler thread did not exit within 2 s; source left open"
+                return
         if self._src is not None:
             self._src.close()
+            self._src = None
 
     def __enter__(self):
         return self.start()

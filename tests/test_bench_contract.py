@@ -74,6 +74,10 @@ def test_bench_measurement_hygiene_fields_cpu():
     assert rec["value_sustained"] > 0 and rec["sustain_ms"] == 50.0
     assert abs(rec["value_sustained"] - 64 * 64 / (rec["ms_per_step_sustained"] * 1e-3) / 1e9) \
         < 1e-3 * max(1.0, rec["value_sustained"])
+    # steady state (VERDICT r5 Next #4): K-step windows after >= 300 ms of load,
+    # with a clock record per rank (None on the CPU)
+    assert rec["value_steady"] > 0 and len(rec["value_steady_windows"]) == 5 and rec["steady_ms"] == 300.0
+    assert rec["steady_clocks"] == [None]
     assert rec["cpu_runs"] >= 5 and 0 < rec["cpu_ms_per_image_min"] <= rec["cpu_ms_per_image"]
     # the host's enqueue time of the timed steps rides along, never above the step time
     assert 0 < rec["host_enqueue_ms_per_step"] <= rec["ms_per_step"]

@@ -37,3 +37,40 @@ def test_sampler_without_gpu_reports_why():
         cs.start()
     finally:
         cs.stop()
+
+
+def test_bdf_matching_is_strict():
+    """a rank's clocks come from its own GPU or from nowhere."""
+    assert clocks._bdf_match("0000:03:00.0", "0000:03:00") and clocks._bdf_match("0000:03:00.0", "0000:03:00.0")
+    assert not clocks._bdf_match("0000:13:00.0", "0000:03:00") and not clocks._bdf_match(None, "0000:03:00")
+    cs = clocks.ClockSampler(hz=50, bdf="ffff:ff:1f")  # no such device anywhere
+    assert cs.source is None and cs.error
+
+
+def test_stop_leaves_a_busy_source_open():
+    """stop() never closes the metrics source under a read still in
+    flight (the join timed out): it records why instead."""
+    import threading
+    import time
+
+    gate = threading.Event()
+
+    class Slow:
+        closed = False
+
+        def read(self):
+            gate.wait(10)
+            return {}
+
+        def close(self):
+            Slow.closed = True
+
+    cs = clocks.ClockSampler.__new__(clocks.ClockSampler)
+    cs.period, cs.samples, cs.read_us, cs.error, cs._src, cs.source = 0.01, [], [], None, Slow(), "fake"
+    cs._stop, cs._t = threading.Event(), None
+    cs.start()
+    time.sleep(0.05)  # the thread is inside read()
+    cs.stop()         # join(2 s) times out
+    assert not Slow.closed and "did not exit" in cs.error
+    gate.set()
+    cs._t.join(5)
