@@ -63,43 +63,40 @@ struct FastParams {
     float T2;                         // decision margin 2 * max_c tol_c
 };
 
+// one class of the reference chain
+#define MPX_DIRECT_CLASS(c)                                                                               \
+    do {                                                                                                  \
+        const double d0 = pr - cp.mu[3 * (c) + 0];                                                        \
+        const double d1 = pg - cp.mu[3 * (c) + 1];                                                        \
+        const double d2 = pb - cp.mu[3 * (c) + 2];                                                        \
+        const double *A = cp.A + 9 * (c);                                                                 \
+        double t0 = fma(d0, A[0], 0.0), t1 = fma(d0, A[1], 0.0), t2 = fma(d0, A[2], 0.0);                \
+        t0 = fma(d1, A[3], t0);                                                                           \
+        t1 = fma(d1, A[4], t1);                                                                           \
+        t2 = fma(d1, A[5], t2);                                                                           \
+        t0 = fma(d2, A[6], t0);                                                                           \
+        t1 = fma(d2, A[7], t1);                                                                           \
+        t2 = fma(d2, A[8], t2);                                                                           \
+        double dist = fma(t0, d0, 0.0);                                                                   \
+        dist = fma(t1, d1, dist);                                                                         \
+        dist = fma(t2, d2, dist);                                                                         \
+        if (dist < best) {                                                                                \
+            best = dist;                                                                                  \
+            cls = (c);                                                                                    \
+        }                                                                                                 \
+    } while (0)
+
 __device__ __forceinline__ uint32_t classify_direct(uint32_t p, int nc, const ClassParams &cp) {
     const double pr = (double)mpx_px_r(p), pg = (double)mpx_px_g(p), pb = (double)mpx_px_b(p);
     double best = 1.7976931348623157e308;  // DBL_MAX
     int cls = -1;
-    auto one = [&](int c) {
-        const double d0 = pr - cp.mu[3 * c + 0];
-        const double d1 = pg - cp.mu[3 * c + 1];
-        const double d2 = pb - cp.mu[3 * c + 2];
-        const double *A = cp.A + 9 * c;
-        double t0 = fma(d0, A[0], 0.0), t1 = fma(d0, A[1], 0.0), t2 = fma(d0, A[2], 0.0);
-        t0 = fma(d1, A[3], t0);
-        t1 = fma(d1, A[4], t1);
-        t2 = fma(d1, A[5], t2);
-        t0 = fma(d2, A[6], t0);
-        t1 = fma(d2, A[7], t1);
-        t2 = fma(d2, A[8], t2);
-        double dist = fma(t0, d0, 0.0);
-        dist = fma(t1, d1, dist);
-        dist = fma(t2, d2, dist);
-        if (dist < best) {
-            best = dist;
-            cls = c;
-        }
-    };
-    // four classes per trip: their parameters arrive in one batch of scalar
-    // loads (one s_load wait per class made the deferred stages
-    // latency-bound, round 6); the classes stay in order (strict '<')
-    int c = 0;
-    for (; c + 4 <= nc; c += 4) {
-        one(c);
-        one(c + 1);
-        one(c + 2);
-        one(c + 3);
-    }
-    for (; c < nc; ++c) one(c);
+    // a plain loop: unrolled, the dynamic class index into the by-value kernel
+    // argument made the compiler copy all of ClassParams to scratch (3080 B
+    // per lane) in every kernel that inlines this chain (round 6)
+    for (int c = 0; c < nc; ++c) MPX_DIRECT_CLASS(c);
     return (p & 0x00ffffffu) | ((uint32_t)(uint8_t)cls << 24);
 }
+#undef MPX_DIRECT_CLASS
 
 __global__ void classify_direct_kernel(uint32_t *__restrict__ img, int64_t npix, int nc, ClassParams cp,
                                        int vec) {
@@ -185,21 +182,24 @@ __device__ __forceinline__ bool classify_fp32_one(uint32_t p, int nc, const Fast
                 b = (float)((p >> 16) & 0xffu) - 128.0f;
     const float f[9] = {r * r, g * g, b * b, r * g, r * b, g * b, r, g, b};
     uint32_t B = kKeyInit, S = kKeyInit;
-    auto one = [&](int c) {
+    int c = 0;
+    for (; c + 4 <= nc; c += 4) {  // one batch of scalar loads per four classes
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float *w = fp.w[c + j];
+            float d = w[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) d = fmaf(w[k], f[k], d);
+            rank_key(make_key(d, (uint32_t)(c + j)), B, S);
+        }
+    }
+    for (; c < nc; ++c) {
         const float *w = fp.w[c];
         float d = w[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) d = fmaf(w[k], f[k], d);
         rank_key(make_key(d, (uint32_t)c), B, S);
-    };
-    int c = 0;
-    for (; c + 4 <= nc; c += 4) {  // one batch of scalar loads per four classes
-        one(c);
-        one(c + 1);
-        one(c + 2);
-        one(c + 3);
     }
-    for (; c < nc; ++c) one(c);
     out = (p & 0x00ffffffu) | ((B & 31u) << 24);
     return decided(B, S, fp.T2);
 }
@@ -216,38 +216,19 @@ __device__ __forceinline__ bool classify_fp32_one(uint32_t p, int nc, const Fast
 // ---------------------------------------------------------------------------
 constexpr int kAmbCap = 512;
 
-// NQ: 16-B vectors (4 pixels each) per thread and loop trip; nvec counts
-// groups of NQ vectors. OPT (tuning, MPX_CLS_OPT): bit 1 non-temporal loads,
-// bit 2 non-temporal stores, bit 8 interleaved FMA chains without inline asm,
-// bit 16 two trips of loads in flight instead of one,
-// bit 4 wave-contiguous vectors (vector qq of a
-// thread at wave base * NQ + 64 qq + lane, so every load / store instruction
-// covers 1 KiB of consecutive bytes; nvec must then be a multiple of 64).
-typedef uint32_t cls_u32x4 __attribute__((ext_vector_type(4)));  // the nontemporal builtins take clang vectors
-template <int OPT>
-__device__ __forceinline__ uint4 cls_load(const uint4 *p) {
-    if constexpr (OPT & 1) {
-        const cls_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const cls_u32x4 *>(p));
-        return make_uint4(x[0], x[1], x[2], x[3]);
-    }
-    return *p;
-}
-template <int OPT>
-__device__ __forceinline__ void cls_store(uint4 *p, uint4 x) {
-    if constexpr (OPT & 2)
-        __builtin_nontemporal_store(cls_u32x4{x.x, x.y, x.z, x.w}, reinterpret_cast<cls_u32x4 *>(p));
-    else
-        *p = x;
-}
-template <int NQ, int OPT>
-__device__ __forceinline__ int64_t cls_vec(int64_t i, int qq) {
-    if constexpr (OPT & 4) return (i & ~63ll) * NQ + qq * 64 + (i & 63);
-    return i * NQ + qq;
-}
+// NQ = 2 16-B vectors (8 pixels) per thread and loop trip (nvec counts pairs
+// of vectors): 8192^2, nc 4 / 16 / 32: 126 / 357-359 / 616-626 µs against 127
+// / 361-365 / 638-641 with one (round 3). The pairs' FMA chains are issued
+// interleaved (each FMA's result is needed NP / 2 instructions later, not by
+// the next one) and the top-2 step is plain C (v_med3_u32 by pattern, no
+// inline asm): nc = 16 / 32 307.6 -> 302.3 / 526.8 -> 521.7 µs (round 4).
+// Non-temporal loads / stores, wave-contiguous vectors and two trips of loads
+// in flight measured neutral (profiles/lab3_classify.md) and were removed.
+constexpr int kFastNQ = 2;
 
-template <int NQ, int OPT = 0>
 __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, FastParams fp, uint32_t *amb) {
+    constexpr int NQ = kFastNQ;
     constexpr int NP = 4 * NQ;  // pixels per thread and trip
     __shared__ int64_t s_amb[kAmbCap];
     __shared__ uint32_t s_ambpx[kAmbCap];
@@ -257,12 +238,12 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     uint4 *v = reinterpret_cast<uint4 *>(img);
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // software-pipelined grid-stride loop: the next 16-B vector is in flight
-    // while this one is ranked (a thread walks ~32 vectors at 8192^2; without
+    // software-pipelined grid-stride loop: the next 16-B vectors are in flight
+    // while these are ranked (a thread walks ~32 vectors at 8192^2; without
     // the prefetch each step exposes a full HBM round trip)
     auto load_q = [&](uint4 (&q)[NQ], int64_t it) {
 #pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) q[qq] = it < nvec ? cls_load<OPT>(v + cls_vec<NQ, OPT>(it, qq)) : uint4{};
+        for (int qq = 0; qq < NQ; ++qq) q[qq] = it < nvec ? v[it * NQ + qq] : uint4{};
     };
     auto unpack = [&](const uint4 (&q)[NQ], uint32_t (&px)[NP]) {
 #pragma unroll
@@ -302,35 +283,21 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
         for (int q = 0; q < NP; ++q) B[q] = S[q] = kKeyInit;
         auto one_class = [&](int c) {
             const float *w = fp.w[c];
-            if constexpr (OPT & 8) {
-                // the pairs' FMA chains interleaved (each FMA's result is
-                // needed NP / 2 instructions later, not by the next one), the
-                // top-2 step in plain C (v_med3_u32 by pattern, no inline asm)
-                f2_t d[NP / 2];
+            f2_t d[NP / 2];
 #pragma unroll
-                for (int h = 0; h < NP / 2; ++h) d[h] = f2_t{w[9], w[9]};
+            for (int h = 0; h < NP / 2; ++h) d[h] = f2_t{w[9], w[9]};
 #pragma unroll
-                for (int k = 0; k < 9; ++k)
+            for (int k = 0; k < 9; ++k)
 #pragma unroll
-                    for (int h = 0; h < NP / 2; ++h) d[h] = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d[h]);
+                for (int h = 0; h < NP / 2; ++h) d[h] = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d[h]);
 #pragma unroll
-                for (int h = 0; h < NP / 2; ++h) {
+            for (int h = 0; h < NP / 2; ++h) {
 #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        const uint32_t k = make_key_s(q ? d[h].y : d[h].x, (uint32_t)c);
-                        uint32_t &Bq = B[2 * h + q], &Sq = S[2 * h + q];
-                        Sq = max(min(Bq, k), min(max(Bq, k), Sq));
-                        Bq = min(Bq, k);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int h = 0; h < NP / 2; ++h) {
-                    f2_t d = {w[9], w[9]};
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) d = __builtin_elementwise_fma(f2_t{w[k], w[k]}, f[h][k], d);
-                    rank_key(make_key_s(d.x, (uint32_t)c), B[2 * h], S[2 * h]);
-                    rank_key(make_key_s(d.y, (uint32_t)c), B[2 * h + 1], S[2 * h + 1]);
+                for (int q = 0; q < 2; ++q) {
+                    const uint32_t k = make_key_s(q ? d[h].y : d[h].x, (uint32_t)c);
+                    uint32_t &Bq = B[2 * h + q], &Sq = S[2 * h + q];
+                    Sq = max(min(Bq, k), min(max(Bq, k), Sq));
+                    Bq = min(Bq, k);
                 }
             }
         };
@@ -351,7 +318,7 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             if (__builtin_expect(!decided(B[k], S[k], fp.T2), 0)) {
                 const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count (one global add at the end)
                 if (slot < (uint32_t)kAmbCap) {  // deferred
-                    s_amb[slot] = cls_vec<NQ, OPT>(i, k >> 2) * 4 + (k & 3);
+                    s_amb[slot] = (i * NQ + (k >> 2)) * 4 + (k & 3);
                     s_ambpx[slot] = px[k];
                 } else {
                     o[k] = classify_direct(px[k], nc, cp);
@@ -359,42 +326,15 @@ __global__ __launch_bounds__(256) void classify_fast32_kernel(uint32_t *__restri
             }
         }
 #pragma unroll
-        for (int qq = 0; qq < NQ; ++qq)
-            cls_store<OPT>(v + cls_vec<NQ, OPT>(i, qq), make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]));
+        for (int qq = 0; qq < NQ; ++qq) v[i * NQ + qq] = make_uint4(o[4 * qq], o[4 * qq + 1], o[4 * qq + 2], o[4 * qq + 3]);
     };
-    if constexpr ((OPT & 16) != 0) {
-        // two trips of loads in flight: two register sets in fixed roles (a
-        // copy between them would wait for the copied loads); each set is
-        // unpacked and re-issued for the trip after next before its pixels
-        // are ranked
-        uint4 qa[NQ], qb[NQ];
-        load_q(qa, i);
-        load_q(qb, i + stride);
-        while (i < nvec) {
-            {
-                uint32_t px[NP];
-                unpack(qa, px);
-                if (i + 2 * stride < nvec) load_q(qa, i + 2 * stride);
-                rank_store(px, i);
-            }
-            if ((i += stride) >= nvec) break;
-            {
-                uint32_t px[NP];
-                unpack(qb, px);
-                if (i + 2 * stride < nvec) load_q(qb, i + 2 * stride);
-                rank_store(px, i);
-            }
-            i += stride;
-        }
-    } else {
-        uint4 qn[NQ];
-        load_q(qn, i);
-        for (; i < nvec; i += stride) {
-            uint32_t px[NP];
-            unpack(qn, px);
-            if (i + stride < nvec) load_q(qn, i + stride);
-            rank_store(px, i);
-        }
+    uint4 qn[NQ];
+    load_q(qn, i);
+    for (; i < nvec; i += stride) {
+        uint32_t px[NP];
+        unpack(qn, px);
+        if (i + stride < nvec) load_q(qn, i + stride);
+        rank_store(px, i);
     }
     __syncthreads();
     const uint32_t nd = min(s_namb, (uint32_t)kAmbCap);
@@ -770,20 +710,15 @@ __device__ __forceinline__ uint32_t mfma8_chunk(const uint4 &q, const Mfma8Lane 
     return undecided;
 }
 
-// WIN = false (production): each chunk is stored as soon as it is ranked and the undecided
-// pixels are re-stored one by one after the block's grid-stride loop — after
-// their lines left L2, so every fix-up is a partial-line HBM write (56-71 MiB
-// per 8192^2 image, kernels_r3.md).
-// WIN = true (MPX_CLS_MFMA8_WIN=1): a block ranks kWin8 chunks per wave into LDS,
-// resolves that window's undecided pixels there (all lanes busy on the fp64
-// chain), and only then stores the window: every output byte is written once,
-// in whole 512-B chunk runs.
-constexpr int kWin8 = 4;
-constexpr int kAmb8WinCap = 1024;  // undecided pixels per window (of 4 x 4 x 128)
-
+// Each chunk is stored as soon as it is ranked and the undecided pixels are
+// re-stored one by one after the block's grid-stride loop (partial-line HBM
+// writes: 56-71 MiB per 8192^2 image, kernels_r3.md). Ranking a window of
+// chunks into LDS and resolving its undecided pixels before one whole store
+// wrote every byte once (1.03x the image against 1.22x) but ran 434-444 ->
+// 523 µs at nc = 32 (three barriers per window): retired (round 6).
 constexpr int kAmb8Cap2 = 256;  // pixels the fp32 stage leaves to the fp64 chain, per block
 
-template <int NREG, bool WIN>
+template <int NREG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void classify_mfma8_kernel(uint32_t *__restrict__ img, int64_t nchunks, int nc,
                                                              ClassParams cp, I8Params ip, FastParams fp, uint32_t *amb) {
     const int lane = threadIdx.x & 63;
@@ -792,135 +727,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     const Mfma8Lane L = mfma8_lane(ip, lane);
     uint4 *v = reinterpret_cast<uint4 *>(img);
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    if constexpr (!WIN) {
-        __shared__ int64_t s_amb[kAmb8Cap];
-        __shared__ uint32_t s_ambpx[kAmb8Cap];
-        __shared__ uint32_t s_namb;
-        if (threadIdx.x == 0) s_namb = 0;
-        __syncthreads();
-        const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        int64_t ch = wave;
-        uint4 qn = ch < nchunks ? v[ch * 32 + col] : uint4{};
-        for (; ch < nchunks; ch += nwaves) {
-            const uint4 q = qn;
-            if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
-            uint4 o;
-            const uint32_t und = mfma8_chunk<NREG>(q, L, ip.T2, o);
-            if (h == 0) {
-                const uint32_t px[4] = {q.x, q.y, q.z, q.w};
-                uint32_t *op = &o.x;
+    __shared__ int64_t s_amb[kAmb8Cap];
+    __shared__ uint32_t s_ambpx[kAmb8Cap];
+    __shared__ uint32_t s_namb;
+    if (threadIdx.x == 0) s_namb = 0;
+    __syncthreads();
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    int64_t ch = wave;
+    uint4 qn = ch < nchunks ? v[ch * 32 + col] : uint4{};
+    for (; ch < nchunks; ch += nwaves) {
+        const uint4 q = qn;
+        if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
+        uint4 o;
+        const uint32_t und = mfma8_chunk<NREG>(q, L, ip.T2, o);
+        if (h == 0) {
+            const uint32_t px[4] = {q.x, q.y, q.z, q.w};
+            uint32_t *op = &o.x;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    if (__builtin_expect((und >> m) & 1u, 0)) {
-                        const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count
-                        if (slot < (uint32_t)kAmb8Cap) {
-                            s_amb[slot] = (ch * 32 + col) * 4 + m;
-                            s_ambpx[slot] = px[m];
-                        } else {
-                            op[m] = classify_direct(px[m], nc, cp);
-                        }
-                    }
-                }
-                v[ch * 32 + col] = o;
-            }
-        }
-        __shared__ int64_t s_amb2[kAmb8Cap2];
-        __shared__ uint32_t s_ambpx2[kAmb8Cap2];
-        __shared__ uint32_t s_namb2;
-        if (threadIdx.x == 0) s_namb2 = 0;
-        __syncthreads();
-        const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
-        if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
-        // two stages, every lane busy in each: the fp32 proven-margin ranking
-        // settles all but ~1% of the int8 path's undecided pixels (its bound is
-        // ~2^-16 of the weights' against the int8 keys' 2^-8 .. 2^-16); the
-        // rest take the exact fp64 chain together
-        for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
-            const uint32_t px = s_ambpx[j];
-            uint32_t o;
-            if (classify_fp32_one(px, nc, fp, o)) {
-                img[s_amb[j]] = o;
-            } else {
-                const uint32_t slot = atomicAdd(&s_namb2, 1u);
-                if (slot < (uint32_t)kAmb8Cap2) {
-                    s_amb2[slot] = s_amb[j];
-                    s_ambpx2[slot] = px;
-                } else {
-                    img[s_amb[j]] = classify_direct(px, nc, cp);
-                }
-            }
-        }
-        __syncthreads();
-        const uint32_t nd2 = min(s_namb2, (uint32_t)kAmb8Cap2);
-        for (uint32_t j = threadIdx.x; j < nd2; j += blockDim.x) img[s_amb2[j]] = classify_direct(s_ambpx2[j], nc, cp);
-    } else {
-        constexpr int NW = 4;  // waves per block (launch_bounds 256)
-        __shared__ uint4 s_out[kWin8][NW][32];
-        __shared__ uint16_t s_ambi[kAmb8WinCap];  // (t, wave, col, m) of an undecided pixel
-        __shared__ uint32_t s_ambpx[kAmb8WinCap];
-        __shared__ uint32_t s_namb;
-        const int wl = threadIdx.x >> 6;
-        if (threadIdx.x == 0) s_namb = 0;
-        __syncthreads();
-        const int64_t ch0 = (int64_t)blockIdx.x * NW;  // the block's first chunk; wave wl takes ch0 + wl + t nwaves
-        // block-uniform trip count (every wave passes every barrier)
-        const int64_t trips = ch0 < nchunks ? (nchunks - ch0 + nwaves - 1) / nwaves : 0;
-        uint32_t total = 0;
-        uint4 qn = ch0 + wl < nchunks ? v[(ch0 + wl) * 32 + col] : uint4{};
-        for (int64_t t0 = 0; t0 < trips; t0 += kWin8) {
-#pragma unroll 1  // one copy of the chunk body (unrolled 4x it outgrows the instruction cache)
-            for (int tt = 0; tt < kWin8; ++tt) {
-                const int64_t ch = ch0 + wl + (t0 + tt) * nwaves;
-                if (ch < nchunks) {  // wave-uniform
-                    const uint4 q = qn;
-                    if (ch + nwaves < nchunks) qn = v[(ch + nwaves) * 32 + col];
-                    uint4 o;
-                    const uint32_t und = mfma8_chunk<NREG>(q, L, ip.T2, o);
-                    if (h == 0) {
-                        const uint32_t px[4] = {q.x, q.y, q.z, q.w};
-                        uint32_t *op = &o.x;
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            if (__builtin_expect((und >> m) & 1u, 0)) {
-                                const uint32_t slot = atomicAdd(&s_namb, 1u);
-                                if (slot < (uint32_t)kAmb8WinCap) {
-                                    s_ambi[slot] = (uint16_t)((((tt * NW + wl) * 32 + col) << 2) | m);
-                                    s_ambpx[slot] = px[m];
-                                } else {
-                                    op[m] = classify_direct(px[m], nc, cp);
-                                }
-                            }
-                        }
-                        s_out[tt][wl][col] = o;
+            for (int m = 0; m < 4; ++m) {
+                if (__builtin_expect((und >> m) & 1u, 0)) {
+                    const uint32_t slot = atomicAdd(&s_namb, 1u);  // also the block's count
+                    if (slot < (uint32_t)kAmb8Cap) {
+                        s_amb[slot] = (ch * 32 + col) * 4 + m;
+                        s_ambpx[slot] = px[m];
+                    } else {
+                        op[m] = classify_direct(px[m], nc, cp);
                     }
                 }
             }
-            __syncthreads();
-            const uint32_t na = s_namb;
-            const uint32_t nd = min(na, (uint32_t)kAmb8WinCap);
-            for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
-                const uint32_t e = s_ambi[j], px = s_ambpx[j];
-                uint32_t o;
-                if (!classify_fp32_one(px, nc, fp, o)) o = classify_direct(px, nc, cp);  // fp64 only where fp32 cannot decide
-                reinterpret_cast<uint32_t *>(&s_out[0][0][0])[e] = o;
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                total += na;
-                s_namb = 0;
-            }
-            // the window's chunks, whole: thread -> (tt, wave, col) over 512 uint4
-#pragma unroll
-            for (int k = 0; k < kWin8 * NW * 32 / 256; ++k) {
-                const int e = threadIdx.x + k * 256;
-                const int tt = e / (NW * 32), w2 = (e / 32) % NW, c2 = e % 32;
-                const int64_t ch = ch0 + w2 + (t0 + tt) * nwaves;
-                if (t0 + tt < trips && ch < nchunks) v[ch * 32 + c2] = s_out[tt][w2][c2];
-            }
-            __syncthreads();  // s_out and s_namb are rewritten by the next window
+            v[ch * 32 + col] = o;
         }
-        if (amb && threadIdx.x == 0 && total) atomicAdd(amb, total);  // one global add per block
     }
+    __shared__ int64_t s_amb2[kAmb8Cap2];
+    __shared__ uint32_t s_ambpx2[kAmb8Cap2];
+    __shared__ uint32_t s_namb2;
+    if (threadIdx.x == 0) s_namb2 = 0;
+    __syncthreads();
+    const uint32_t nd = min(s_namb, (uint32_t)kAmb8Cap);
+    if (amb && threadIdx.x == 0 && s_namb) atomicAdd(amb, s_namb);  // one global add per block
+    // two stages, every lane busy in each: the fp32 proven-margin ranking
+    // settles all but ~1% of the int8 path's undecided pixels (its bound is
+    // ~2^-16 of the weights' against the int8 keys' 2^-8 .. 2^-16); the
+    // rest take the exact fp64 chain together
+    for (uint32_t j = threadIdx.x; j < nd; j += blockDim.x) {
+        const uint32_t px = s_ambpx[j];
+        uint32_t o;
+        if (classify_fp32_one(px, nc, fp, o)) {
+            img[s_amb[j]] = o;
+        } else {
+            const uint32_t slot = atomicAdd(&s_namb2, 1u);
+            if (slot < (uint32_t)kAmb8Cap2) {
+                s_amb2[slot] = s_amb[j];
+                s_ambpx2[slot] = px;
+            } else {
+                img[s_amb[j]] = classify_direct(px, nc, cp);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nd2 = min(s_namb2, (uint32_t)kAmb8Cap2);
+    for (uint32_t j = threadIdx.x; j < nd2; j += blockDim.x) img[s_amb2[j]] = classify_direct(s_ambpx2[j], nc, cp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1039,13 +905,9 @@ __device__ __forceinline__ uint32_t mfma8s_pixel(uint32_t p, const Mfma8sLane<NS
 constexpr int kAmb8sCapW = 256;   // deferred (vector, mask) entries per wave
 constexpr int kAmb8sCap2W = 64;   // pixels the fp32 stage leaves to the fp64 chain, per wave
 
-// PF: trips of loads in flight (1: the next trip's 16 B under this trip's
-// ranking; 2: two register sets in fixed roles, the trip after next issued
-// before this one is ranked — twice the bytes in flight per lane)
-// MEM (tuning, MPX_CLS_MFMA8S_MEM): bit 1 non-temporal loads, bit 2
-// non-temporal stores of the image vectors (cls_load / cls_store); 4 = probe:
-// the same loop without the ranking (alpha cleared; output NOT classified)
-template <int NS, int PF = 1, int MEM = 0>
+// One trip of loads in flight (two measured level, non-temporal loads /
+// stores measured neutral or slower: profiles/lab3_classify.md, round 5).
+template <int NS>
 __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, I8Params ip, FastParams fp,
                                                               uint32_t *amb) {
@@ -1063,10 +925,6 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     auto trip = [&](const uint4 q, int64_t vi) {
-        if constexpr ((MEM & 4) != 0) {  // memory-only probe
-            cls_store<MEM>(&v[vi], make_uint4(q.x & 0xffffffu, q.y & 0xffffffu, q.z & 0xffffffu, q.w & 0xffffffu));
-            return;
-        }
         const uint32_t px[4] = {q.x, q.y, q.z, q.w};
         uint32_t o[4];
         bool u[4];
@@ -1085,32 +943,13 @@ __global__ __launch_bounds__(256) void classify_mfma8s_kernel(uint32_t *__restri
                     if ((mask >> m) & 1u) o[m] = classify_direct(px[m], nc, cp);
             }
         }
-        cls_store<MEM>(&v[vi], make_uint4(o[0], o[1], o[2], o[3]));
+        v[vi] = make_uint4(o[0], o[1], o[2], o[3]);
     };
-    if constexpr (PF == 2) {
-        uint4 qa = i < nvec ? cls_load<MEM>(&v[i]) : uint4{};
-        uint4 qb = i + stride < nvec ? cls_load<MEM>(&v[i + stride]) : uint4{};
-        while (i < nvec) {
-            {
-                const uint4 q = qa;
-                if (i + 2 * stride < nvec) qa = cls_load<MEM>(&v[i + 2 * stride]);
-                trip(q, i);
-            }
-            if ((i += stride) >= nvec) break;
-            {
-                const uint4 q = qb;
-                if (i + 2 * stride < nvec) qb = cls_load<MEM>(&v[i + 2 * stride]);
-                trip(q, i);
-            }
-            i += stride;
-        }
-    } else {
-        uint4 qn = i < nvec ? cls_load<MEM>(&v[i]) : uint4{};
-        for (; i < nvec; i += stride) {
-            const uint4 q = qn;
-            if (i + stride < nvec) qn = cls_load<MEM>(&v[i + stride]);
-            trip(q, i);
-        }
+    uint4 qn = i < nvec ? v[i] : uint4{};
+    for (; i < nvec; i += stride) {
+        const uint4 q = qn;
+        if (i + stride < nvec) qn = v[i + stride];
+        trip(q, i);
     }
     // this wave's deferred pixels: the fp32 proven-margin ranking first, the
     // exact fp64 chain for what it leaves (every lane of the wave busy in each
@@ -1304,7 +1143,6 @@ __device__ __forceinline__ uint32_t mfma16_pixel(uint32_t p, const Mfma16Lane<NS
 // classes, round 6). Fix-up block b owns sub-list b: it reads its count,
 // re-ranks the entries and zeroes the count for the next launch.
 constexpr uint32_t kDeferSubs = 256;
-constexpr uint32_t kFixupParts = 4;  // fix-up blocks per sub-list (4 waves per SIMD: the stages' dependent chains overlap)
 struct DeferList {
     uint64_t *ent;  // kDeferSubs x cap entries; nullptr: re-rank inside each wave (no device list)
     uint32_t *ctr;  // 2 x kDeferSubs counters, used by calls of alternating parity
@@ -1328,37 +1166,66 @@ __device__ __forceinline__ uint32_t fix_entry(uint32_t *img, uint64_t e, int nc,
     return (uint32_t)__popc(mask);
 }
 
-// grid = kDeferSubs x kFixupParts blocks; block b takes part b / kDeferSubs of
-// sub-list b % kDeferSubs, one (entry, pixel slot) pair per thread — a thread
-// re-ranks at most one pixel per pass, so a wave's dependent fp32 / fp64
-// chains are short and four waves per SIMD overlap them (one thread per
-// entry, one wave per SIMD, ran 25-47 µs on ~50K entries). It also zeroes the
-// counters of the other parity, which the next call appends to.
+// grid = kDeferSubs blocks: block b re-ranks sub-list b in chunks of
+// kFixChunk entries, each in three block-wide phases with every lane busy:
+// expand the entries' undecided pixels into an LDS list, rank them with the
+// fp32 proven margin, and run the exact fp64 chain on the compacted rest.
+// (One thread per entry ran the fp32 and fp64 chains with a third of the
+// lanes active and the fp64 chain in nearly every wave: 25-47 µs for ~50K
+// entries, round 6.) The block also zeroes the other parity's counter, which
+// the next call appends to.
+constexpr int kFixChunk = 1024;
+
+// the exact chain alone (the one-shot kernel's rare list-overflow path: the
+// fp32 stage's registers would raise the whole kernel's VGPR count)
+__device__ __forceinline__ uint32_t fix_entry_direct(uint32_t *img, uint64_t e, int nc, const ClassParams &cp) {
+    const int64_t vi = (int64_t)(e >> 4);
+    const uint32_t mask = (uint32_t)e & 15u;
+    for (int m = 0; m < 4; ++m)
+        if ((mask >> m) & 1u) img[vi * 4 + m] = classify_direct(img[vi * 4 + m], nc, cp);
+    return (uint32_t)__popc(mask);
+}
+
 __global__ __launch_bounds__(256) void classify_fixup_kernel(uint32_t *__restrict__ img, DeferList dl, int nc,
                                                              ClassParams cp, FastParams fp, uint32_t *amb) {
-    const uint32_t sub = blockIdx.x % kDeferSubs, part = blockIdx.x / kDeferSubs;
+    __shared__ int64_t s_px[4 * kFixChunk];   // pixel indices of one chunk's undecided pixels
+    __shared__ int64_t s_px2[4 * kFixChunk];  // those the fp32 stage leaves to the fp64 chain
+    __shared__ uint32_t s_n, s_n2, s_tot;
+    const uint32_t sub = blockIdx.x;
     const uint32_t n = min(dl.ctr[dl.par * kDeferSubs + sub], dl.cap);
     const uint64_t *ent = dl.ent + (size_t)sub * dl.cap;
-    uint32_t px = 0;
-    for (uint32_t j = part * 256 + threadIdx.x; j < 4 * n; j += 256 * kFixupParts) {
-        const uint64_t e = ent[j >> 2];
-        const uint32_t m = j & 3;
-        if (!((e >> m) & 1u)) continue;
-        const int64_t vi = (int64_t)(e >> 4);
-        const uint32_t p = img[vi * 4 + m];  // RGB untouched by the provisional result
-        uint32_t o;
-        if (!classify_fp32_one(p, nc, fp, o)) o = classify_direct(p, nc, cp);
-        img[vi * 4 + m] = o;
-        ++px;
+    if (threadIdx.x == 0) s_tot = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += kFixChunk) {
+        const uint32_t cn = min(n - c0, (uint32_t)kFixChunk);
+        if (threadIdx.x == 0) s_n = s_n2 = 0;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < 4 * cn; j += 256) {  // expand
+            const uint64_t e = ent[c0 + (j >> 2)];
+            const uint32_t m = j & 3;
+            if ((e >> m) & 1u) s_px[atomicAdd(&s_n, 1u)] = (int64_t)(e >> 4) * 4 + m;
+        }
+        __syncthreads();
+        const uint32_t np = s_n;
+        for (uint32_t k = threadIdx.x; k < np; k += 256) {  // fp32 stage
+            const int64_t idx = s_px[k];
+            uint32_t o;
+            if (classify_fp32_one(img[idx], nc, fp, o))
+                img[idx] = o;
+            else
+                s_px2[atomicAdd(&s_n2, 1u)] = idx;
+        }
+        __syncthreads();
+        const uint32_t n2 = s_n2;
+        for (uint32_t k = threadIdx.x; k < n2; k += 256) {  // the exact chain, compacted
+            const int64_t idx = s_px2[k];
+            img[idx] = classify_direct(img[idx], nc, cp);
+        }
+        if (threadIdx.x == 0) s_tot += np;
+        __syncthreads();
     }
-    __shared__ uint32_t s_px;
-    if (threadIdx.x == 0) s_px = 0;
-    __syncthreads();
-    if (px) atomicAdd(&s_px, px);
-    __syncthreads();
     if (threadIdx.x == 0) {
-        if (amb && s_px) atomicAdd(amb, s_px);
-        if (part == 0) dl.ctr[(dl.par ^ 1u) * kDeferSubs + sub] = 0;
+        if (amb && s_tot) atomicAdd(amb, s_tot);
+        dl.ctr[(dl.par ^ 1u) * kDeferSubs + sub] = 0;
     }
 }
 
@@ -1366,8 +1233,8 @@ __global__ __launch_bounds__(256) void classify_fixup_kernel(uint32_t *__restric
 // trip of loads ahead, per-wave deferral lists without block barriers): the
 // remainder of an image past classify_mfma16t_kernel's whole blocks, and the
 // whole image when no device deferral list could be allocated.
-template <int NSET, int NR, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void classify_mfma16_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
+template <int NSET, int NR>
+__global__ __launch_bounds__(256) void classify_mfma16_kernel(uint32_t *__restrict__ img, int64_t nvec, int nc,
                                                               ClassParams cp, HalfParams hp, FastParams fp,
                                                               DeferList dl, uint32_t *amb) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1467,8 +1334,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // to the launch's device list and classify_fixup_kernel.
 constexpr int kM16Trips = 4;
 
-template <int NSET, int NR, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void classify_mfma16t_kernel(
+template <int NSET, int NR>
+__global__ __launch_bounds__(256) void classify_mfma16t_kernel(
     uint32_t *__restrict__ img, int nc, ClassParams cp, HalfParams hp, FastParams fp, DeferList dl, uint32_t *amb) {
     constexpr int T = kM16Trips;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1512,7 +1379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (b0 + j < dl.cap)
             ent[b0 + j] = e;
         else
-            over += fix_entry(img, e, nc, cp, fp);  // list full: this lane re-ranks it (never at benchmark rates)
+            over += fix_entry_direct(img, e, nc, cp);  // list full: this lane re-ranks it (never at benchmark rates)
     }
     if (amb && over) atomicAdd(amb, over);
 }
@@ -1974,13 +1841,8 @@ int classify_resolve_uncached(int nc, const double *mu, const double *inv, int p
     // mfma8 re-ranks its undecided pixels in fp32 first: its FastParams too
     // (T2 = +inf when the fp32 bound cannot be proven: the fp64 chain then
     // takes every undecided pixel)
-    // (MPX_CLS_MFMA8_FP32=0, A/B: every undecided pixel to the fp64 chain)
-    static const bool fp32_stage = [] {
-        const char *e = std::getenv("MPX_CLS_MFMA8_FP32");
-        return !(e && e[0] == '0');
-    }();
     auto fp_for_i8 = [&] {
-        if (!fp32_stage || !build_fast(nc, mu, inv, fp)) fp.T2 = INFINITY;
+        if (!build_fast(nc, mu, inv, fp)) fp.T2 = INFINITY;
     };
     if (path == MPX_CLS_AUTO && auto_mfma8(nc) && build_i8(nc, mu, inv, ip8)) {
         fp_for_i8();
@@ -2058,20 +1920,8 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
     HalfParams hp;
     const int chosen = classify_resolve(nc, mu, inv, path, aligned16(img), fp, fp64, ip8, hp);
     int64_t done = 0;  // pixels handled by a fast path; the rest go DIRECT
-    // MFMA8 below 9 classes: the one-pixel-per-lane 4x4x4 form (MFMA8S);
-    // MPX_CLS_MFMA8_SMALL=0 keeps the 32x32 form there (A/B)
-    static const bool small8 = [] {
-        const char *e = std::getenv("MPX_CLS_MFMA8_SMALL");
-        return !(e && e[0] == '0');
-    }();
-    // the small form up to kMfma8sMaxClasses; MPX_CLS_MFMA8S_MAX=k (8..16)
-    // moves the boundary (A/B; read once)
-    static const int small_max = [] {
-        const char *e = std::getenv("MPX_CLS_MFMA8S_MAX");
-        const int k = e ? std::atoi(e) : 0;
-        return k >= 8 && k <= 16 ? k : kMfma8sMaxClasses;
-    }();
-    if (chosen == MPX_CLS_MFMA8 && nc <= small_max && small8) {
+    // MFMA8 up to kMfma8sMaxClasses: the one-pixel-per-lane 4x4x4 form (MFMA8S)
+    if (chosen == MPX_CLS_MFMA8 && nc <= kMfma8sMaxClasses) {
         const int64_t nvec = npix / 4;
         if (nvec > 0) {
             const int64_t blocks = (nvec + 255) / 256;
@@ -2081,43 +1931,12 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             // store latency on each wave's critical path (gfx950 stores count
             // in vmcnt with the loads). 8192^2, µs, 8 -> 16 blocks per CU:
             // nc = 2 126-129 -> 118, nc = 4 133-135 -> 128-130, nc = 8 same
-            // (profiles/lab3_classify.md). MPX_CLS_MFMA8S_GRID=k overrides
-            // (tuning).
-            static const int gcap = [] {
-                const char *e = std::getenv("MPX_CLS_MFMA8S_GRID");
-                const int k = e ? std::atoi(e) : 0;
-                return k > 0 ? k : 16;
-            }();
+            // (profiles/lab3_classify.md)
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256)
-                                   : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * gcap);
+                                   : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
             const int ns = (nc + 1) / 2;
-            // MPX_CLS_MFMA8S_PF=2: two trips of loads in flight; MPX_CLS_MFMA8S_MEM=1..3:
-            // non-temporal loads (1) / stores (2) / both (3) (A/B; read once)
-            static const int pf = [] {
-                const char *e = std::getenv("MPX_CLS_MFMA8S_PF");
-                return (e && e[0] == '2') ? 2 : 1;
-            }();
-            static const int mem = [] {
-                const char *e = std::getenv("MPX_CLS_MFMA8S_MEM");
-                return (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
-            }();
-#define MPX_MFMA8S_L(NS, PF, MEM) \
-    hipLaunchKernelGGL((classify_mfma8s_kernel<NS, PF, MEM>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb)
-#define MPX_MFMA8S(NS)                    \
-    do {                                  \
-        if (pf == 2)                      \
-            MPX_MFMA8S_L(NS, 2, 0);       \
-        else if (mem == 1)                \
-            MPX_MFMA8S_L(NS, 1, 1);       \
-        else if (mem == 2)                \
-            MPX_MFMA8S_L(NS, 1, 2);       \
-        else if (mem == 3)                \
-            MPX_MFMA8S_L(NS, 1, 3);       \
-        else if (mem == 4)                \
-            MPX_MFMA8S_L(NS, 1, 4);       \
-        else                              \
-            MPX_MFMA8S_L(NS, 1, 0);       \
-    } while (0)
+#define MPX_MFMA8S(NS) \
+    hipLaunchKernelGGL((classify_mfma8s_kernel<NS>), dim3(g), dim3(256), 0, s, img, nvec, nc, cp, ip8, fp, amb)
             if (ns == 1)
                 MPX_MFMA8S(1);
             else if (ns == 2)
@@ -2127,15 +1946,12 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             else if (ns == 4)
                 MPX_MFMA8S(4);
             else if (ns == 5)
-                MPX_MFMA8S_L(5, 1, 0);
+                MPX_MFMA8S(5);
             else if (ns == 6)
-                MPX_MFMA8S_L(6, 1, 0);
-            else if (ns == 7)
-                MPX_MFMA8S_L(7, 1, 0);
+                MPX_MFMA8S(6);
             else
-                MPX_MFMA8S_L(8, 1, 0);
+                MPX_MFMA8S(7);
 #undef MPX_MFMA8S
-#undef MPX_MFMA8S_L
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             done = nvec * 4;
         }
@@ -2146,13 +1962,9 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, 256) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
             // registers ranked in the last 16-class set: an even count (padded classes never win)
             const int last = nc > 16 ? nc - 16 : nc;
-            static const int m16var = [] {  // TEMPORARY A/B (round 6): bit 1 = no device list, bit 2 = looped kernel only
-                const char *e = std::getenv("MPX_CLS_M16_VAR");
-                return e ? std::atoi(e) : 0;
-            }();
-            // whole blocks of kM16Trips x 256 vectors to the one-shot kernel (with the
-            // device deferral list), the rest looped
-            const int64_t want = (m16var & 6) ? 0 : nvec / (256 * kM16Trips);
+            // a caller geometry (the harness's launch sweeps) drives the looped
+            // kernel over the whole image; by default whole blocks go one-shot
+            const int64_t want = grid > 0 ? 0 : nvec / (256 * kM16Trips);
             const DeferList dl = want > 0 ? defer_list(s, true) : DeferList{nullptr, nullptr, 0, 0};
             const int64_t nblk = dl.ent != nullptr ? want : 0;
             const int64_t vdone = nblk * 256 * kM16Trips;
@@ -2163,10 +1975,10 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 #define MPX_MFMA16(NSET, NR)                                                                                          \
     do {                                                                                                              \
         if (nblk > 0)                                                                                                 \
-            hipLaunchKernelGGL((classify_mfma16t_kernel<NSET, NR, 1>), dim3((unsigned)nblk), dim3(256), 0, s, img, nc, cp, \
+            hipLaunchKernelGGL((classify_mfma16t_kernel<NSET, NR>), dim3((unsigned)nblk), dim3(256), 0, s, img, nc, cp, \
                                hp, fp, dl, amb);                                                                      \
         if (rvec > 0)                                                                                                 \
-            hipLaunchKernelGGL((classify_mfma16_kernel<NSET, NR, 1>), dim3(gr), dim3(256), 0, s, rimg, rvec, nc, cp, hp, \
+            hipLaunchKernelGGL((classify_mfma16_kernel<NSET, NR>), dim3(gr), dim3(256), 0, s, rimg, rvec, nc, cp, hp, \
                                fp, none, amb);                                                                        \
     } while (0)
             if (nc <= 16) {
@@ -2192,34 +2004,21 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
 #undef MPX_MFMA16
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             if (nblk > 0) {
-                hipLaunchKernelGGL(classify_fixup_kernel, dim3(kDeferSubs * kFixupParts), dim3(256), 0, s, img, dl, nc, cp, fp,
-                                   amb);
+                hipLaunchKernelGGL(classify_fixup_kernel, dim3(kDeferSubs), dim3(256), 0, s, img, dl, nc, cp, fp, amb);
                 MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
             }
             done = nvec * 4;
         }
     } else if (chosen == MPX_CLS_MFMA8) {
         const int64_t nchunks = npix / 128;
-        // MPX_CLS_MFMA8_WIN=1: windowed fix-ups (every byte written once, 1.03x
-        // the image's bytes against 1.22x, but 434-444 -> 523 us at nc = 32 on
-        // one box: profiles/lab3_classify.md); off by default
-        static const bool win = [] {
-            const char *e = std::getenv("MPX_CLS_MFMA8_WIN");
-            return e && e[0] == '1';
-        }();
         if (nchunks > 0) {
             const int64_t blocks = (nchunks + 3) / 4;
             // 16 blocks per CU (round-5 sweep at 8192^2, 2048 -> 4096 blocks:
             // nc = 12 269.5 -> 261.1 µs, 16 269.7 -> 262.7, 32 391.1 -> 375.2;
             // 8192 and 16384 slower again; profiles/lab3_classify.md)
             const int g = grid > 0 ? grid : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 16);
-#define MPX_MFMA8_LAUNCH(NREG)                                                                                       \
-    do {                                                                                                             \
-        if (win)                                                                                                     \
-            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, true>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, fp, amb); \
-        else                                                                                                         \
-            hipLaunchKernelGGL((classify_mfma8_kernel<NREG, false>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, fp, amb); \
-    } while (0)
+#define MPX_MFMA8_LAUNCH(NREG) \
+    hipLaunchKernelGGL((classify_mfma8_kernel<NREG>), dim3(g), dim3(256), 0, s, img, nchunks, nc, cp, ip8, fp, amb)
             if (nc <= 8)
                 MPX_MFMA8_LAUNCH(4);
             else if (nc <= 16)
@@ -2260,24 +2059,7 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             done = nchunks * 128;
         }
     } else if (chosen == MPX_CLS_FAST) {
-        // 8 pixels per thread and trip (two 16-B vectors): same box, 8192^2,
-        // nc 4 / 16 / 32: 126 / 357-359 / 616-626 us vs 127 / 361-365 / 638-641
-        // with 4 (profiles/lab3_classify.md). MPX_CLS_NQ=1 selects 4 (A/B); read once
-        static const int nq = [] {
-            const char *e = std::getenv("MPX_CLS_NQ");
-            return (e && e[0] == '1') ? 1 : 2;
-        }();
-        // fast32 OPT bits (MPX_CLS_OPT overrides): 8 = interleaved FMA chains,
-        // the default since round 4 (nc = 16 / 32: 307.6 -> 301.8 / 523.8 ->
-        // 519.2 us medians, two alternated rounds; profiles/lab3_classify.md);
-        // the memory-policy / layout bits measured neutral and stay off
-        static const int opt = [] {
-            const char *e = std::getenv("MPX_CLS_OPT");
-            const int o = e ? std::atoi(e) : 8;
-            return o >= 0 && o <= 31 ? o : 8;
-        }();
-        int64_t nvec = npix / (4 * nq);
-        if (opt & 4) nvec &= ~63ll;  // whole waves only; the rest goes DIRECT
+        const int64_t nvec = npix / (4 * kFastNQ);
         if (nvec > 0) {
             // the kernel is compiled for 256-thread workgroups
             // (__launch_bounds__(256)): a larger caller block would not launch
@@ -2288,31 +2070,9 @@ int classify_impl(uint32_t *img, int64_t npix, int nc, const double *mu, const d
             // nc = 12 285.6 -> 247.4 µs, 16 297.9 -> 288.2, 32 524.4 -> 504.9;
             // profiles/lab3_classify.md)
             const int g = grid > 0 ? (int)useful_grid(grid, nvec, blk) : (int)std::min<int64_t>(blocks, (int64_t)kNumCUs * 32);
-            // wave-contiguous vectors need waves that start at multiples of 64 threads
-            const int o = (opt & 4) && blk % 64 != 0 ? opt & 3 : opt;
-            if (nq == 2 && o != 0) {
-                switch (o) {
-#define MPX_FAST32_OPT(k)                                                                                           \
-    case k:                                                                                                         \
-        hipLaunchKernelGGL((classify_fast32_kernel<2, k>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);  \
-        break;
-                    MPX_FAST32_OPT(1) MPX_FAST32_OPT(2) MPX_FAST32_OPT(3) MPX_FAST32_OPT(4) MPX_FAST32_OPT(5)
-                    MPX_FAST32_OPT(6) MPX_FAST32_OPT(7) MPX_FAST32_OPT(8) MPX_FAST32_OPT(10) MPX_FAST32_OPT(12)
-                    MPX_FAST32_OPT(15) MPX_FAST32_OPT(24) MPX_FAST32_OPT(26)
-                    default:
-                        hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
-#undef MPX_FAST32_OPT
-                }
-            } else if (nq == 2)
-                hipLaunchKernelGGL(classify_fast32_kernel<2>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
-            else if ((o & 24) == 24)  // 4 pixels per thread (5 waves per SIMD), two trips in flight
-                hipLaunchKernelGGL((classify_fast32_kernel<1, 24>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
-            else if (o & 8)
-                hipLaunchKernelGGL((classify_fast32_kernel<1, 8>), dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
-            else
-                hipLaunchKernelGGL(classify_fast32_kernel<1>, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
+            hipLaunchKernelGGL(classify_fast32_kernel, dim3(g), dim3(blk), 0, s, img, nvec, nc, cp, fp, amb);
             MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
-            done = nvec * 4 * nq;
+            done = nvec * 4 * kFastNQ;
         }
     }
     if (done < npix) {

@@ -495,38 +495,6 @@ def test_roberts_rgb_gpu_matches_cpu(gpu, hw):
     assert torch.equal(ops.roberts_rgb(img.to(gpu)).cpu(), ops.roberts_rgb(img))
 
 
-@pytest.mark.parametrize("env", [{"MPX_CLS_OPT": str(o)} for o in (0, 1, 2, 3, 4, 5, 6, 7, 10, 12, 15, 24, 26)] + [{"MPX_CLS_MFMA8_WIN": "1"}, {"MPX_CLS_MFMA8_FP32": "0"}])
-def test_classify_env_variants_match_cpu(gpu, env, tmp_path):
-    """The A/B variants read once per process from the environment (fast32
-    memory policy / wave-contiguous layout bits, mfma8 fix-ups after the loop
-    instead of windowed) classify exactly like the CPU reference, including a
-    tail of pixels outside whole waves and an all-ties image."""
-    import subprocess
-    import sys
-    code = (
-        "import torch, sys, numpy as np\n"
-        "from cuda_mpi_openmp_amd import ops\n"
-        "from tests.helpers import rand_img, smooth_img\n"
-        "out = {}\n"
-        "for name, img, nc in (('rand', rand_img(509, 641, seed=11), 24), ('ties', smooth_img(64, 96, seed=4), 2)):\n"
-        "    rng = np.random.default_rng(3)\n"
-        "    h, w = img.shape[:2]\n"
-        "    pts = [np.stack([rng.integers(0, w, 64), rng.integers(0, h, 64)], 1) for _ in range(nc)]\n"
-        "    if name == 'ties': pts = [pts[0], pts[1], pts[0]]\n"
-        "    mu, inv = ops.class_stats(img, pts)\n"
-        "    cpu = img.clone(); ops.classify_(cpu, mu, inv)\n"
-        "    for path in ('fast', 'mfma8'):\n"
-        "        d = img.cuda(); ops.classify_(d, mu, inv, path=path)\n"
-        "        out[name + path] = bool(torch.equal(d.cpu(), cpu))\n"
-        "torch.save(out, sys.argv[1])\n")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = tmp_path / "o.pt"
-    subprocess.run([sys.executable, "-c", code, str(p)], check=True, cwd=root, env=dict(os.environ, PYTHONPATH=root, **env),
-                   timeout=120)
-    res = torch.load(p, weights_only=True)
-    assert all(res.values()), res
-
-
 @pytest.mark.parametrize("fname", ["sobel5", "gauss5", "roberts", "sobel5_dense"])
 def test_conv_resident_hint_same_bytes(gpu, fname):
     """MPX_CONV_RESIDENT (ops.conv(..., resident=True), ConvLauncher.resident)
