@@ -103,8 +103,6 @@ _SIGNATURES = {
     "mpx_sort": (c_int, [c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_workspace_bytes": (c_i64, [c_i64, c_int]),
     "mpx_sort_ws": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
-    "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
-    "mpx_sort_scatter_probe": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_ws_status": (c_int, [c_vp, c_i64, c_int]),
     "mpx_sort_lane_order_ok": (c_int, [c_vp]),
     "mpx_cpu_sort": (None, [c_vp, c_i64, c_int]),
@@ -129,6 +127,9 @@ _TUNE_SIGNATURES = {
     "mpx_conv_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
     "mpx_selftest_fast_sqrt": (c_int, [c_vp, c_int, c_vp]),
     "mpx_strip_copy_probe": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    # lab5 radix variants / scatter probe (native/tune/sort_variants.hip)
+    "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
+    "mpx_sort_scatter_probe": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
 }
 _tune = None
 

@@ -41,7 +41,7 @@ def variant_sort(x, variant):
     dt = DTYPES[x.dtype]
     nb = int(L.mpx_sort_workspace_bytes(x.numel(), dt))
     ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
-    _native.check(L.mpx_sort_variant(x.data_ptr(), x.numel(), dt, ws.data_ptr(), nb, variant, _native.stream_of(x)))
+    _native.check(_native.tune_lib().mpx_sort_variant(x.data_ptr(), x.numel(), dt, ws.data_ptr(), nb, variant, _native.stream_of(x)))
 
 
 def main():

@@ -62,7 +62,7 @@ def main():
         ws = torch.empty(nb, dtype=torch.uint8, device=dev)
         st = _native.stream_of(x)
         for k, what in KNOCKS.items():
-            med, mn = timed(lambda k=k: _native.check(L.mpx_sort_scatter_probe(x.data_ptr(), n, ws.data_ptr(), nb, k, st)))
+            med, mn = timed(lambda k=k: _native.check(_native.tune_lib().mpx_sort_scatter_probe(x.data_ptr(), n, ws.data_ptr(), nb, k, st)))
             print(json.dumps({"part": "knock", "knock": k, "what": what, "n": n,
                               "ms_4_passes": round(med, 4), "ms_min": round(mn, 4)}), flush=True)
     if "variants" in PARTS:
@@ -95,7 +95,7 @@ def main():
             rec = {"part": "variants", "case": name, "n": n}
             for v in VARIANTS:
                 def run(v=v):
-                    _native.check(L.mpx_sort_variant(work.data_ptr(), n, dt, ws.data_ptr(), nb, v,
+                    _native.check(_native.tune_lib().mpx_sort_variant(work.data_ptr(), n, dt, ws.data_ptr(), nb, v,
                                                      _native.stream_of(work)))
                 med, mn = timed(run, reset=lambda: work.copy_(src))
                 rec[f"v{v}_ms"] = round(med, 4)
