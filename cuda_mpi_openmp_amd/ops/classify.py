@@ -54,12 +54,11 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``mfma16`` — f16 MFMA distance GEMM (v_mfma_f32_32x32x16_f16, f16
         hi + lo weight limbs, exact integer features, fp32 keys): one pixel
         per lane with all of its classes in that lane;
-      * ``auto``   — ``mfma8`` below 9 classes, at 15-16 and from 20 (where it
-        measured faster on MI355X, round-5 sweeps at 8192^2, µs: nc = 4 123
-        vs 134, 8 172 vs 188, 15 262 vs 279, 16 260-267 vs 288-297, 32
-        376-381 vs 505-524), else ``fast`` (the f32 MFMA shares the VALU's
-        fp32 datapath on gfx950; at 9-14 the int8 forms' lead over fast32 is
-        within the box-to-box spread or negative, and fast32 wins at 17-19).
+      * ``auto``   — ``mfma16`` from 2 classes, ``mfma8`` at 1 (each where
+        its statistics permit a bound; then ``mfma8``, ``fast``, ``direct``).
+        Round-6 medians at 8192^2, µs, mfma16 vs mfma8: nc = 1 129 vs 111,
+        2-4 within 3 % (inside the ±4 % box-to-box spread), 5 123 vs 142,
+        8 133 vs 172, 16 168 vs 278, 32 277 vs 397.
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes
@@ -76,26 +75,40 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
             if not (ambiguous.is_cuda and ambiguous.dtype == torch.int32 and ambiguous.numel() >= 1):
                 raise ValueError("ambiguous must be a 1-element int32 device tensor")
             amb = ambiguous.data_ptr()
-        _native.check(L.mpx_classify_ex(img.data_ptr(), h * w, nc, mu_c, inv_c, grid, block, PATHS[path], amb,
+        _native.check(L.mpx_classify_ex(img.data_ptr(), h * w, nc, mu_c.ptr, inv_c.ptr, grid, block, PATHS[path], amb,
                                         _native.stream_of(img)))
     else:
-        L.mpx_cpu_classify(img.data_ptr(), h * w, nc, mu_c, inv_c)
+        L.mpx_cpu_classify(img.data_ptr(), h * w, nc, mu_c.ptr, inv_c.ptr)
     return img
 
 
+class _F64:
+    """A contiguous float64 view or copy and a ctypes array over its buffer
+    (which the object keeps alive). ctypes arrays built from Python lists cost
+    ~40 µs per call, a third of an 8192^2 classification; from_buffer ~1 µs."""
+
+    __slots__ = ("arr", "ptr")
+
+    def __init__(self, a: np.ndarray):
+        arr = np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+        if not arr.flags.writeable:
+            arr = arr.copy()
+        self.arr = arr
+        self.ptr = (ctypes.c_double * max(1, arr.size)).from_buffer(arr) if arr.size else (ctypes.c_double * 1)()
+
+
 def _params(mu: np.ndarray, inv: np.ndarray):
-    mu = np.ascontiguousarray(mu, dtype=np.float64).reshape(-1)
-    inv = np.ascontiguousarray(inv, dtype=np.float64).reshape(-1)
-    nc = mu.size // 3
-    if inv.size != 9 * nc or not 1 <= nc <= MAX_CLASSES:
+    m, i = _F64(mu), _F64(inv)
+    nc = m.arr.size // 3
+    if i.arr.size != 9 * nc or not 1 <= nc <= MAX_CLASSES:
         raise ValueError("mu must be (nc, 3) and inv (nc, 3, 3) with 1 <= nc <= 32")
-    return _native.f64_array(mu.tolist()), _native.f64_array(inv.tolist()), nc
+    return m, i, nc
 
 
 def plan(mu: np.ndarray, inv: np.ndarray, path: str = "auto") -> Tuple[str, float]:
     """(path actually run, fp32 decision margin) for these class statistics."""
     mu_c, inv_c, nc = _params(mu, inv)
     margin = ctypes.c_float(0.0)
-    r = _native.lib().mpx_classify_plan(nc, mu_c, inv_c, PATHS[path], ctypes.byref(margin))
+    r = _native.lib().mpx_classify_plan(nc, mu_c.ptr, inv_c.ptr, PATHS[path], ctypes.byref(margin))
     _native.check(r if r < 0 else 0)
     return PATH_NAMES[r], float(margin.value)

@@ -1748,32 +1748,20 @@ int classify_choose(int nc, int path, bool fast_ok) {
     return path;
 }
 
-// AUTO runs MFMA8 (its statistics permitting) where it measured faster than
-// FAST32. Round 5 (the one-pixel-per-lane 4x4x4 form below 9 classes, the
-// int8 bound from the actual weight rounding, host parameter cache), one box,
-// 8192^2, three rotated images, two runs each, median µs
-// (profiles/raw/r5/b2/, profiles/lab3_classify.md):
-//   nc      2        3        4        6        8        12       16       20       24       32
-//   fast  132-139  127-128  134      162-166  188-189  241-245  295-303  352-353  402-410  510-517
-//   mfma8 123-128  126      128-129  149-153  176      277-281  280-283  341-342  340-341  407-413
-// The 4x4x4 form's cost grows with its row sets (two classes each), the
-// 32x32 form's with its ranked accumulator registers (8 for <= 16 classes,
-// 12 for <= 24, 16 for <= 32) and FAST32's linearly. Late round 5, the
-// 4x4x4 form at 5-8 row sets (4 waves per SIMD; 3 at 8 sets) against both,
-// with 16 / 32 blocks per CU, on four boxes (profiles/raw/r5/{small16,
-// auto14,auto15,mid}/), µs:
-//   nc        10        11        12        13        14        15       16
-//   fast    218-226   238-242   235-247   251-252   262-276   279      288-297
-//   4x4x4   229-232   262-263   223-240   246-251   245-290    —       286-287
-//   32x32   291-292   293-297   259-271   260-264   260-264   262      260-264
-// The 4x4x4 form beats the 32x32 form up to 13 classes on every box
-// (kMfma8sMaxClasses: explicit mfma8 runs it there); against FAST32 its lead
-// at 12-14 is within the box-to-box spread and it loses at 11, so AUTO keeps
-// FAST32 at 9-14 and 17-19 and takes MFMA8 below 9 classes, at 15-16 (the
-// 32x32 form ranks the same 8 registers at 15 as at 16) and from 20.
-constexpr int kAutoMfma8MinClasses = 20;
+// AUTO: MFMA16 from 2 classes, MFMA8 at 1 class, each where its statistics
+// permit a bound (else the next one down: MFMA8, FAST32, DIRECT). Round 6,
+// one box, 8192^2, three rounds, median µs, host marshalling included
+// (profiles/raw/r6/g2/, profiles/lab3_classify.md):
+//   nc        1    2    3    4    5    6    8    12   16   32
+//   mfma16   129  117  118  120  123  127  133  157  168  277
+//   mfma8    111  114  117  118  142  147  172  231  278  397
+// At 2-4 classes the two are within 3 %, less than the box-to-box spread
+// (±4 %), so the rule takes the one form there; at 1 class the 4x4x4 int8
+// form's single row set is 16 % cheaper than a 32-row f16 tile, and from 5
+// classes MFMA16 wins by 13-40 %. The earlier per-class-count table
+// (FAST32 at 9-14 / 17-19, MFMA8 elsewhere; round 5) is retired.
+constexpr int kAutoMfma16MinClasses = 2;
 constexpr int kMfma8sMaxClasses = 13;
-inline bool auto_mfma8(int nc) { return nc <= 8 || nc == 15 || nc == 16 || nc >= kAutoMfma8MinClasses; }
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
 // the parameters it needs built; DIRECT when no fp32 / int bound exists.
@@ -1844,9 +1832,15 @@ int classify_resolve_uncached(int nc, const double *mu, const double *inv, int p
     auto fp_for_i8 = [&] {
         if (!build_fast(nc, mu, inv, fp)) fp.T2 = INFINITY;
     };
-    if (path == MPX_CLS_AUTO && auto_mfma8(nc) && build_i8(nc, mu, inv, ip8)) {
-        fp_for_i8();
-        return MPX_CLS_MFMA8;
+    if (path == MPX_CLS_AUTO) {
+        if (nc >= kAutoMfma16MinClasses && build_half(nc, mu, inv, hp)) {
+            fp_for_i8();
+            return MPX_CLS_MFMA16;
+        }
+        if (build_i8(nc, mu, inv, ip8)) {
+            fp_for_i8();
+            return MPX_CLS_MFMA8;
+        }
     }
     const bool ok = path == MPX_CLS_MFMA64   ? build_fast64(nc, mu, inv, fp64)
                     : path == MPX_CLS_MFMA8  ? build_i8(nc, mu, inv, ip8)

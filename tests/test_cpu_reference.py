@@ -140,32 +140,20 @@ def test_classify_plan_routes():
         return ops.class_stats(img, [rng.integers(0, 64, (30, 2)) for _ in range(nc)])
 
     mu, inv = stats(4)
-    # below 9 classes AUTO runs the one-pixel-per-lane int8 MFMA form (round 5)
+    # from 2 classes AUTO runs the f16-MFMA form (round 6), at 1 the 4x4x4
+    # int8 form
     path, margin = ops.classify_plan(mu, inv, "auto")
-    assert path == "mfma8" and margin >= 1
+    assert path == "mfma16" and margin > 0
     assert ops.classify_plan(mu, inv, "fast")[0] == "fast" and 0 < ops.classify_plan(mu, inv, "fast")[1] < 1e-2
     assert ops.classify_plan(mu, inv, "mfma")[0] == "mfma"
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
-    mu20, inv20 = stats(20)
-    assert ops.classify_plan(mu20, inv20, "auto")[0] == "mfma8"
-    mu19, inv19 = stats(19)
-    assert ops.classify_plan(mu19, inv19, "auto")[0] == "fast"
-    # 15 classes: the 32x32 int8 form (late round 5); 9-14 stay on the
-    # packed-VALU path
-    mu15, inv15 = stats(15)
-    assert ops.classify_plan(mu15, inv15, "auto")[0] == "mfma8"
-    for k in (9, 11, 12, 14):
+    assert ops.classify_plan(mu, inv, "mfma8")[0] == "mfma8"
+    mu1, inv1 = stats(1)
+    assert ops.classify_plan(mu1, inv1, "auto")[0] == "mfma8"
+    for k in (2, 3, 9, 15, 16, 19, 20, 28, 32):
         muk, invk = stats(k)
-        assert ops.classify_plan(muk, invk, "auto")[0] == "fast", k
-    # at exactly 16 and from 20 classes AUTO runs the exact int8-MFMA distance
-    # GEMM (measured faster there; margin in key units)
-    mu16, inv16 = stats(16)
-    assert ops.classify_plan(mu16, inv16, "auto")[0] == "mfma8"
-    mu21, inv21 = stats(21)
-    assert ops.classify_plan(mu21, inv21, "auto")[0] == "mfma8"
-    mu28, inv28 = stats(28)
-    path28, margin28 = ops.classify_plan(mu28, inv28, "auto")
-    assert path28 == "mfma8" and margin28 >= 1
+        assert ops.classify_plan(muk, invk, "auto")[0] == "mfma16", k
+    mu20, inv20 = stats(20)
     assert ops.classify_plan(mu20, inv20, "mfma")[0] == "mfma"
     # fp64 GEMM: same validation, a bound ~2^29 x tighter than the fp32 one
     path64, margin64 = ops.classify_plan(mu20, inv20, "mfma64")
