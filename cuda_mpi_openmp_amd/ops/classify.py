@@ -54,11 +54,11 @@ def classify_(img: torch.Tensor, mu: np.ndarray, inv: np.ndarray, path: str = "a
       * ``mfma16`` — f16 MFMA distance GEMM (v_mfma_f32_32x32x16_f16, f16
         hi + lo weight limbs, exact integer features, fp32 keys): one pixel
         per lane with all of its classes in that lane;
-      * ``auto``   — ``mfma16`` from 2 classes, ``mfma8`` at 1 (each where
-        its statistics permit a bound; then ``mfma8``, ``fast``, ``direct``).
-        Round-6 medians at 8192^2, µs, mfma16 vs mfma8: nc = 1 129 vs 111,
-        2-4 within 3 % (inside the ±4 % box-to-box spread), 5 123 vs 142,
-        8 133 vs 172, 16 168 vs 278, 32 277 vs 397.
+      * ``auto``   — ``mfma16`` from 4 classes, ``fast`` below (each where
+        its statistics permit a bound; else ``fast``, then ``direct``).
+        Round-6 medians at 8192^2, µs, fast / mfma16: nc = 1 97 / 118,
+        3 117 / 122, 4 127 / 121, 8 187 / 141, 16 297 / 174, 32 531 / 286
+        (``mfma8`` never led by more than the box spread).
     The fp32/fp64-GEMM paths classify a pixel only when its best/second margin exceeds a
     rigorous bound on the fp32-vs-reference error and recompute every other
     pixel with the fp64 chain, so every path returns identical classes

@@ -1748,19 +1748,20 @@ int classify_choose(int nc, int path, bool fast_ok) {
     return path;
 }
 
-// AUTO: MFMA16 from 2 classes, MFMA8 at 1 class, each where its statistics
-// permit a bound (else the next one down: MFMA8, FAST32, DIRECT). Round 6,
-// one box, 8192^2, three rounds, median µs, host marshalling included
-// (profiles/raw/r6/g2/, profiles/lab3_classify.md):
-//   nc        1    2    3    4    5    6    8    12   16   32
-//   mfma16   129  117  118  120  123  127  133  157  168  277
-//   mfma8    111  114  117  118  142  147  172  231  278  397
-// At 2-4 classes the two are within 3 %, less than the box-to-box spread
-// (±4 %), so the rule takes the one form there; at 1 class the 4x4x4 int8
-// form's single row set is 16 % cheaper than a 32-row f16 tile, and from 5
-// classes MFMA16 wins by 13-40 %. The earlier per-class-count table
-// (FAST32 at 9-14 / 17-19, MFMA8 elsewhere; round 5) is retired.
-constexpr int kAutoMfma16MinClasses = 2;
+// AUTO: MFMA16 from 4 classes, FAST32 below, each where its statistics
+// permit a bound (else FAST32, then DIRECT). Round 6, 8192^2, three rotated
+// images, host marshalling included, median µs of three alternated rounds on
+// one box (profiles/raw/r6/lab3/, profiles/lab3_classify.md):
+//   nc        1    2    3    4    5    8    12   16   24   32
+//   mfma16   118  113  122  121  125  141  158  174  251  286
+//   mfma8    110  112  116  120  146  176  232  277  322  392
+//   fast      97  106  117  127  146  187  237  297  415  531
+// A second box (profiles/raw/r6/inwave/) ordered fast32 / mfma16 the same
+// way at 1-4 classes (99 / 131, 104 / 117, 116 / 121, 125 / 120). Below 4
+// classes FAST32 needs no fix-up launch and no MFMA; from 4 MFMA16 wins, by
+// 14-46 % from 5. MFMA8 never wins by more than the spread of its
+// neighbours, so AUTO does not take it (explicit "mfma8" still runs it).
+constexpr int kAutoMfma16MinClasses = 4;
 constexpr int kMfma8sMaxClasses = 13;
 
 // The path AUTO (or an explicit path) resolves to for these statistics, with
@@ -1832,15 +1833,9 @@ int classify_resolve_uncached(int nc, const double *mu, const double *inv, int p
     auto fp_for_i8 = [&] {
         if (!build_fast(nc, mu, inv, fp)) fp.T2 = INFINITY;
     };
-    if (path == MPX_CLS_AUTO) {
-        if (nc >= kAutoMfma16MinClasses && build_half(nc, mu, inv, hp)) {
-            fp_for_i8();
-            return MPX_CLS_MFMA16;
-        }
-        if (build_i8(nc, mu, inv, ip8)) {
-            fp_for_i8();
-            return MPX_CLS_MFMA8;
-        }
+    if (path == MPX_CLS_AUTO && nc >= kAutoMfma16MinClasses && build_half(nc, mu, inv, hp)) {
+        fp_for_i8();
+        return MPX_CLS_MFMA16;
     }
     const bool ok = path == MPX_CLS_MFMA64   ? build_fast64(nc, mu, inv, fp64)
                     : path == MPX_CLS_MFMA8  ? build_i8(nc, mu, inv, ip8)

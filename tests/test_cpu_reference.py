@@ -140,17 +140,17 @@ def test_classify_plan_routes():
         return ops.class_stats(img, [rng.integers(0, 64, (30, 2)) for _ in range(nc)])
 
     mu, inv = stats(4)
-    # from 2 classes AUTO runs the f16-MFMA form (round 6), at 1 the 4x4x4
-    # int8 form
+    # from 4 classes AUTO runs the f16-MFMA form (round 6), below it fast32
     path, margin = ops.classify_plan(mu, inv, "auto")
     assert path == "mfma16" and margin > 0
     assert ops.classify_plan(mu, inv, "fast")[0] == "fast" and 0 < ops.classify_plan(mu, inv, "fast")[1] < 1e-2
     assert ops.classify_plan(mu, inv, "mfma")[0] == "mfma"
     assert ops.classify_plan(mu, inv, "direct") == ("direct", 0.0)
     assert ops.classify_plan(mu, inv, "mfma8")[0] == "mfma8"
-    mu1, inv1 = stats(1)
-    assert ops.classify_plan(mu1, inv1, "auto")[0] == "mfma8"
-    for k in (2, 3, 9, 15, 16, 19, 20, 28, 32):
+    for k in (1, 2, 3):
+        muk, invk = stats(k)
+        assert ops.classify_plan(muk, invk, "auto")[0] == "fast", k
+    for k in (5, 9, 15, 16, 19, 20, 28, 32):
         muk, invk = stats(k)
         assert ops.classify_plan(muk, invk, "auto")[0] == "mfma16", k
     mu20, inv20 = stats(20)

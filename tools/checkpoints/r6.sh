@@ -1,0 +1,50 @@
+# Round-6 GPU checkpoints: bash tools/gpu.sh checkpoint r6_<x>
+# (each a chain of time-bounded gpu.sh steps; outputs under gpurun_out/r6/<x>).
+
+# lab3 final: classifier GPU tests after the AUTO rule change (mfma16 from 2
+# classes), three alternated 8192^2 sweeps of auto / mfma16 / mfma8 / fast,
+# the kernel trace and two counter passes (VALU per pair, MFMA busy).
+ckpt_r6_lab3() {
+    export O=${O:-gpurun_out/r6/lab3}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    for r in 1 2 3; do
+        LAB3_NCS=1,2,3,4,5,8,12,16,24,32 LAB3_PATHS=auto,mfma16,mfma8,fast LAB3_TAG=r$r \
+            bash tools/gpu.sh run lab3_$r 300 python -u tools/experiments/lab3_m16.py || return 1
+    done &&
+    LAB3_PROF=1 LAB3_NCS=4,16,32 LAB3_PATHS=auto,mfma8,fast \
+        bash tools/gpu.sh prof lab3_trace -- python tools/experiments/lab3_m16.py &&
+    local i=0 grp
+    for grp in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" \
+               "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
+               "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
+        i=$((i + 1))
+        LAB3_PROF=1 LAB3_NCS=4,16,32 LAB3_PATHS=auto,mfma8,fast \
+            bash tools/gpu.sh pmc lab3_pmc$i "$grp" -- python tools/experiments/lab3_m16.py || return 1
+    done
+}
+
+# lab3 in-wave exact fallback of the one-shot mfma16 kernel (no fix-up launch)
+# against the device deferral list: A = libmpx (list), B = $LIB (in-wave up to
+# 16 classes); classifier GPU tests on B first.
+ckpt_r6_inwave() {
+    export O=${O:-gpurun_out/r6/inwave}
+    mkdir -p "$O"
+    local lib=${LIB:-abtmp/libmpx.so}
+    MPX_LIB_PATH=$lib bash tools/gpu.sh tests tests/test_gpu_kernels.py -k "classify" &&
+    LAB3_NCS=1,2,3,4,5,6,8,12,16 LAB3_PATHS=mfma16,fast \
+        bash tools/gpu.sh ab lab3 "$lib" 3 -- python -u tools/experiments/lab3_m16.py
+}
+
+# lab3 one-shot mfma16 kernel occupancy (amdgpu_waves_per_eu for the 1-set
+# instantiations up to 16 classes): A = libmpx, B = abtmp/w5 (5 waves per
+# SIMD, no scratch) and abtmp/w6 (6, a few spill slots in the rare paths).
+ckpt_r6_wpe() {
+    export O=${O:-gpurun_out/r6/wpe}
+    mkdir -p "$O"
+    MPX_LIB_PATH=abtmp/w5/libmpx.so bash tools/gpu.sh tests tests/test_gpu_kernels.py -k "classify_mfma16" &&
+    LAB3_NCS=2,3,4,5,8,12,16 LAB3_PATHS=mfma16 \
+        bash tools/gpu.sh ab w5 abtmp/w5/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py &&
+    LAB3_NCS=2,3,4,5,8,12,16 LAB3_PATHS=mfma16 \
+        bash tools/gpu.sh ab w6 abtmp/w6/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
+}

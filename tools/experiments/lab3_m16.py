@@ -64,9 +64,9 @@ def main():
                     ops.classify_(imgs[cyc[0] % 3], mu, inv, path=path, grid=g)
                     cyc[0] += 1
                 med, mn = time_us(run)
-                print(json.dumps({"tag": tag, "nc": nc, "path": path, "grid": g, "us": round(med, 1),
+                print(json.dumps({"tag": tag, "nc": nc, "path": path, "ran": ops.classify_plan(mu, inv, path)[0], "grid": g, "us": round(med, 1),
                                   "us_min": round(mn, 1), "same_as_direct": ok,
-                                  "undecided": int(amb.item()), "var": os.environ.get("MPX_CLS_M16_VAR", "0")}),
+                                  "undecided": int(amb.item())}),
                       flush=True)
 
 
