@@ -7,7 +7,7 @@
 The lab is the grandparent directory name of the GPU binary (reference
 run_test.py:58-60). Unknown ``--key value`` options go to the lab processor.
 New flags: ``--binary_path_hip`` (alias), ``--timeout`` per run, ``--timing``
-(cold | warm | median:N — exported as MPX_TIMING to the GPU binary), and the
+(cold | cold-lazy | warm | median:N — exported as MPX_TIMING to the GPU binary), and the
 default ``--metadata_columns2plot`` is ``[]`` (the reference default raised a
 KeyError in the plot); ``--compat`` restores the
 reference's output-changing behaviour for a literal replay
@@ -40,7 +40,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--metadata_columns2plot", type=str, default="[]",
                    help='JSON list of CSV columns listed in the plot legend, e.g. ["filename"]')
     p.add_argument("--timeout", type=float, default=None, help="Per-run timeout in seconds.")
-    p.add_argument("--timing", type=str, default=None, help="GPU timing policy: cold | warm | median:N")
+    p.add_argument("--timing", type=str, default=None, help="GPU timing policy: cold | cold-lazy | warm | median:N")
     p.add_argument("--warmup", type=int, default=None,
                    help="untimed launches before the timed one(s) in the GPU binary (MPX_WARMUP)")
     p.add_argument("--compat", action="store_true",

@@ -148,9 +148,14 @@ def test_gpu_info():
 @pytest.mark.gpu
 def test_lab2_gpu_timing_policies(tmp_path):
     src = os.path.join(LAB2_DATA, "96.data")
-    for pol in ("cold", "warm", "median:5"):
+    ms = {}
+    for pol in ("cold", "cold-lazy", "warm", "median:5"):
         r = run("labs/lab2/src/to_plot_hip_exe", f"32\n32\n16\n16\n{src}\n{tmp_path}/o.data", env={"MPX_TIMING": pol})
         assert r.returncode == 0 and r.stdout.startswith("HIP execution time: <")
+        assert "unknown MPX_TIMING" not in r.stderr
+        ms[pol] = float(r.stdout.split("<")[1].split()[0])
+    # cold-lazy also times the code object's lazy load (~0.25 ms per module)
+    assert ms["cold-lazy"] > ms["cold"]
 
 
 @pytest.mark.gpu

@@ -48,3 +48,29 @@ ckpt_r6_wpe() {
     LAB3_NCS=2,3,4,5,8,12,16 LAB3_PATHS=mfma16 \
         bash tools/gpu.sh ab w6 abtmp/w6/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
 }
+
+# Multi-GPU rehearsal on one GPU (VERDICT r5 Next #2 / #7): the conv jobs of
+# tools/scale.py at 1/2/4 ranks sharing the GPU (gloo control plane, peer
+# halos), weak and strong; the driver bench with rank 1's peer mapping failing
+# (every rank must take the fallback, verified, rc 0) and with rank 1's
+# streaming phase timing out (value_streaming null, status records it, rc 0).
+ckpt_r6_multi() {
+    export O=${O:-gpurun_out/r6/multi}
+    mkdir -p "$O"
+    bash tools/gpu.sh run scale 900 python -u tools/scale.py --gpus 1,2,4 --rehearse --only conv --quick \
+        --out "$O/scale" &&
+    MPX_DIST_BACKEND=gloo MPX_PEER_INJECT=map_fail@1 bash tools/gpu.sh run inject_map 300 \
+        python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline &&
+    MPX_DIST_BACKEND=gloo MPX_BENCH_INJECT_STREAM_TIMEOUT=1 bash tools/gpu.sh run inject_stream 300 \
+        python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline
+}
+
+# The reference-methodology harness rows VERDICT r5 Next #5 asks for: the
+# literal [[16,16],[1024,1024]] grid in every lab2 bucket, and cold runs that
+# include HIP's lazy code-object load (no preload).
+ckpt_r6_hcmp() {
+    export O=${O:-gpurun_out/r6/hcmp}
+    mkdir -p "$O"
+    timeout -k 10 1000 bash tools/harness_compare.sh literal lazy > "$O/hcmp.log" 2>&1 || { tail -20 "$O/hcmp.log"; return 1; }
+    tail -30 "$O/hcmp.log"
+}
