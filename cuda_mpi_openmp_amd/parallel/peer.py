@@ -40,7 +40,8 @@ Set-up is collective and TIME-BOUNDED everywhere:
 Fault injection (tests): ``MPX_PEER_INJECT=open_stall@R`` (rank R's IPC open
 never returns), ``verify_corrupt@R`` (R reports a wrong checksum),
 ``probe_corrupt@R`` (R writes a wrong probe pattern), ``map_fail@R`` (R's
-mapping of its neighbours' mailboxes fails: every rank must agree on RCCL).
+mapping of its neighbours' mailboxes fails — in every set-up: conv, streaming
+conv and Jacobi —, so every rank must agree on RCCL).
 
 Limitation of the open deadline: ``open_stall`` sleeps on the
 helper thread BEFORE it calls into HIP, so the tests show the vote and the
@@ -523,13 +524,14 @@ def try_peer_halo(ctx: DistContext, slab: Slab, own: torch.Tensor) -> Optional[P
     every = _allgather(ctx, mine, "conv: handles")
     ph = None
     if mine is not None:
-        try:
-            if _injected("map_fail", ctx.rank):  # fault hook: this rank cannot map its neighbours
-                raise RuntimeError("injected mapping failure (MPX_PEER_INJECT map_fail)")
-            ph = PeerHalo(ctx, slab, own, mb, every)
-        except Exception as e:  # noqa: BLE001
-            err = f"{type(e).__name__}: {e}"
-            mb = None  # freed by the failed PeerHalo
+        if _injected("map_fail", ctx.rank):  # fault hook: this rank cannot map its neighbours
+            err = "RuntimeError: injected mapping failure (MPX_PEER_INJECT map_fail)"
+        else:
+            try:
+                ph = PeerHalo(ctx, slab, own, mb, every)
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+                mb = None  # freed by the failed PeerHalo
     if not _agree(ctx, ph is not None, "conv: map vote"):
         if ph is not None:
             ph.close(collective=False)  # nobody launched a kernel on the mailboxes
@@ -667,6 +669,8 @@ def try_jacobi_peer(ctx: DistContext, slab: Slab, bufs: List[torch.Tensor], layo
     link = None
     if mine is not None:
         try:
+            if _injected("map_fail", ctx.rank):
+                raise RuntimeError("injected mapping failure (MPX_PEER_INJECT map_fail)")
             link = JacobiPeerLink(ctx, slab, bufs, mb, every)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
@@ -899,6 +903,8 @@ def try_stream_halo(ctx: DistContext, slab: Slab, bufs: List[torch.Tensor], filt
     link = None
     if mine is not None:
         try:
+            if _injected("map_fail", ctx.rank):
+                raise RuntimeError("injected mapping failure (MPX_PEER_INJECT map_fail)")
             link = StreamHaloLink(ctx, slab, bufs, mb, every, filt, fused)
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"

@@ -246,6 +246,126 @@ class ClockSampler:
         return (len(self.samples) - 1) / ((self.samples[-1][0] - self.samples[0][0]) / 1e9)
 
 
+class ProcessClockSampler(ClockSampler):
+    """The same sampler in a child process (this file run as a script), so its
+    reads never take the benchmark's GIL: a 100 Hz thread in the benchmark
+    process cost the steady windows 2-3 % of their rate and made the first one
+    up to 25 % slow (round 6, profiles/lab2_conv.md). The child appends one
+    line per sample to a temporary file; ``stop()`` ends it (its exact PID)
+    and reads the file back. The child reads the SMU through amdsmi / sysfs
+    only; it never initialises the GPU's compute stack."""
+
+    def __init__(self, hz: float = 200.0, bdf: Optional[str] = None, ready_s: float = 30.0):
+        self.period = 1.0 / max(1.0, hz)
+        self.samples = []
+        self.read_us = []
+        self.source = None
+        self.error = None
+        self._src = None
+        self._t = None
+        self._stop = threading.Event()
+        self._hz, self._bdf, self._ready_s = hz, bdf, ready_s
+        self._proc = None
+        self._path = None
+
+    def start(self) -> "ProcessClockSampler":
+        import json
+        import subprocess
+        import sys
+        import tempfile
+
+        if self._proc is not None:
+            return self
+        fd, self._path = tempfile.mkstemp(prefix="mpx-clocks-", suffix=".txt")
+        os.close(fd)
+        cmd = [sys.executable, os.path.abspath(__file__), "--hz", str(self._hz), "--out", self._path]
+        if self._bdf:
+            cmd += ["--bdf", self._bdf]
+        self._proc = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL,
+                                      stderr=subprocess.DEVNULL)
+        t_end = time.monotonic() + self._ready_s
+        while time.monotonic() < t_end:  # the header line: source, or why there is none
+            with open(self._path) as f:
+                head = f.readline()
+            if head.endswith("\n"):
+                h = json.loads(head)
+                self.source, self.error = h.get("source"), h.get("error")
+                break
+            if self._proc.poll() is not None:
+                self.error = f"sampler process exited rc={self._proc.returncode} before its header"
+                break
+            time.sleep(0.01)
+        else:
+            self.error = f"sampler process not ready within {self._ready_s} s"
+        return self
+
+    def stop(self) -> None:
+        import json
+
+        p, self._proc = self._proc, None
+        if p is None:
+            return
+        if p.poll() is None:
+            p.terminate()
+            try:
+                p.wait(timeout=5)
+            except Exception:  # noqa: BLE001
+                p.kill()
+                p.wait(timeout=5)
+        try:
+            with open(self._path) as f:
+                lines = f.read().splitlines()
+        finally:
+            os.unlink(self._path)
+        for ln in lines[1:]:
+            try:
+                t, us, m = ln.split("\t", 2)
+                self.samples.append((int(t), json.loads(m)))
+                self.read_us.append(float(us))
+            except ValueError:
+                pass  # a line cut by the termination
+
+
+def _child_main(argv=None) -> int:
+    """``clocks.py --hz H --out FILE [--bdf B]``: ProcessClockSampler's child."""
+    import argparse
+    import json
+    import signal
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hz", type=float, default=100.0)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--bdf", default=None)
+    a = ap.parse_args(argv)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    cs = ClockSampler(hz=a.hz, bdf=a.bdf)
+    with open(a.out, "a") as f:
+        f.write(json.dumps({"source": cs.source, "error": cs.error}) + "\n")
+        f.flush()
+        if cs._src is None:
+            return 0
+        period = 1.0 / max(1.0, a.hz)
+        nxt = time.monotonic()
+        while not stop.is_set():
+            t0 = _clock_ns()
+            try:
+                m = cs._src.read()
+            except Exception:  # noqa: BLE001
+                break
+            t1 = _clock_ns()
+            f.write(f"{(t0 + t1) // 2}\t{(t1 - t0) / 1e3:.1f}\t{json.dumps(m)}\n")
+            f.flush()
+            nxt += period
+            d = nxt - time.monotonic()
+            if d > 0:
+                stop.wait(d)
+            else:
+                nxt = time.monotonic()
+    cs._src.close()
+    return 0
+
+
 def key_fields(summary: dict) -> dict:
     """The handful of fields that attribute a rate change, as flat medians."""
     pick = {}
@@ -267,3 +387,7 @@ def timed_with_clocks(fn: Callable[[], None], sampler: Optional[ClockSampler]) -
     t0 = _clock_ns()
     fn()
     return t0, _clock_ns()
+
+
+if __name__ == "__main__":
+    raise SystemExit(_child_main())

@@ -74,3 +74,22 @@ ckpt_r6_hcmp() {
     timeout -k 10 1000 bash tools/harness_compare.sh literal lazy > "$O/hcmp.log" 2>&1 || { tail -20 "$O/hcmp.log"; return 1; }
     tail -30 "$O/hcmp.log"
 }
+
+# The driver's bench command twice after the steady-window changes (one
+# untimed window after each settle loop, clock sampler in a child process).
+ckpt_r6_bench() {
+    export O=${O:-gpurun_out/r6/bench}
+    mkdir -p "$O"
+    for r in 1 2; do
+        bash tools/gpu.sh run bench$r 300 python bench.py --gpus 1 --steps 20 --warmup 5 || return 1
+    done
+}
+
+# Strong-scaling per-rank floor: one rank's slab of a 4096^2 frame at
+# 4096..512 rows, with and without its resident halo rows, and the whole
+# frame cut into 1..8 launches (tools/experiments/strong_floor.py).
+ckpt_r6_floor() {
+    export O=${O:-gpurun_out/r6/floor}
+    mkdir -p "$O"
+    bash tools/gpu.sh run floor 300 python -u tools/experiments/strong_floor.py
+}
