@@ -73,16 +73,18 @@ class DeviceBuffer {
 //               a CUDA context; the kernel's own first dispatch is timed;
 //   warm      : one untimed warm-up launch, then time one launch (default);
 //   median:N  : warm-up, then the median of N timed launches;
-//   cold-lazy : cold without init_stream_queue: the timed span also holds
-//               HIP's lazy load of the kernel's code object and the queue's
-//               first dispatch (CUDA 12's lazy module loading, the closest
-//               match to how the reference's published cold numbers were taken).
+//   cold-lazy : cold without the code-object preload: the timed span also
+//               holds HIP's lazy load of the kernel's module (CUDA 12's lazy
+//               module loading, the closest match to how the reference's
+//               published cold numbers were taken); the stream's first
+//               dispatch still happens before the timer (CUDA creates its
+//               queues with the context).
 // MPX_WARMUP=W overrides the number of untimed launches (harness --warmup W).
 struct TimingPolicy {
     bool warmup = true;
     int warmups = 1;
     int reps = 1;
-    bool preload = true;  // init_stream_queue before timing
+    bool preload = true;  // mpx_preload_modules before timing
     static TimingPolicy from_env() {
         TimingPolicy p;
         const char *s = std::getenv("MPX_TIMING");
@@ -107,14 +109,14 @@ struct TimingPolicy {
 // Runtime set-up that CUDA performs at context creation but HIP defers to the
 // first launch: loading each code object (~0.25 ms per module, measured with
 // AMD_LOG_LEVEL=4, profiles/harness_vs_published.md) and the first dispatch on
-// the stream. Done before the timer starts under every policy but
-// 'cold-lazy' ('cold' included): the measured kernel itself still runs for
-// the first time.
+// the stream. Both happen before the timer starts under every policy, 'cold'
+// included ('cold-lazy' skips the preload): the measured kernel itself still
+// runs for the first time.
 // (HIP_ENABLE_DEFERRED_LOADING=0 would do the same, but HIP reads it before
 // main(), so it only works when set by the caller's environment.)
 __global__ void mpx_runtime_noop_kernel() {}
-inline void init_stream_queue(hipStream_t stream) {
-    MPX_CHECK(mpx_preload_modules());
+inline void init_stream_queue(hipStream_t stream, bool preload = true) {
+    if (preload) MPX_CHECK(mpx_preload_modules());
     hipLaunchKernelGGL(mpx_runtime_noop_kernel, dim3(1), dim3(64), 0, stream);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -130,7 +132,7 @@ struct NoRestore {
 template <typename F, typename R = NoRestore>
 float time_kernel(F &&launch, hipStream_t stream = nullptr, R &&restore = R{}) {
     const TimingPolicy pol = TimingPolicy::from_env();
-    if (pol.preload) init_stream_queue(stream);
+    init_stream_queue(stream, pol.preload);
     hipEvent_t a, b;
     HIP_CHECK(hipEventCreate(&a));
     HIP_CHECK(hipEventCreate(&b));
@@ -233,7 +235,7 @@ class Parts {
             // filled the inputs may return before its last DMA chunk lands, and
             // nothing orders it before this stream's kernels — drain the device
             HIP_CHECK(hipDeviceSynchronize());
-            if (pol.preload) init_stream_queue(p_[i].stream);
+            init_stream_queue(p_[i].stream, pol.preload);
         }
         for (int w = 0; w < pol.warmups; ++w) {
             for (int i = 0; i < size(); ++i) {

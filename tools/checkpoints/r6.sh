@@ -93,3 +93,10 @@ ckpt_r6_floor() {
     mkdir -p "$O"
     bash tools/gpu.sh run floor 300 python -u tools/experiments/strong_floor.py
 }
+
+# The new GPU tests (fallback records, cold-lazy policy) then the harness rows.
+ckpt_r6_newtests() {
+    export O=${O:-gpurun_out/r6/newtests}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_bench_launch.py tests/test_cli_programs.py -k "bench or timing"
+}

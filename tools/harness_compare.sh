@@ -8,8 +8,8 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 # usage: harness_compare.sh [lab2] [lab2xl] [lab1] [literal] [lazy]
 #   (default: lab2 lab2xl lab1)
 #   literal: lab2 [[16,16],[1024,1024]] with MPX_GEOM_LITERAL=1 (every
-#   workgroup of the published grid launched, empty ones included), cold and
-#   warm, every bucket
+#   workgroup of the published grid launched, empty ones included), cold,
+#   warm and cold-lazy, every bucket
 #   lazy: --timing cold-lazy (no code-object preload, no first dispatch before
 #   the timer: HIP's lazy module load lands in the timed span), every lab2
 #   bucket and lab1 n = 10^6
@@ -43,7 +43,7 @@ for bucket in $([[ " $WHICH " == *" lab2xl "* ]] && echo xl4096); do
   done
 done
 for bucket in $([[ " $WHICH " == *" literal "* ]] && echo small medium large); do
-  for timing in cold warm; do
+  for timing in cold warm cold-lazy; do
     W=$O/lab2_${bucket}_${timing}_literal/lab2; mkdir -p $W/src
     cp labs/lab2/src/to_plot_hip_exe labs/lab2/src/cpu_exe $W/src/
     MPX_GEOM_LITERAL=1 timeout -k 10 600 python run_test.py --binary_path_cuda $W/src/to_plot_hip_exe \

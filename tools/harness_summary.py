@@ -52,7 +52,9 @@ root = args[0] if args else "gpurun_out/harness_cmp"
 rows = []
 for d in sorted(glob.glob(os.path.join(root, "*", "lab*"))):
     tag = os.path.basename(os.path.dirname(d))
-    lab, size, timing = tag.split("_")
+    lab, size, timing, *variant = tag.split("_")  # <lab>_<bucket|n>_<timing>[_literal]
+    if variant:
+        timing = f"{timing}-{'-'.join(variant)}"
     for f in glob.glob(os.path.join(d, "src", "stats_*.csv")):
         df = pd.read_csv(f)
         dev = "CPU (-O0, 1 thread)" if os.path.basename(f).startswith("stats_cpu_") else "MI355X"
@@ -86,6 +88,23 @@ if "--speedups" in sys.argv:
         sp = " / ".join(f"**{x[0] / x[1]:.1f}x**" for x in cells if x)
         pub = PUBLISHED_SPEEDUP.get((lab, size))
         print(f"| {lab} | {size} | {cpu_ms} | {gpu_ms} | {sp} | {str(pub) + 'x' if pub else '—'} |")
+    sys.exit(0)
+if "--like-for-like" in sys.argv:
+    # lab2's published [[16,16],[1024,1024]] row under every methodology knob:
+    # trimmed vs literal grid (MPX_GEOM_LITERAL=1), preloaded vs lazy code objects
+    geo = "[[16, 16], [1024, 1024]]"
+    cols = [("cold", "cold, trimmed grid, preloaded"), ("cold-literal", "cold, literal grid, preloaded"),
+            ("cold-lazy", "cold, trimmed grid, lazy load"), ("cold-lazy-literal", "cold, literal grid, lazy load"),
+            ("warm", "warm, trimmed"), ("warm-literal", "warm, literal")]
+    print("| bucket | reference RTX A6000 (cold) | " + " | ".join(c[1] for c in cols) + " |")
+    print("|---|---|" + "---|" * len(cols))
+    for size in ("small", "medium", "large"):
+        g = out[(out.lab == "lab2") & (out["size"] == size) & (out.geometry == geo) & (out.device == "MI355X")]
+        cells = []
+        for t, _ in cols:
+            v = g[g.timing == t].median_ms
+            cells.append(f"{float(v.iloc[0]):.5f}" if len(v) else "—")
+        print(f"| {size} | {BASELINE[('lab2', size)][geo]} | " + " | ".join(cells) + " |")
     sys.exit(0)
 if "--vs-baseline" in sys.argv:
     out["geometry"] = [("CPU" if d.startswith("CPU") else g) for d, g in zip(out.device, out.geometry)]
