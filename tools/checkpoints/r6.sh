@@ -100,3 +100,20 @@ ckpt_r6_newtests() {
     mkdir -p "$O"
     bash tools/gpu.sh tests tests/test_gpu_bench_launch.py tests/test_cli_programs.py -k "bench or timing"
 }
+
+# Final-tree kernel profile (kernels_r6.md): smoke, the driver's bench, the lab3
+# AUTO sweep, then one trace + the counter groups over every production kernel
+# at the BASELINE sizes (tools/prof_all.py), summarised on the box.
+ckpt_r6_final() {
+    export O=${O:-gpurun_out/r6/final}
+    mkdir -p "$O"
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    LAB3_NCS=1,2,3,4,5,8,12,16,24,32 LAB3_PATHS=auto LAB3_TAG=auto \
+        bash tools/gpu.sh run lab3_auto 400 python -u tools/experiments/lab3_m16.py &&
+    bash tools/gpu.sh profile kfinal -- python3 tools/prof_all.py &&
+    python tools/experiments/kprof_table.py "$O" > "$O/kernels_table.md" &&
+    python tools/pmc_median.py "$O"/kfinal.pmc* > "$O/medians.md" &&
+    python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
+    du -sh "$O" && find "$O" -name "*.db" -delete && du -sh "$O"
+}

@@ -45,7 +45,8 @@ def main():
         del a, b, c
     if "lab3" in which:
         img = torch.randint(0, 256, (8192, 8192, 4), dtype=torch.uint8, device=dev)
-        for nc, paths in ((4, ("fast", "mfma8")), (16, ("direct", "fast", "mfma8")), (32, ("fast", "mfma8"))):
+        for nc, paths in ((4, ("fast", "mfma8", "mfma16")), (16, ("direct", "fast", "mfma8", "mfma16")),
+                          (32, ("fast", "mfma8", "mfma16"))):
             mu, inv = ops.class_stats(img.cpu(), class_points_for(8192, 8192, nc, 64, seed=nc))
             for path in paths:
                 for _ in range(REPS):
