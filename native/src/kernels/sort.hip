@@ -299,26 +299,34 @@ __global__ __launch_bounds__(256) void fill_u8_kernel(uint8_t *__restrict__ x, i
 // scatters (variants 9-21, AUTO above 2^18 keys) are stable only because one
 // ds_add_rtn_u32 applies its same-address lanes in ascending lane order —
 // observed on gfx950, not promised by the ISA. This probe checks it once per
-// device before the first such sort: four waves, three address patterns
-// (every lane on one counter; lane % 3; a scattered 5-way split), each lane's
-// returned count must equal the number of lower lanes on its counter. On a
-// failure AUTO falls back to the peer-mask ranking (variants 7 / 8, which
-// rank with explicit lane masks) and the explicit RANK variants refuse.
-__global__ __launch_bounds__(256) void lds_rtn_order_probe_kernel(uint32_t *bad) {
-    __shared__ uint32_t cnt[4][3][8];
+// device before the first such sort, in the scatter's widest shape (1024
+// threads, 16 waves, as variant 22 ranks), with four address patterns: every
+// lane on one counter, lane % 3, a scattered 5-way split, and most lanes on
+// one counter with a few elsewhere. Every address comes from a per-lane value
+// the compiler cannot prove uniform (`zero[lane]`, all 0 at run time), so the
+// atomic optimizer cannot turn the one-counter pattern into one add plus an
+// mbcnt prefix (ascending by construction: that would test the compiler, not
+// the LDS). Each lane's returned count must equal the number of
+// lower lanes on its counter. On a failure AUTO falls back to the peer-mask
+// ranking (variants 7 / 8, which rank with explicit lane masks) and the
+// explicit RANK variants refuse.
+__device__ __forceinline__ int probe_addr(int k, int lane) {
+    return k == 0 ? 0 : k == 1 ? lane % 3 : k == 2 ? (lane * 7) % 5 : (lane % 9 == 4 ? 1 + lane % 5 : 0);
+}
+
+__global__ __launch_bounds__(1024) void lds_rtn_order_probe_kernel(uint32_t *bad, const uint32_t *zero) {
+    constexpr int kPat = 4;
+    __shared__ uint32_t cnt[16][kPat][8];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int i = lane; i < 24; i += 64) (&cnt[w][0][0])[i] = 0;
+    for (int i = lane; i < kPat * 8; i += 64) (&cnt[w][0][0])[i] = 0;
     __syncthreads();
+    const uint32_t z = zero[lane];  // 0, but per lane and from memory
     uint32_t err = 0;
-    const int addr[3] = {0, lane % 3, (lane * 7) % 5};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t got = atomicAdd(&cnt[w][k][addr[k]], 1u);
+    for (int k = 0; k < kPat; ++k) {
+        const uint32_t got = atomicAdd(&cnt[w][k][probe_addr(k, lane) + z], 1u);
         uint32_t want = 0;
-        for (int j = 0; j < lane; ++j) {
-            const int aj = k == 0 ? 0 : k == 1 ? j % 3 : (j * 7) % 5;
-            want += aj == addr[k];
-        }
+        for (int j = 0; j < lane; ++j) want += probe_addr(k, j) == probe_addr(k, lane);
         err |= got != want;
     }
     if (err) bad[0] = 1u;  // vector store; any lane of any wave
@@ -341,9 +349,9 @@ int lds_rtn_order_ok(hipStream_t s) {
         return -1;  // no synchronous probe inside a graph capture (not cached: the next eager sort probes)
     uint32_t *d = nullptr, h = 1u;
     int ok = -1;
-    if (hipMalloc(&d, sizeof(uint32_t)) == hipSuccess) {
-        if (hipMemsetAsync(d, 0, sizeof(uint32_t), s) == hipSuccess) {
-            hipLaunchKernelGGL(lds_rtn_order_probe_kernel, dim3(1), dim3(256), 0, s, d);
+    if (hipMalloc(&d, 65 * sizeof(uint32_t)) == hipSuccess) {  // [0] = the flag, [1..64] = per-lane zeros
+        if (hipMemsetAsync(d, 0, 65 * sizeof(uint32_t), s) == hipSuccess) {
+            hipLaunchKernelGGL(lds_rtn_order_probe_kernel, dim3(1), dim3(1024), 0, s, d, d + 1);
             if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
                 hipStreamSynchronize(s) == hipSuccess)
                 ok = h == 0u ? 1 : 0;
