@@ -117,3 +117,34 @@ ckpt_r6_final() {
     python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
     du -sh "$O" && find "$O" -name "*.db" -delete && du -sh "$O"
 }
+
+# lab3 one-shot mfma16 kernel: 2 / 8 vectors per thread against 4 (A/B libs
+# abtmp/t2, abtmp/t8; small class counts), and the kernel trace of the
+# rotating nc = 4 loop (where the 121 µs per call go).
+ckpt_r6_trips() {
+    export O=${O:-gpurun_out/r6/trips}
+    mkdir -p "$O"
+    LAB3_NCS=4 LAB3_PATHS=mfma16,fast bash tools/gpu.sh prof rot_trace -- python tools/experiments/lab3_m16.py &&
+    for t in t2 t8; do
+        MPX_LIB_PATH=abtmp/$t/libmpx.so bash tools/gpu.sh tests tests/test_gpu_kernels.py -k "classify_mfma16" &&
+        LAB3_NCS=3,4,5,8 LAB3_PATHS=mfma16 \
+            bash tools/gpu.sh ab $t abtmp/$t/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py || return 1
+    done
+}
+
+# Short-slab segment sweep of the band kernel (strong-scaling per-rank floor).
+ckpt_r6_seg() {
+    export O=${O:-gpurun_out/r6/seg}
+    mkdir -p "$O"
+    bash tools/gpu.sh run seg 300 python -u tools/experiments/small_slab_seg.py
+}
+
+# lab3 mfma16: class constants pinned in VGPRs (no per-pixel re-copy from
+# SGPRs) — B = abtmp/pin against libmpx, classifier GPU tests on B first.
+ckpt_r6_pin() {
+    export O=${O:-gpurun_out/r6/pin}
+    mkdir -p "$O"
+    MPX_LIB_PATH=abtmp/pin/libmpx.so bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=2,3,4,5,8,12,16,24,32 LAB3_PATHS=mfma16 \
+        bash tools/gpu.sh ab pin abtmp/pin/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
+}
