@@ -148,3 +148,10 @@ ckpt_r6_pin() {
     LAB3_NCS=2,3,4,5,8,12,16,24,32 LAB3_PATHS=mfma16 \
         bash tools/gpu.sh ab pin abtmp/pin/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
 }
+
+# The whole -m gpu suite on the final tree.
+ckpt_r6_tests() {
+    export O=${O:-gpurun_out/r6/tests}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests
+}
