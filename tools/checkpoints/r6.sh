@@ -155,3 +155,12 @@ ckpt_r6_tests() {
     mkdir -p "$O"
     bash tools/gpu.sh tests
 }
+
+# The conv jobs of the scaling driver on the final tree (one GPU, ranks share it).
+ckpt_r6_multi2() {
+    export O=${O:-gpurun_out/r6/multi2}
+    mkdir -p "$O"
+    bash tools/gpu.sh run scale 900 python -u tools/scale.py --gpus 1,2,4 --rehearse --only conv --quick \
+        --out "$O/scale" &&
+    MPX_DIST_BACKEND=gloo bash tools/gpu.sh run drv2 300 python bench.py --gpus 2 --steps 20 --warmup 5
+}
