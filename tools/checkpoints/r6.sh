@@ -164,3 +164,14 @@ ckpt_r6_multi2() {
         --out "$O/scale" &&
     MPX_DIST_BACKEND=gloo bash tools/gpu.sh run drv2 300 python bench.py --gpus 2 --steps 20 --warmup 5
 }
+
+# Sort bench on the final tree, three runs (VERDICT r5 Next #3: within ±1 % of
+# round 5's 0.689-0.697 / 0.722-0.730 ms at 2^26).
+ckpt_r6_sort() {
+    export O=${O:-gpurun_out/r6/sort}
+    mkdir -p "$O"
+    for r in 1 2 3; do
+        LAB5_DTYPES=int32,float32 LAB5_LOGN=24,26 LAB5_VARIANTS=22 LAB5_ITERS=9 \
+            bash tools/gpu.sh run sort$r 300 python -u tools/experiments/lab5_bench.py || return 1
+    done
+}
