@@ -166,7 +166,9 @@ def test_job_span_charges_injected_start_skew():
     assert rec["start_skew_ms"] >= 250.0 and rec["job_span_ms"] >= rec["start_skew_ms"]
     # without the hook the ranks leave at one agreed instant (aligned_start): the
     # skew is the spin's resolution plus scheduling noise, not barrier wake-ups
-    assert base["start_skew_ms"] < 20.0
+    # (bounded well below the injected 300 ms: a loaded CI host can deschedule
+    # a spinning rank for tens of ms)
+    assert base["start_skew_ms"] < 100.0
     assert rec["max_rank_span_ms"] < 150.0  # no rank's own span holds the delay
     assert rec["value"] < base["value"] * (base["job_span_ms"] / 300.0)
 
