@@ -175,3 +175,14 @@ ckpt_r6_sort() {
             bash tools/gpu.sh run sort$r 300 python -u tools/experiments/lab5_bench.py || return 1
     done
 }
+
+# lab3 mfma16 with the fix-up fused into the one-shot kernel (the last block
+# of each sub-list re-ranks it; no fix-up launch): B = abtmp/fused against
+# libmpx, classifier GPU tests on B first.
+ckpt_r6_fused() {
+    export O=${O:-gpurun_out/r6/fused}
+    mkdir -p "$O"
+    MPX_LIB_PATH=abtmp/fused/libmpx.so bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py -k "classify" &&
+    LAB3_NCS=2,3,4,5,8,12,16,24,32 LAB3_PATHS=mfma16 \
+        bash tools/gpu.sh ab fused abtmp/fused/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
+}
