@@ -79,8 +79,9 @@ $(PYLIB): $(LIB_OBJS) | $(B)
 $(B)/t_%.o: native/tune/%.hip $(HDRS) | $(B)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(TUNELIB): $(B)/t_edge_variants.o $(B)/t_sort_variants.o $(PYLIB)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(B)/t_edge_variants.o $(B)/t_sort_variants.o -L$(dir $(PYLIB)) -lmpx -Wl,-rpath,'$$ORIGIN'
+TUNEOBJ   := $(B)/t_edge_variants.o $(B)/t_sort_variants.o $(B)/t_jacobi_variants.o $(B)/t_vsub_variants.o
+$(TUNELIB): $(TUNEOBJ) $(PYLIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(TUNEOBJ) -L$(dir $(PYLIB)) -lmpx -Wl,-rpath,'$$ORIGIN'
 
 $(ALIB): $(LIB_OBJS) | $(B)
 	rm -f $@ && ar rcs $@ $(LIB_OBJS)

@@ -43,7 +43,6 @@ _SIGNATURES = {
     "mpx_stream_sync": (c_int, [c_vp]),
     "mpx_vsub_f64": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
     "mpx_vsub_f32": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp]),
-    "mpx_vsub_variant": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
     "mpx_roberts": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "mpx_conv": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _fp, _fp, c_vp]),
     "mpx_conv_direct": (
@@ -66,7 +65,6 @@ _SIGNATURES = {
     "mpx_filter_name": (c_char_p, [c_int]),
     "mpx_class_stats": (c_int, [c_vp, c_int, c_int, c_int, _ip, _ip, _dp, _dp]),
     "mpx_classify": (c_int, [c_vp, c_i64, c_int, _dp, _dp, c_int, c_int, c_int, c_vp]),
-    "mpx_jacobi_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp]),
     "mpx_comm_load": (c_int, [ctypes.c_char_p]),
     "mpx_comm_version": (c_int, []),
     "mpx_comm_unique_id": (c_int, [c_vp, c_int]),
@@ -130,6 +128,9 @@ _TUNE_SIGNATURES = {
     # lab5 radix variants / scatter probe (native/tune/sort_variants.hip)
     "mpx_sort_variant": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_vp]),
     "mpx_sort_scatter_probe": (c_int, [c_vp, c_i64, c_vp, c_i64, c_int, c_vp]),
+    # lab1 / Jacobi tuning variants (native/tune/{vsub,jacobi}_variants.hip)
+    "mpx_vsub_variant": (c_int, [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp]),
+    "mpx_jacobi_variant": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp]),
 }
 _tune = None
 

@@ -14,7 +14,7 @@ from cuda_mpi_openmp_amd import _native, ops  # noqa: E402
 
 
 def main():
-    L = _native.lib()
+    L = _native.tune_lib()  # the variants live in libmpx_tune.so
     dev = torch.device("cuda:0")
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
     for dt in (torch.float64, torch.float32):

@@ -41,7 +41,7 @@ def main():
             us = time_us(fn)
             nb = byts if tag == "torch_sub" else 2 * n * a.element_size()
             print(json.dumps({"dtype": name, "what": tag, "us": round(us, 1), "TBps": round(nb / us / 1e6, 3)}))
-        L = _native.lib()
+        L = _native.tune_lib()  # the variants live in libmpx_tune.so
         fp64 = int(dtype == torch.float64)
         for kind, what in ((0, "1vec"), (1, "2vec"), (2, "1vec_ntload"), (3, "2vec_ntload")):
             for block in (256, 1024):
