@@ -516,3 +516,33 @@ def test_conv_resident_hint_same_bytes(gpu, fname):
     assert torch.equal(out, a)
     ln.resident = False
     assert not ln.resident
+
+
+def test_tune_library_variants_match_production(gpu):
+    """The tuning entry points that live in libmpx_tune.so (round 6: the
+    Jacobi and vsub variants left libmpx) compute what the production kernels
+    compute: vsub kinds 0-3 against ops.vsub, Jacobi wave variants against
+    ops.jacobi_sweep, interior rows bit-exact."""
+    from cuda_mpi_openmp_amd import _native
+
+    T = _native.tune_lib()
+    for dt in (torch.float32, torch.float64):
+        a = torch.rand(1 << 20, dtype=dt, device=gpu)
+        b = torch.rand(1 << 20, dtype=dt, device=gpu)
+        want = ops.vsub(a, b)
+        for kind in range(4):
+            c = torch.full_like(a, float("nan"))
+            _native.check(T.mpx_vsub_variant(a.data_ptr(), b.data_ptr(), c.data_ptr(), a.numel(),
+                                             int(dt == torch.float64), kind, 0, None))
+            torch.cuda.synchronize()
+            assert torch.equal(c, want), (dt, kind)
+        n = 512
+        u = torch.rand((n + 2, n), dtype=dt, device=gpu)
+        ref = torch.empty_like(u)
+        ops.jacobi_sweep(u, ref, 1, n + 1)
+        for R, aux in ((8, 0), (8, 18), (5, 2), (16, 22)):
+            un = torch.zeros_like(u)
+            _native.check(T.mpx_jacobi_variant(u.data_ptr(), un.data_ptr(), n, n, 1, n + 1, None,
+                                               int(dt == torch.float64), R, aux, None))
+            torch.cuda.synchronize()
+            assert torch.equal(un[1:n + 1, 1:-1], ref[1:n + 1, 1:-1]), (dt, R, aux)

@@ -186,3 +186,12 @@ ckpt_r6_fused() {
     LAB3_NCS=2,3,4,5,8,12,16,24,32 LAB3_PATHS=mfma16 \
         bash tools/gpu.sh ab fused abtmp/fused/libmpx.so 3 -- python -u tools/experiments/lab3_m16.py
 }
+
+# After the Jacobi / vsub variants moved to the tune library.
+ckpt_r6_tunemove() {
+    export O=${O:-gpurun_out/r6/tunemove}
+    mkdir -p "$O"
+    bash tools/gpu.sh tests tests/test_gpu_kernels.py tests/test_gpu_headline.py tests/test_peer_halo.py \
+        -k "jacobi or vsub or tune" &&
+    JBENCH_R=8 JBENCH_AUX=18 bash tools/gpu.sh run jbench 300 python -u tools/experiments/jbench.py 8192
+}
