@@ -195,3 +195,13 @@ ckpt_r6_tunemove() {
         -k "jacobi or vsub or tune" &&
     JBENCH_R=8 JBENCH_AUX=18 bash tools/gpu.sh run jbench 300 python -u tools/experiments/jbench.py 8192
 }
+
+# The driver's bench command under the kernel trace (per-kernel stats of the
+# flagship step), summarised for profiles/.
+ckpt_r6_benchprof() {
+    export O=${O:-gpurun_out/r6/benchprof}
+    mkdir -p "$O"
+    bash tools/gpu.sh prof bench_trace -- python3 bench.py --gpus 1 --steps 20 --warmup 5 &&
+    python tools/prof_summary.py trace "$O/bench_trace" > "$O/bench_trace.md" &&
+    find "$O" -name "*.db" -delete
+}
