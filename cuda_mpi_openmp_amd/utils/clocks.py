@@ -339,6 +339,7 @@ def _child_main(argv=None) -> int:
     a = ap.parse_args(argv)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    parent = os.getppid()  # a parent that dies without stop() must not leave this loop running
     cs = ClockSampler(hz=a.hz, bdf=a.bdf)
     with open(a.out, "a") as f:
         f.write(json.dumps({"source": cs.source, "error": cs.error}) + "\n")
@@ -347,7 +348,7 @@ def _child_main(argv=None) -> int:
             return 0
         period = 1.0 / max(1.0, a.hz)
         nxt = time.monotonic()
-        while not stop.is_set():
+        while not stop.is_set() and os.getppid() == parent:
             t0 = _clock_ns()
             try:
                 m = cs._src.read()

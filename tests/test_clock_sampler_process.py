@@ -60,3 +60,32 @@ def test_process_sampler_child_writes_samples(tmp_path, monkeypatch):
     assert len(ps.samples) == len(lines) - 1 and all(m["current_gfxclk"] == 2100.0 for _, m in ps.samples)
     t0 = [t for t, _ in ps.samples]
     assert t0 == sorted(t0) and abs(t0[-1] - clocks._clock_ns()) < 10e9
+
+
+def test_process_sampler_child_exits_with_its_parent(tmp_path, monkeypatch):
+    """The child's loop ends when its parent is gone (os.getppid changes), so
+    a benchmark that dies without stop() leaves no sampler behind."""
+    out = tmp_path / "s.txt"
+
+    class Fake:
+        def read(self):
+            return {"current_gfxclk": 2100.0}
+
+        def close(self):
+            pass
+
+    def init(self, hz=200.0, bdf=None):
+        self._src, self.source, self.error = Fake(), "fake", None
+
+    monkeypatch.setattr(clocks.ClockSampler, "__init__", init)
+    real = os.getppid()
+    calls = [0]
+
+    def ppid():
+        calls[0] += 1
+        return real if calls[0] < 5 else 1  # re-parented after a few samples
+    monkeypatch.setattr(clocks.os, "getppid", ppid)
+    t0 = time.monotonic()
+    assert clocks._child_main(["--hz", "200", "--out", str(out)]) == 0
+    assert time.monotonic() - t0 < 5
+    assert 2 <= len(out.read_text().splitlines()) <= 6
