@@ -1,7 +1,11 @@
-/* Tuning entry points of libmpx.so (not part of the production C API in
- * capi.h). They live beside file-local kernels that libmpx_tune.so cannot
- * reach: the sort's schedule variants and its scatter attribution probe.
- * Used by tools/experiments/{lab5_bench,sort_probe}.py and the GPU sort suite. */
+/* Tuning entry points exported by libmpx_tune.so (native/tune/, `make tune`),
+ * not by libmpx.so and not part of the production C API in capi.h. Declared
+ * here for the sort (native/tune/sort_variants.hip, kernels shared with the
+ * production sort through src/kernels/sort_radix.hpp); the conv, Jacobi and
+ * vsub variants (mpx_conv_variant, mpx_jacobi_variant, mpx_vsub_variant) are
+ * bound by name from Python (_native.tune_lib). Used by
+ * tools/experiments/{lab5_bench,sort_probe,jbench,vsub_sweep}.py, tools/kbench.py
+ * and the GPU suites. */
 #ifndef MPX_TUNING_H
 #define MPX_TUNING_H
 
@@ -11,7 +15,7 @@
 extern "C" {
 #endif
 
-/* The sort with a fixed radix schedule (sort.hip, radix_sort32): 0 = AUTO,
+/* The sort with a fixed radix schedule (sort_variants.hip): 0 = AUTO,
  * 1 onesweep (look-back), 2 reduce-then-scan, 4 / 7 / 8 persistent scatters
  * (round 2-3), 9-13 the returning-add ranking (8192 / 4096-key tiles, 3 blocks
  * per CU, two tiles in flight), 14 the lean onesweep, 15 the same at one block per CU. */
