@@ -205,3 +205,12 @@ ckpt_r6_benchprof() {
     python tools/prof_summary.py trace "$O/bench_trace" > "$O/bench_trace.md" &&
     find "$O" -name "*.db" -delete
 }
+
+# Last look at the committed tree: smoke and the driver's bench command.
+ckpt_r6_last() {
+    export O=${O:-gpurun_out/r6/last}
+    mkdir -p "$O"
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh run bench_default 300 python bench.py
+}
