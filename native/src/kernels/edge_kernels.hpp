@@ -73,6 +73,48 @@ __device__ __forceinline__ void mag2_to_gray(float s0, float s1, uint32_t &g0, u
     }
 }
 
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// Four magnitudes at once, no float->int conversion (band kernels: 20 VALU for
+// four pixels where two mag2_to_gray take 24).
+// r = v_sqrt(med3(s, 0.5^2, 255.5^2)) as in mag2_to_gray; then, packed,
+// x+- = (r - 0.5 +- kSqrtMargin) + 2^23. Both sums before the last are exact
+// (r < 512: every operand a multiple of ulp(r)), and the last rounds to the
+// nearest integer, so x+- = 2^23 + RNE(r - 0.5 +- m): equal exactly when no
+// integer lies within about m of r, i.e. when v_sqrt (error < m / 4) decides
+// trunc(sqrt_rn(s)) = RNE(r - 0.5 + m) — which is the low byte of x+'s bits
+// (0x4B0000nn, n <= 255 since r <= 255.5 + ulp). The float compare x+ == x-
+// is false on NaN, so a NaN magnitude takes the exact path as before. g[i]
+// holds the gray level in its LOW BYTE only (the callers' v_perm reads byte 0).
+// tests/test_gpu_kernels.py checks this form exhaustively too.
+__device__ __forceinline__ void mag4_to_gray(f2_t s01, f2_t s23, uint32_t g[4]) {
+    constexpr float kTwo23 = 8388608.0f;
+    const f2_t c01 = {__builtin_amdgcn_fmed3f(s01.x, 0.25f, 65280.25f), __builtin_amdgcn_fmed3f(s01.y, 0.25f, 65280.25f)};
+    const f2_t c23 = {__builtin_amdgcn_fmed3f(s23.x, 0.25f, 65280.25f), __builtin_amdgcn_fmed3f(s23.y, 0.25f, 65280.25f)};
+    const f2_t r01 = {__builtin_amdgcn_sqrtf(c01.x), __builtin_amdgcn_sqrtf(c01.y)};
+    const f2_t r23 = {__builtin_amdgcn_sqrtf(c23.x), __builtin_amdgcn_sqrtf(c23.y)};
+    const f2_t kp = {-0.5f + kSqrtMargin, -0.5f + kSqrtMargin}, km = {-0.5f - kSqrtMargin, -0.5f - kSqrtMargin};
+    const f2_t big = {kTwo23, kTwo23};
+    const f2_t p01 = (r01 + kp) + big, m01 = (r01 + km) + big;
+    const f2_t p23 = (r23 + kp) + big, m23 = (r23 + km) + big;
+    const bool ok = (int)(p01.x == m01.x) & (int)(p01.y == m01.y) & (int)(p23.x == m23.x) & (int)(p23.y == m23.y);
+    if (ok) {
+        // whole-vector bit casts: __builtin_bit_cast of one ext_vector element
+        // (p01.y) miscompiles with this ROCm clang (the other element is read)
+        typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+        const u2_t b01 = __builtin_bit_cast(u2_t, p01), b23 = __builtin_bit_cast(u2_t, p23);
+        g[0] = b01.x;
+        g[1] = b01.y;
+        g[2] = b23.x;
+        g[3] = b23.y;
+    } else {
+        g[0] = mpx_sat_u8(sqrtf(s01.x));
+        g[1] = mpx_sat_u8(sqrtf(s01.y));
+        g[2] = mpx_sat_u8(sqrtf(s23.x));
+        g[3] = mpx_sat_u8(sqrtf(s23.y));
+    }
+}
+
 template <int MODE, bool FAST>
 __device__ __forceinline__ uint32_t finish_gray(float gx, float gy) {
     if constexpr (MODE == MPX_CONV_MAG2) {
@@ -344,6 +386,18 @@ __device__ __forceinline__ float from_prev(float v) {
 __device__ __forceinline__ float from_next(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), kDppShl1, 0xf, 0xf, true));
 }
+// Wave shift whose source-less lane (0 for shr, 63 for shl) keeps `old`
+// (bound_ctrl off: that lane's write is the old value, not 0).
+// (a <= b) ? n : 0 for buffer-descriptor sizes (wave-uniform operands): an
+// s_cselect as long as n is not also held in a VGPR — otherwise the select
+// lowers to a lane-mask v_cndmask and the descriptor in VGPRs costs a
+// readfirstlane loop around every access (so no VALU value may be w * 4).
+__device__ __forceinline__ int scalar_le_sel(int a, int b, int n) { return a <= b ? n : 0; }
+template <int CTRL>
+__device__ __forceinline__ float shift_or_old(float old, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                 CTRL, 0xf, 0xf, false));
+}
 
 template <int K, int A, int OWX = 0>
 struct WaveGeom {
@@ -492,8 +546,6 @@ __device__ __forceinline__ float sep_scale(const Taps &t) {
     if constexpr (F::kConst) return Y ? F::sy : F::sx;
     else return Y ? t.wy[2 * K] : t.wx[2 * K];
 }
-
-typedef float f2_t __attribute__((ext_vector_type(2)));
 
 // One step of a tap chain acc = fma(c, x, acc) started at 0. With compile-time
 // taps, zero taps are skipped and the first nonzero tap is a plain product
@@ -860,7 +912,19 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // OPT bit 4 (cost probe only, wrong at strip edges): no apron loads
     const bool ap_have = !HL && !(OPT & 16) && ((ap_left && x0 > 0) || (ap_right && x0 + 256 < w));
     constexpr int kDrop = 0x7ffffff0;
-    const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : kDrop;
+    // DPP-old apron (every production instance; the HL / batched / no-apron
+    // tuning probes keep the select form): lanes 0 / 63 feed their apron luma
+    // as the `old` operand of the wave-shift DPP moves, the only lanes whose
+    // shift has no source lane — no v_cndmask per window value. At the image
+    // edges the lane loads its edge PAIR ((0, 1) / (w-2, w-1)) and one per-lane
+    // byte select per apron pixel makes it (p0, p0) / (p[w-1], p[w-1]).
+    constexpr bool kDppApron = (OPT & (8 | 16 | 512)) == 0;
+    const bool fix_l = kDppApron && ap_left && x0 == 0, fix_r = kDppApron && ap_right && x0 + 256 >= w;
+    // (fix_r: lane 63's quad offset cc = w - 4 plus 8 B, not (w - 2) * 4 — a w * 4
+    // in a VGPR would turn the uniform descriptor-size selects into v_cndmasks)
+    const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : (fix_l ? 0 : (fix_r ? cc * 4 + 8 : kDrop));
+    const uint32_t ap_selx = fix_r ? 0x07060504u : 0x03020100u;  // perm(ap.y, ap.x, .): fix_r takes ap.y
+    const uint32_t ap_sely = fix_l ? 0x03020100u : 0x07060504u;  // fix_l takes ap.x
     const int iy0 = ys - A;
     const int iy_last = ye - 1 + R;
     auto row_ptr = [&](int i) {
@@ -869,18 +933,21 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         return src + (int64_t)gy * pitch;
     };
     // the prefetch ring runs D rows past the walk's last input row (nrows + K - 2);
-    // those loads are never consumed: their offsets go out of range, so the
+    // those loads are never consumed: their descriptor is empty, so the
     // hardware drops them instead of fetching a neighbour segment's rows
     const int i_last = ye - ys + K - 2;
     static_assert(VSEG == 0 || (A == 2 && K == 5 && VSEG >= 8), "vertical sharing: 5-row windows, 2 + 2 halo rows");
     auto load_row = [&](int i, u32x2_t &ap) -> u32x4_t {
         const uint32_t *row = row_ptr(min(i, i_last));
+        // wave-uniform; VSEG: rows an LDS slot delivers issue no memory access.
+        // A dead row gets an empty descriptor (scalar), not dropped offsets: no
+        // per-row v_cndmask on the lanes' (loop-invariant) offsets
+        int nrec = scalar_le_sel(i, i_last, w * 4);
+        if constexpr (VSEG > 0)
+            nrec = ((i < 2 && vx.take_start >= 0) || (i >= VSEG + 2 && vx.take_end >= 0)) ? 0 : nrec;
         const __amdgpu_buffer_rsrc_t rr =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, w * 4, 0x00020000);
-        // wave-uniform; VSEG: rows an LDS slot delivers issue no memory access
-        const bool live = i <= i_last && !(VSEG > 0 && ((i < 2 && vx.take_start >= 0) ||
-                                                        (i >= VSEG + 2 && vx.take_end >= 0)));
-        const int qo = live ? cc * 4 : kDrop, ao = live ? ap_off : kDrop;
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(row), 0, nrec, 0x00020000);
+        const int qo = cc * 4, ao = ap_off;
         u32x4_t q;
         // OPT bit 5: rows no neighbouring segment reads (K-1 <= i < nrows) load
         // non-temporal; bit 6: every row does (probes)
@@ -903,6 +970,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         return q;
     };
     auto fix_quad = [&](u32x4_t q) -> u32x4_t {
+        if constexpr ((OPT & 1024) != 0) return q;  // strip inside the image: no lane past w
         if constexpr (HL) {
             if (q_left) return u32x4_t{q.x, q.x, q.x, q.x};
         }
@@ -943,6 +1011,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             const f2_t lft = {rl(ab.x, 2 * ri), rl(ab.y, 2 * ri)};
             const f2_t rgt = {rl(ab.x, 2 * ri + 1), rl(ab.y, 2 * ri + 1)};
             la = ap_left ? lft : rgt;
+        } else if constexpr (kDppApron) {
+            la = luma2(__builtin_amdgcn_perm(ap.y, ap.x, ap_selx), __builtin_amdgcn_perm(ap.y, ap.x, ap_sely));
         } else {
             la = luma2(ap.x, ap.y);
         }
@@ -951,23 +1021,45 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         wv[A + 1] = l01.y;
         wv[A + 2] = l23.x;
         wv[A + 3] = l23.y;
-        if constexpr (A >= 1) {
-            const float d = from_prev(l23.y);
-            wv[A - 1] = ap_left ? (ap_have ? la.y : l01.x) : d;
+        if constexpr (kDppApron) {
+            // lane 0 (no lane to its left) keeps `old` = its left apron, lane
+            // 63 (none to its right) its right apron
+            if constexpr (A >= 1) wv[A - 1] = shift_or_old<kDppShr1>(la.y, l23.y);
+            if constexpr (A >= 2) wv[A - 2] = shift_or_old<kDppShr1>(la.x, l23.x);
+            if constexpr (R >= 1) wv[A + 4] = shift_or_old<kDppShl1>(la.x, l01.x);
+            if constexpr (R >= 2) wv[A + 5] = shift_or_old<kDppShl1>(la.y, l01.y);
+        } else {
+            if constexpr (A >= 1) {
+                const float d = from_prev(l23.y);
+                wv[A - 1] = ap_left ? (ap_have ? la.y : l01.x) : d;
+            }
+            if constexpr (A >= 2) {
+                const float d = from_prev(l23.x);
+                wv[A - 2] = ap_left ? (ap_have ? la.x : l01.x) : d;
+            }
+            if constexpr (R >= 1) {
+                const float d = from_next(l01.x);
+                wv[A + 4] = ap_right ? (ap_have ? la.x : l23.y) : d;
+            }
+            if constexpr (R >= 2) {
+                const float d = from_next(l01.y);
+                wv[A + 5] = ap_right ? (ap_have ? la.y : l23.y) : d;
+            }
         }
-        if constexpr (A >= 2) {
-            const float d = from_prev(l23.x);
-            wv[A - 2] = ap_left ? (ap_have ? la.x : l01.x) : d;
-        }
-        if constexpr (R >= 1) {
-            const float d = from_next(l01.x);
-            wv[A + 4] = ap_right ? (ap_have ? la.x : l23.y) : d;
-        }
-        if constexpr (R >= 2) {
-            const float d = from_next(l01.y);
-            wv[A + 5] = ap_right ? (ap_have ? la.y : l23.y) : d;
-        }
-        if constexpr (SEP) {
+        if constexpr (SEP && kDppApron && A == 2 && R == 2) {
+            // 5-wide windows: the seven packed operands (w[j], w[j+1]) as the
+            // four aligned pairs plus three half-shifted ones (one v_pk_mov
+            // each), instead of the compiler's per-element copies
+            const f2_t e0 = {wv[0], wv[1]}, e3 = {wv[6], wv[7]};
+            const f2_t pw[7] = {e0, __builtin_shufflevector(e0, l01, 1, 2), l01, __builtin_shufflevector(l01, l23, 1, 2),
+                                l23, __builtin_shufflevector(l23, e3, 1, 2), e3};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                auto pair = [&](int dx) { return pw[2 * e + dx]; };
+                hxr[u][e] = sep_chain<F, K, 0>(taps, pair);
+                if constexpr (TWO) hyr[u][e] = sep_chain<F, K, 2>(taps, pair);
+            }
+        } else if constexpr (SEP) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 auto pair = [&](int dx) { return f2_t{wv[2 * e + dx], wv[2 * e + dx + 1]}; };
@@ -1046,6 +1138,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         const int y = UP ? ye - 1 - (g * D + v) : ys + g * D + v;
         auto slot = [&](int dy) { return UP ? (u + K - dy) % K : (u + 1 + dy) % K; };
         uint32_t gray[4];
+        f2_t sq2[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             f2_t gx = {0.0f, 0.0f}, gy = {0.0f, 0.0f};
@@ -1075,7 +1168,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             if constexpr (TWO) {
                 const f2_t sq = gx * gx + gy * gy;
                 if constexpr (FAST) {
-                    mag2_to_gray(sq.x, sq.y, gray[2 * e], gray[2 * e + 1]);
+                    sq2[e] = sq;  // all four pixels at once below
                 } else {
                     gray[2 * e] = mag_to_gray<false>(sq.x);
                     gray[2 * e + 1] = mag_to_gray<false>(sq.y);
@@ -1085,6 +1178,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
                 gray[2 * e + 1] = finish_gray<MODE, FAST>(gx.y, 0.0f);
             }
         }
+        if constexpr (TWO && FAST) mag4_to_gray(sq2[0], sq2[1], gray);
         const uint32_t a = alp[slot(A)];
         u32x4_t o;
         o.x = __builtin_amdgcn_perm(a, gray[0], 0x04000000u);
@@ -1093,8 +1187,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
         o.w = __builtin_amdgcn_perm(a, gray[3], 0x07000000u);
         const bool row_ok = UP ? y >= ys : y < ye;
         const int yc = row_ok ? y : ys;
-        const __amdgpu_buffer_rsrc_t orow =
-            __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)yc * pitch, 0, row_ok ? w * 4 : 0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
+            out + (int64_t)yc * pitch, 0, UP ? scalar_le_sel(ys, y, w * 4) : scalar_le_sel(y, ye - 1, w * 4), 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(o, orow, st ? cin * 4 : kDrop, 0, (OPT & 2) ? 2 : 0);
         if constexpr (SPW) {
             const int own = rs.own_rows;
@@ -1133,7 +1227,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // segment reads, bit 6 non-temporal loads of every row, bit 7 keeps the apron
 // loads plain under bit 5 / 6, bit 3 one batched apron load per walk (walks of
 // at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
-// lanes instead of aprons.
+// lanes instead of aprons. Bit 10 is internal (set per wave for strips inside
+// the image, see the end of the kernel).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
@@ -1194,10 +1289,21 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
             return;
         }
     }
-    if ((alt & 1) && (sg & 1))  // wave-uniform: odd segments walk up
-        band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
-    else
-        band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+    // wave-uniform: odd segments walk up; strips wholly inside the image (every
+    // strip when w % 256 == 0) skip the per-row clamp of lanes past w (OPT bit 10)
+    constexpr int OIN = (OPT & 512) ? OPT : (OPT | 1024);
+    const bool inside = !(OPT & 512) && strip * SW + 256 <= w;
+    if ((alt & 1) && (sg & 1)) {
+        if (inside)
+            band4_walk<K, A, MODE, FAST, F, true, OIN>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+        else
+            band4_walk<K, A, MODE, FAST, F, true, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+    } else {
+        if (inside)
+            band4_walk<K, A, MODE, FAST, F, false, OIN>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+        else
+            band4_walk<K, A, MODE, FAST, F, false, OPT>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
+    }
 }
 
 // ---------------------------------------------------------------------------

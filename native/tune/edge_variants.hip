@@ -19,13 +19,28 @@ namespace {
 // raw = 2: the paired production path of the band / wave kernels
 // (mag2_to_gray: v_med3 clamp into [0.5^2, 255.5^2], margin test on both
 // lanes, one exact fallback for the pair) — lane pairs (s, s') with s' walking
-// the range backwards, so every value meets fast and fallback partners.
+// the range backwards, so every value meets fast and fallback partners;
+// raw = 3: the four-pixel production path of the band kernels (mag4_to_gray:
+// no float->int conversion, the gray level in the low byte of 2^23 + n) — each
+// value with three partners (walking backwards, and the two mirrors about the
+// range's quarter points), only the low byte compared.
 __global__ void fast_sqrt_selftest_kernel(uint32_t first, uint32_t last, unsigned long long *bad, int raw) {
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long nbad = 0;
     for (uint32_t u = first + blockIdx.x * blockDim.x + threadIdx.x; u <= last && u >= first; u += stride) {
         const float s = __builtin_bit_cast(float, u);
         const uint32_t exact = edge::mag_to_gray<false>(s);
+        if (raw == 3) {
+            const uint32_t n = last - first, k = u - first;
+            const float s1 = __builtin_bit_cast(float, last - k);
+            const float s2 = __builtin_bit_cast(float, first + (k + n / 4) % (n + 1));
+            const float s3 = __builtin_bit_cast(float, first + (k + 3 * (n / 4)) % (n + 1));
+            uint32_t g[4];
+            edge::mag4_to_gray(edge::f2_t{s, s1}, edge::f2_t{s2, s3}, g);
+            nbad += ((g[0] & 255u) != exact) + ((g[1] & 255u) != edge::mag_to_gray<false>(s1)) +
+                    ((g[2] & 255u) != edge::mag_to_gray<false>(s2)) + ((g[3] & 255u) != edge::mag_to_gray<false>(s3));
+            continue;
+        }
         if (raw == 2) {
             const float s1 = __builtin_bit_cast(float, last - (u - first));
             uint32_t g0, g1;
@@ -387,10 +402,11 @@ extern "C" int mpx_conv_variant(const uint32_t *in, uint32_t *out, int w, int h,
 extern "C" int mpx_selftest_fast_sqrt(unsigned long long *bad_device, int raw, void *stream) {
     using namespace mpx;
     MPX_CHECK_ARG(bad_device, "null counter");
-    // raw 0 / 1: every float in [0, 65025] (255^2); raw 2: every float in
-    // [0, +inf] (a squared magnitude is never NaN)
+    // raw 0 / 1: every float in [0, 65025] (255^2); raw 2 / 3: every float in
+    // [0, +inf] (a squared magnitude from finite taps is never NaN)
+    MPX_CHECK_ARG(raw >= 0 && raw <= 3, "raw: 0..3");
     hipLaunchKernelGGL(fast_sqrt_selftest_kernel, dim3(kNumCUs * 16), dim3(256), 0, as_stream(stream), 0u,
-                       raw == 2 ? 0x7F800000u : 0x477E0100u, bad_device, raw);
+                       raw >= 2 ? 0x7F800000u : 0x477E0100u, bad_device, raw);
     MPX_RETURN_IF_HIP_ERROR(hipGetLastError());
     return MPX_OK;
 }

@@ -445,14 +445,17 @@ def test_fast_sqrt_exhaustive(gpu, capsys):
         counts.append(int(bad.item()))
     # the paired production path (mag2_to_gray: v_med3 clamp, margin test on
     # both lanes) over every float in [0, +inf], each paired with another value
-    bad = torch.zeros(1, dtype=torch.int64, device=gpu)
-    _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), 2, 0))
-    torch.cuda.synchronize()
-    counts.append(int(bad.item()))
+    # and the band kernels' four-pixel form (mag4_to_gray: gray level from the
+    # low byte of 2^23 + n, no conversion), every value with three partners
+    for raw in (2, 3):
+        bad = torch.zeros(1, dtype=torch.int64, device=gpu)
+        _native.check(L.mpx_selftest_fast_sqrt(bad.data_ptr(), raw, 0))
+        torch.cuda.synchronize()
+        counts.append(int(bad.item()))
     with capsys.disabled():
         print(f"\nfast sqrt mismatches over all fp32 in [0, 65025]: production {counts[0]}, bare v_sqrt {counts[1]}; "
-              f"paired production path over [0, inf]: {counts[2]}")
-    assert counts[0] == 0 and counts[2] == 0
+              f"over [0, inf]: paired path {counts[2]}, four-pixel path {counts[3]}")
+    assert counts[0] == 0 and counts[2] == 0 and counts[3] == 0
 
 
 @pytest.mark.parametrize("hw", [(5, 64), (23, 130), (47, 260), (200, 300), (1001, 517), (4096, 4096)])

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-6 second-session GPU checkpoints (gpurun: bash tools/checkpoints/r6_s2.sh <name>).
+# Every GPU step has its own time limit; the first failing step ends the call.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+name=$1
+out=$R/gpurun_out/$name
+mkdir -p "$out"
+pmc() {  # pmc <tag> <counters...>: one counter pass over a short bench
+    local tag=$1; shift
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc "$@" -d "$out/pmc_$tag" -o pmc -- \
+        python3 "$R/bench.py" --steps 5 --warmup 2 > "$out/pmc_$tag.log" 2>&1)
+}
+case "$name" in
+g1)  # sobel5 band-kernel VALU cut: lab2 GPU tests, bench, VALU counters
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+        tests/test_gpu_kernels.py tests/test_gpu_headline.py -m gpu > "$out/tests.log" 2>&1 \
+        || { tail -40 "$out/tests.log"; exit 1; }
+    tail -3 "$out/tests.log"
+    timeout -k 10 200 python bench.py > "$out/bench1.log" 2>&1 || { tail -20 "$out/bench1.log"; exit 1; }
+    tail -1 "$out/bench1.log" | cut -c1-700
+    pmc valu SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU; echo "pmc rc=$?"
+    ;;
+edges)  # the band-kernel strip-edge cases only, every filter and width
+    timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread \
+        "tests/test_gpu_kernels.py::test_conv_band_kernel_strip_edges" -m gpu > "$out/tests.log" 2>&1
+    grep -E "passed|failed|FAILED" "$out/tests.log" | tail -60
+    ;;
+probe)  # band-kernel edge debug probe
+    PYTHONPATH=$R timeout -k 10 200 python -u tools/experiments/band_edge_probe.py > "$out/probe.log" 2>&1; rc=$?
+    tail -80 "$out/probe.log"; exit $rc
+    ;;
+*) echo "unknown checkpoint $name"; exit 2 ;;
+esac
