@@ -30,5 +30,8 @@ probe)  # band-kernel edge debug probe
     PYTHONPATH=$R timeout -k 10 200 python -u tools/experiments/band_edge_probe.py > "$out/probe.log" 2>&1; rc=$?
     tail -80 "$out/probe.log"; exit $rc
     ;;
+full)  # the whole GPU suite and smoke on the current tree
+    O=$out bash tools/gpu.sh tests && O=$out bash tools/gpu.sh smoke
+    ;;
 *) echo "unknown checkpoint $name"; exit 2 ;;
 esac
