@@ -925,6 +925,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     const int ap_off = ap_have ? (ap_left ? x0 - 2 : x0 + 256) * 4 : (fix_l ? 0 : (fix_r ? cc * 4 + 8 : kDrop));
     const uint32_t ap_selx = fix_r ? 0x07060504u : 0x03020100u;  // perm(ap.y, ap.x, .): fix_r takes ap.y
     const uint32_t ap_sely = fix_l ? 0x03020100u : 0x07060504u;  // fix_l takes ap.x
+    if constexpr (VSEG > 0) ye = ys + VSEG;  // (the caller's guarantee, made visible: every bound compile-time)
     const int iy0 = ys - A;
     const int iy_last = ye - 1 + R;
     auto row_ptr = [&](int i) {
@@ -997,12 +998,15 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     u32x2_t apr[D];
     f2_t hxr[SEP ? K : 1][2], hyr[SEP ? K : 1][2];  // separable: per-row horizontal sums
     float win[SEP ? 1 : K][NV];                      // dense: per-row luminance windows
-    uint32_t alp[K];
+    // alpha bytes of each ring row, two pixels per register (byte 0 / 1: pixels
+    // 0 / 1 of the lane's quad; 2 / 3 in alq): two v_perm per consumed row,
+    // and the output's v_perm reads the byte straight from them
+    uint32_t alp[K], alq[K];
 
     auto consume = [&](int u, u32x4_t px, u32x2_t ap, int ri) {
         const f2_t l01 = luma2(px.x, px.y), l23 = luma2(px.z, px.w);
-        alp[u] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(px.w, px.z, 0x07030000u),
-                                       __builtin_amdgcn_perm(px.y, px.x, 0x07030000u), 0x07060302u);
+        alp[u] = __builtin_amdgcn_perm(px.y, px.x, 0x0c0c0703u);
+        alq[u] = __builtin_amdgcn_perm(px.w, px.z, 0x0c0c0703u);
         f2_t la;
         if constexpr ((OPT & 8) != 0) {
             auto rl = [&](float x, int l) {
@@ -1179,12 +1183,12 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             }
         }
         if constexpr (TWO && FAST) mag4_to_gray(sq2[0], sq2[1], gray);
-        const uint32_t a = alp[slot(A)];
+        const uint32_t a = alp[slot(A)], b = alq[slot(A)];
         u32x4_t o;
         o.x = __builtin_amdgcn_perm(a, gray[0], 0x04000000u);
         o.y = __builtin_amdgcn_perm(a, gray[1], 0x05000000u);
-        o.z = __builtin_amdgcn_perm(a, gray[2], 0x06000000u);
-        o.w = __builtin_amdgcn_perm(a, gray[3], 0x07000000u);
+        o.z = __builtin_amdgcn_perm(b, gray[2], 0x04000000u);
+        o.w = __builtin_amdgcn_perm(b, gray[3], 0x05000000u);
         const bool row_ok = UP ? y >= ys : y < ye;
         const int yc = row_ok ? y : ys;
         const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(
@@ -1229,6 +1233,7 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
 // lanes instead of aprons. Bit 10 is internal (set per wave for strips inside
 // the image, see the end of the kernel).
+inline constexpr int kBandFullSeg = 16;  // the auto segment of a 4096^2 frame (edge_launch.hpp)
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
@@ -1290,10 +1295,25 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
         }
     }
     // wave-uniform: odd segments walk up; strips wholly inside the image (every
-    // strip when w % 256 == 0) skip the per-row clamp of lanes past w (OPT bit 10)
+    // strip when w % 256 == 0) skip the per-row clamp of lanes past w (OPT bit
+    // 10); 5-row windows over exactly kBandFullSeg rows (every segment of the
+    // 4096^2 flagship) run the fully unrolled walk — no loop-carried ring
+    // copies, every row's liveness and load policy compile-time
     constexpr int OIN = (OPT & 512) ? OPT : (OPT | 1024);
     const bool inside = !(OPT & 512) && strip * SW + 256 <= w;
-    if ((alt & 1) && (sg & 1)) {
+    const bool up = (alt & 1) && (sg & 1);
+    if constexpr (K == 5 && A == 2 && !(OPT & 8)) {
+        if (inside && ye - ys == kBandFullSeg) {
+            if (up)
+                band4_walk<K, A, MODE, FAST, F, true, OIN, false, kBandFullSeg>(in, out, w, pitch, ys, ye, y_lo, y_hi,
+                                                                                strip * SW, taps, rs);
+            else
+                band4_walk<K, A, MODE, FAST, F, false, OIN, false, kBandFullSeg>(in, out, w, pitch, ys, ye, y_lo, y_hi,
+                                                                                 strip * SW, taps, rs);
+            return;
+        }
+    }
+    if (up) {
         if (inside)
             band4_walk<K, A, MODE, FAST, F, true, OIN>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);
         else

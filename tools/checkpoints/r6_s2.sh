@@ -4,7 +4,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 name=$1
-out=$R/gpurun_out/$name
+out=$R/gpurun_out/${OUTNAME:-$name}
 mkdir -p "$out"
 pmc() {  # pmc <tag> <counters...>: one counter pass over a short bench
     local tag=$1; shift
@@ -32,6 +32,13 @@ probe)  # band-kernel edge debug probe
     ;;
 full)  # the whole GPU suite and smoke on the current tree
     O=$out bash tools/gpu.sh tests && O=$out bash tools/gpu.sh smoke
+    ;;
+g2)  # g1 plus a second bench and a kernel trace of the bench
+    OUTNAME=g2 bash "$0" g1 || exit 1
+    timeout -k 10 200 python bench.py > "$out/bench2.log" 2>&1 || { tail -20 "$out/bench2.log"; exit 1; }
+    tail -1 "$out/bench2.log" | cut -c1-300
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o trace -- \
+        python3 "$R/bench.py" --steps 20 --warmup 5 > "$out/trace.log" 2>&1); echo "trace rc=$?"
     ;;
 *) echo "unknown checkpoint $name"; exit 2 ;;
 esac
