@@ -1233,7 +1233,6 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
 // lanes instead of aprons. Bit 10 is internal (set per wave for strips inside
 // the image, see the end of the kernel).
-inline constexpr int kBandFullSeg = 16;  // the auto segment of a 4096^2 frame (edge_launch.hpp)
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,
@@ -1296,23 +1295,13 @@ __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves
     }
     // wave-uniform: odd segments walk up; strips wholly inside the image (every
     // strip when w % 256 == 0) skip the per-row clamp of lanes past w (OPT bit
-    // 10); 5-row windows over exactly kBandFullSeg rows (every segment of the
-    // 4096^2 flagship) run the fully unrolled walk — no loop-carried ring
-    // copies, every row's liveness and load policy compile-time
+    // 10). (A fully unrolled walk for the flagship's 16-row segments cut the
+    // loop-carried ring copies — 8.38M VALU per frame against 8.5M — but ran
+    // the burst 2-5 % slower: 20 KB of straight-line code per walk against a
+    // 5-row loop body; profiles/lab2_conv.md, round 6.)
     constexpr int OIN = (OPT & 512) ? OPT : (OPT | 1024);
     const bool inside = !(OPT & 512) && strip * SW + 256 <= w;
     const bool up = (alt & 1) && (sg & 1);
-    if constexpr (K == 5 && A == 2 && !(OPT & 8)) {
-        if (inside && ye - ys == kBandFullSeg) {
-            if (up)
-                band4_walk<K, A, MODE, FAST, F, true, OIN, false, kBandFullSeg>(in, out, w, pitch, ys, ye, y_lo, y_hi,
-                                                                                strip * SW, taps, rs);
-            else
-                band4_walk<K, A, MODE, FAST, F, false, OIN, false, kBandFullSeg>(in, out, w, pitch, ys, ye, y_lo, y_hi,
-                                                                                 strip * SW, taps, rs);
-            return;
-        }
-    }
     if (up) {
         if (inside)
             band4_walk<K, A, MODE, FAST, F, true, OIN>(in, out, w, pitch, ys, ye, y_lo, y_hi, strip * SW, taps, rs);

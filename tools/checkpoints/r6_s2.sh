@@ -40,5 +40,26 @@ g2)  # g1 plus a second bench and a kernel trace of the bench
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o trace -- \
         python3 "$R/bench.py" --steps 20 --warmup 5 > "$out/trace.log" 2>&1); echo "trace rc=$?"
     ;;
+ab)  # same-box A/B of the driver bench over library builds (cuda_mpi_openmp_amd/_lib/ab/libmpx_<v>.so;
+    # "new" = this tree), alternated: AB_VARIANTS="r6a mid new", AB_ROUNDS=3
+    for k in $(seq 1 ${AB_ROUNDS:-3}); do
+        for v in ${AB_VARIANTS:-r6a new}; do
+            if [ $v = new ]; then lib=$R/cuda_mpi_openmp_amd/_lib/libmpx.so; else lib=$R/cuda_mpi_openmp_amd/_lib/ab/libmpx_$v.so; fi
+            MPX_LIB_PATH=$lib timeout -k 10 200 python bench.py > "$out/bench_${v}_$k.log" 2>&1 \
+                || { tail -20 "$out/bench_${v}_$k.log"; exit 1; }
+            python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); c=d['steady_clocks'][0]; print(sys.argv[2], sys.argv[3], d['value'], d['value_sustained'], d['value_steady'], d['value_streaming'], d['value_warm_cache'], c.get('gfxclk_mhz'), c.get('power_w'))" "$out/bench_${v}_$k.log" $v $k
+        done
+    done
+    ;;
+final)  # smoke, the driver bench, and the per-kernel profile (prof_all) of the current tree
+    export O=$out
+    bash tools/gpu.sh smoke &&
+    bash tools/gpu.sh run bench 300 python bench.py --gpus 1 --steps 20 --warmup 5 &&
+    bash tools/gpu.sh profile kfinal -- python3 tools/prof_all.py &&
+    python tools/experiments/kprof_table.py "$O" > "$O/kernels_table.md" &&
+    python tools/pmc_median.py "$O"/kfinal.pmc* > "$O/medians.md" &&
+    python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
+    find "$O" -name "*.db" -delete && du -sh "$O"
+    ;;
 *) echo "unknown checkpoint $name"; exit 2 ;;
 esac
