@@ -327,7 +327,10 @@ def run(args) -> int:
             from cuda_mpi_openmp_amd.utils.clocks import key_fields
 
             ssam.stop()
-            mine = key_fields(ssam.summary(t_lo, t_hi, pad_ns=3_000_000))
+            # the windows last a few ms (K steps each): at 100 Hz they hold 0-1
+            # samples, so the record spans the last 100 ms of the settle load
+            # (the same rotated steps, back to back) plus the windows
+            mine = key_fields(ssam.summary(t_lo - 100_000_000, t_hi, pad_ns=3_000_000))
             mine.update(source=ssam.source, error=ssam.error)
         steady = {"wins": wins, "clocks": parallel.all_gather_object(mine, ctx)}
 
@@ -492,7 +495,7 @@ def run(args) -> int:
             rec["value_steady"] = _sig(pixels * len(w) / sum(w) / 1e9)
             rec["value_steady_windows"] = [_sig(pixels / x / 1e9) for x in w]
             rec["steady_ms"] = args.steady_ms
-            rec["steady_clocks"] = steady["clocks"]  # per rank: gfxclk / power medians over the windows
+            rec["steady_clocks"] = steady["clocks"]  # per rank: gfxclk / power medians, last 100 ms of load + windows
         if warm is not None:
             rec["value_warm_cache"] = _sig(pixels / warm / 1e9)
             rec["ms_per_step_warm_cache"] = round(warm * 1e3 / max(1, args.steps), 5)
