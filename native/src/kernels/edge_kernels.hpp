@@ -919,6 +919,11 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // edges the lane loads its edge PAIR ((0, 1) / (w-2, w-1)) and one per-lane
     // byte select per apron pixel makes it (p0, p0) / (p[w-1], p[w-1]).
     constexpr bool kDppApron = (OPT & (8 | 16 | 512)) == 0;
+    // OPT bit 11 (walks of at most 32 rows, the launcher checks): every apron
+    // of the walk in ONE load up front, luma once; row i's lanes 0 / 63 then
+    // fetch theirs with two ds_bpermute (the LDS crossbar, no VALU) — no
+    // per-row apron load, luma or edge select
+    constexpr bool BPA = kDppApron && (OPT & 2048) != 0;
     const bool fix_l = kDppApron && ap_left && x0 == 0, fix_r = kDppApron && ap_right && x0 + 256 >= w;
     // (fix_r: lane 63's quad offset cc = w - 4 plus 8 B, not (w - 2) * 4 — a w * 4
     // in a VGPR would turn the uniform descriptor-size selects into v_cndmasks)
@@ -960,6 +965,12 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             ap = u32x2_t{0u, 0u};
         } else if constexpr ((OPT & 8) != 0) {  // aprons come from the batch load
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, (OPT & 64) ? 2 : 0);
+        } else if constexpr (BPA) {  // aprons come from the batch load (bpermute form)
+            if ((OPT & 32) && i >= K - 1 && i < ye - ys)
+                q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 2);
+            else
+                q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 0);
+            ap = u32x2_t{0u, 0u};
         } else if ((OPT & 64) || ((OPT & 32) && i >= K - 1 && i < ye - ys)) {
             q = __builtin_amdgcn_raw_buffer_load_b128(rr, qo, 0, 2);
             ap = __builtin_amdgcn_raw_buffer_load_b64(rr, ao, 0, (OPT & 128) ? 0 : 2);
@@ -982,6 +993,18 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // j >> 1's left (j even) or right (j odd) apron as two luma values; row
     // i's consumer reads lanes 2i / 2i+1 with v_readlane (wave-uniform i).
     f2_t ab = {0.0f, 0.0f};
+    int bp_addr = 0;
+    if constexpr (BPA) {
+        const int nload = ye - ys + K - 1;  // <= 32
+        const int j = lane >> 1;
+        const bool side = lane & 1;  // 0: left apron (x0-2, x0-1), 1: right (x0+256, x0+257)
+        const bool edge = side ? x0 + 256 >= w : x0 == 0;
+        const int col = side ? (edge ? w - 2 : x0 + 256) : (edge ? 0 : x0 - 2);
+        const u32x2_t v = *reinterpret_cast<const u32x2_t *>(row_ptr(min(j, nload - 1)) + col);
+        // image edge: the edge pixel twice (clamp-to-edge)
+        ab = luma2((edge && side) ? v.y : v.x, (edge && !side) ? v.x : v.y);
+        bp_addr = ap_right ? 4 : 0;  // lane 63 reads lane 2i + 1 (right), the others lane 2i
+    }
     if constexpr ((OPT & 8) != 0) {
         const int nload = ye - ys + K - 1;  // <= 32, checked by the launcher
         const int j = lane >> 1, side = lane & 1;
@@ -1015,6 +1038,10 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
             const f2_t lft = {rl(ab.x, 2 * ri), rl(ab.y, 2 * ri)};
             const f2_t rgt = {rl(ab.x, 2 * ri + 1), rl(ab.y, 2 * ri + 1)};
             la = ap_left ? lft : rgt;
+        } else if constexpr (BPA) {
+            const int a = bp_addr + 8 * ri;
+            la = f2_t{__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(ab.x))),
+                      __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(ab.y)))};
         } else if constexpr (kDppApron) {
             la = luma2(__builtin_amdgcn_perm(ap.y, ap.x, ap_selx), __builtin_amdgcn_perm(ap.y, ap.x, ap_sely));
         } else {
@@ -1231,8 +1258,10 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
 // segment reads, bit 6 non-temporal loads of every row, bit 7 keeps the apron
 // loads plain under bit 5 / 6, bit 3 one batched apron load per walk (walks of
 // at most 32 rows: segment + K - 1 <= 32), bit 9 248-column strips with halo
-// lanes instead of aprons. Bit 10 is internal (set per wave for strips inside
-// the image, see the end of the kernel).
+// lanes instead of aprons, bit 11 batched aprons fetched per row by
+// ds_bpermute (walks of at most 32 rows; the production launch for segments
+// of at most 28 rows). Bit 10 is internal (set per wave for strips inside the
+// image, see the end of the kernel).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
 __global__ __launch_bounds__((OPT & 4) ? 1024 : 256) __attribute__((amdgpu_waves_per_eu((OPT & 1) ? 5 : 1))) void conv_band4_kernel(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                          int w, int pitch, int oy0, int oy1, int y_lo, int y_hi,

@@ -119,6 +119,12 @@ int launch_wave(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
 // (16-row segments) 30.1 us; 5 / 6 waves (13 / 11 rows, two rounds) 32.6 /
 // 32.1; 20 / 24 rows 34.9 / 32.2; no alternation 32.4.
 inline constexpr int kBand4PerSimd = 4;
+inline int band4_auto_seg(int w, int rows, bool hl = false, int per_simd = kBand4PerSimd) {
+    const int strips = hl ? (w + 247) / 248 : (w + 255) / 256;
+    const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
+    const int64_t work = (int64_t)rows * strips;
+    return (int)std::max<int64_t>(8, (work + slots - 1) / slots);
+}
 // SP: the fused streaming-halo form (mpx_conv_stream_peer_run; *sp required, its
 // n_edge filled in here).
 template <int K, int A, int MODE, bool FAST, class F, int OPT = 0, bool SP = false>
@@ -130,12 +136,8 @@ int launch_band4(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, i
     if (!rs.dn) rs.dn = in;
     if (rs.up != in || rs.dn != in || SP) alt |= 2;  // remote halo rows: boundary segments first
     const int strips = (OPT & 512) ? (w + 247) / 248 : (w + 255) / 256;
-    if (seg <= 0) {
-        const int64_t slots = (int64_t)kNumCUs * 4 * per_simd;
-        const int64_t work = (int64_t)(oy1 - oy0) * strips;
-        seg = (int)std::max<int64_t>(8, (work + slots - 1) / slots);
-    }
-    MPX_CHECK_ARG(!(OPT & 8) || seg + K - 1 <= 32, "batched aprons: walks of at most 32 rows");
+    if (seg <= 0) seg = band4_auto_seg(w, oy1 - oy0, (OPT & 512) != 0, per_simd);
+    MPX_CHECK_ARG(!(OPT & (8 | 2048)) || seg + K - 1 <= 32, "batched aprons: walks of at most 32 rows");
     const int segs = (oy1 - oy0 + seg - 1) / seg;
     const int64_t nwaves = (int64_t)strips * segs;
     MPX_CHECK_ARG(nwaves < ((int64_t)1 << 31) - 4, "image too large for one launch");
@@ -239,9 +241,16 @@ int launch_band(const uint32_t *in, uint32_t *out, int w, int pitch, int oy0, in
     }
     if (m == 1)
         return launch_band4<K, A, MODE, true, F, 0>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+    // walks of at most 32 rows (every segment of a 4096^2 frame: 16 + 4) take
+    // the batched aprons (OPT bit 11: one apron load and luma per walk, two
+    // ds_bpermute per row instead of a load, a luma and two selects)
+    const int seg = band4_auto_seg(w, oy1 - oy0);
+    const bool bpa = seg + K - 1 <= 32;
     if (m == 2 || tl_conv_resident)
-        return launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
-    return launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, 0, rs);
+        return bpa ? launch_band4<K, A, MODE, true, F, 2 | 2048>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, seg, rs)
+                   : launch_band4<K, A, MODE, true, F, 2>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, seg, rs);
+    return bpa ? launch_band4<K, A, MODE, true, F, 34 | 2048>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, seg, rs)
+               : launch_band4<K, A, MODE, true, F, 34>(in, out, w, pitch, oy0, oy1, y_lo, y_hi, taps, s, seg, rs);
 }
 
 // Named filters whose taps are compiled in (zero taps disappear); selected

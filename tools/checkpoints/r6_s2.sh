@@ -61,5 +61,16 @@ final)  # smoke, the driver bench, and the per-kernel profile (prof_all) of the 
     python tools/experiments/trace_db.py "$O/kfinal" --top 40 > "$O/trace.md" &&
     find "$O" -name "*.db" -delete && du -sh "$O"
     ;;
+g3)  # band-kernel change check: edge probe, lab2 GPU tests, VALU counters, then the bench A/B
+    PYTHONPATH=$R timeout -k 10 200 python -u tools/experiments/band_edge_probe.py > "$out/probe.log" 2>&1 \
+        || { tail -30 "$out/probe.log"; exit 1; }
+    tail -3 "$out/probe.log"
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+        tests/test_gpu_kernels.py tests/test_gpu_headline.py -m gpu > "$out/tests.log" 2>&1 \
+        || { tail -40 "$out/tests.log"; exit 1; }
+    tail -1 "$out/tests.log"
+    pmc valu SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS; echo "pmc rc=$?"
+    OUTNAME=$name AB_VARIANTS="${AB_VARIANTS:-r6a alp new}" bash "$0" ab
+    ;;
 *) echo "unknown checkpoint $name"; exit 2 ;;
 esac
