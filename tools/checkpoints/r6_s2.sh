@@ -72,5 +72,11 @@ g3)  # band-kernel change check: edge probe, lab2 GPU tests, VALU counters, then
     pmc valu SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS; echo "pmc rc=$?"
     OUTNAME=$name AB_VARIANTS="${AB_VARIANTS:-r6a alp new}" bash "$0" ab
     ;;
+multi)  # the driver's N-rank command rehearsed on one GPU (ranks share it), weak and strong
+    export O=$out
+    MPX_DIST_BACKEND=gloo bash tools/gpu.sh run drv2 300 python bench.py --gpus 2 --steps 20 --warmup 5 &&
+    MPX_DIST_BACKEND=gloo bash tools/gpu.sh run drv4s 300 python bench.py --gpus 4 --steps 20 --warmup 5 --layout strong
+    for f in "$O"/drv*.log; do echo "$f"; grep '^{' "$f" | tail -1 | cut -c1-420; done
+    ;;
 *) echo "unknown checkpoint $name"; exit 2 ;;
 esac
