@@ -912,8 +912,8 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // OPT bit 4 (cost probe only, wrong at strip edges): no apron loads
     const bool ap_have = !HL && !(OPT & 16) && ((ap_left && x0 > 0) || (ap_right && x0 + 256 < w));
     constexpr int kDrop = 0x7ffffff0;
-    // DPP-old apron (every production instance; the HL / batched / no-apron
-    // tuning probes keep the select form): lanes 0 / 63 feed their apron luma
+    // DPP-old apron (every production instance; the HL / readlane-batched
+    // (bit 3) / no-apron tuning probes keep the select form): lanes 0 / 63 feed their apron luma
     // as the `old` operand of the wave-shift DPP moves, the only lanes whose
     // shift has no source lane — no v_cndmask per window value. At the image
     // edges the lane loads its edge PAIR ((0, 1) / (w-2, w-1)) and one per-lane
@@ -922,8 +922,9 @@ __device__ __forceinline__ void band4_walk(const uint32_t *__restrict__ in, uint
     // OPT bit 11 (walks of at most 32 rows, the launcher checks): every apron
     // of the walk in ONE load up front, luma once; row i's lanes 0 / 63 then
     // fetch theirs with two ds_bpermute (the LDS crossbar, no VALU) — no
-    // per-row apron load, luma or edge select
-    constexpr bool BPA = kDppApron && (OPT & 2048) != 0;
+    // per-row apron load, luma or edge select. Not for the fused streaming
+    // halo's edge walks (SPW): their mailbox rows need system-scope loads
+    constexpr bool BPA = kDppApron && (OPT & 2048) != 0 && !SPW;
     const bool fix_l = kDppApron && ap_left && x0 == 0, fix_r = kDppApron && ap_right && x0 + 256 >= w;
     // (fix_r: lane 63's quad offset cc = w - 4 plus 8 B, not (w - 2) * 4 — a w * 4
     // in a VGPR would turn the uniform descriptor-size selects into v_cndmasks)
