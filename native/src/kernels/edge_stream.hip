@@ -26,8 +26,14 @@ template <int K, int A, int MODE, class F>
 int run_sp(const uint32_t *in, uint32_t *out, int w, int pitch, int own_rows, int y_lo, int y_hi, const Taps &taps,
            hipStream_t s, const edge::RowSrc &rs, mpx_conv_stream_peer *sp) {
     // the production band launch (NT stores, NT loads of the rows no neighbouring
-    // segment re-reads: OPT 34), auto segments
-    return edgel::launch_band4<K, A, MODE, true, F, 34, true>(in, out, w, pitch, 0, own_rows, y_lo, y_hi, taps, s, 0,
+    // segment re-reads: OPT 34), auto segments; walks of at most 32 rows take
+    // the batched aprons (bit 11) in their interior waves — the edge waves,
+    // whose mailbox rows need system-scope loads, keep the per-row aprons
+    const int seg = edgel::band4_auto_seg(w, own_rows);
+    if (seg + K - 1 <= 32)
+        return edgel::launch_band4<K, A, MODE, true, F, 34 | 2048, true>(in, out, w, pitch, 0, own_rows, y_lo, y_hi, taps,
+                                                                          s, seg, rs, edgel::kBand4PerSimd, 1, sp);
+    return edgel::launch_band4<K, A, MODE, true, F, 34, true>(in, out, w, pitch, 0, own_rows, y_lo, y_hi, taps, s, seg,
                                                                rs, edgel::kBand4PerSimd, 1, sp);
 }
 
